@@ -1,0 +1,272 @@
+#!/usr/bin/env python3
+"""bench.py -- device-resident batched TCP checksum on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4]
+
+A step = one pass of the hot path (one tcpck_batch_* CHECKSUM launch) over one
+batch of synthetic segments already resident in HBM.  Default workload (N=1)
+is BASELINE.json configs[1] (C2): 1,048,576 segments with a 1460-B Ethernet-MSS
+payload = 1492-B checksummed images (32-B pseudo+TCP header + payload,
+SURVEY.md fact 3), fixed stride.  With N>1 GPUs (one process per GPU via
+torch.distributed.run) every rank checksums its own 1M-image shard
+(first_index = rank * count, shard-reproducible generator), no data-path
+collective: at N=8 this is configs[4] (C5, 8M segments over 8 GPUs), weak
+scaling.  Rank 0 prints ONE JSON line with the driver's fields plus:
+
+  roofline      dominant kernel vs the HBM-read roof (8.0 TB/s): achieved =
+                algorithmic bytes per launch (sum of image bytes + 2 B written
+                per image) / average launch time from HIP events on the launch
+                stream; traffic = PMC HBM bytes per launch from the committed
+                rocprofv3 pass (profiles/pmc_summary.json), else null
+  cpu_baseline  the reference's own CalculateChecksum (oracle/_ref, built from
+                /root/reference/include/tcp-header.h) on the host cores, on a
+                bounded sample of the same images (rank 0, N=1 only); falls back
+                to the in-repo C restatement ("port") where oracle/_ref is absent
+  e2e           host-memory rate incl. pinned hipMemcpyAsync H2D + D2H (not `value`)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "tcp-stack_amd"))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+METRIC = "GiB/s device-resident TCP checksum over batched segments; % HBM roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md (spec 8.0 TB/s)
+GIB = float(1 << 30)
+
+CONFIGS = {
+    # name: (description, kind, count, image bytes)
+    "c2": ("C2: 1M x 1460-B payload (1492-B images), fixed stride, device-resident", "fixed", 1 << 20, 1492),
+    "c3": ("C3: 4M images, payload uniform over {64,576,1460} B (96/608/1492-B images), packed, u64 offsets",
+           "mixed", 4 << 20, None),
+    "c4": ("C4: 256K x 64-KiB jumbo images (payload 65504), fixed stride", "fixed", 256 << 10, 65536),
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline time budget")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-e2e", action="store_true")
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    import tcpck
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    desc, kind, count, L = CONFIGS[args.config]
+    ctx = tcpck.Context(local)
+    stream = torch.cuda.current_stream()
+    first = rank * count
+    if kind == "fixed":
+        arena = torch.empty(count * L, dtype=torch.uint8, device="cuda")
+        tcpck.synth_fixed(arena, L, L, count, seed=42, first_index=first, stream=stream)
+        img_bytes = count * L
+
+        def step(out):
+            ctx.batch_fixed(tcpck.OP_CHECKSUM, arena, L, L, count, out, stream=stream)
+    else:
+        from synth_np import mixed_layout
+        off, ln, total = mixed_layout(count, seed=42 + rank)
+        arena = torch.empty(total, dtype=torch.uint8, device="cuda")
+        d_off = torch.from_numpy(off).cuda()
+        d_ln = torch.from_numpy(ln).cuda()
+        tcpck.synth_var(arena, d_off, d_ln, 1492, count, seed=42, first_index=first, stream=stream)
+        img_bytes = int(ln.astype(np.int64).sum())
+
+        def step(out):
+            ctx.batch_var(tcpck.OP_CHECKSUM, arena, d_off, d_ln, count, out, total_bytes=img_bytes,
+                          min_len=int(ln.min()), max_len=int(ln.max()), packed=True, stream=stream)
+    out = torch.empty(count, dtype=torch.int16, device="cuda")
+    torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        step(out)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        starts[i].record(stream)
+        step(out)
+        ends[i].record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    launch_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts, ends)]))
+
+    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    tmax = float(t.item())
+    total_bytes = img_bytes * world * args.steps
+    value = total_bytes / tmax / GIB
+
+    # Checksum digest of this rank's results (parity spot-check on the host below).
+    res = out.cpu().numpy().view(np.uint16)
+
+    if rank != 0:
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+
+    algo_bytes = img_bytes + 2 * count  # per launch: image bytes read + 2 B written per image
+    achieved = algo_bytes / (launch_ms * 1e-3) / 1e9
+    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(args.config),
+                "algorithmic_bytes_per_launch": algo_bytes, "avg_launch_ms": round(launch_ms, 5)}
+
+    rec = {
+        "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(tmax / args.steps * 1e3, 5),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u16",
+        "data": "synthetic (device-generated: send-path headers + splitmix64 payloads, seed 42)",
+        "config": {"workload": desc, "images_per_gpu": count, "image_bytes": L if L else "96/608/1492",
+                   "bytes_per_gpu": img_bytes, "parallelism": f"shard{world} (independent per-GPU batches, no collective)"},
+        "roofline": roofline,
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        rec["cpu_baseline"] = cpu_baseline(arena, res, kind, count, L, args.cpu_seconds,
+                                           None if kind == "fixed" else (off, ln))
+    if world == 1 and not args.no_e2e and kind == "fixed":
+        rec["e2e"] = e2e_rate(ctx, arena, res, count, L)
+    print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def pmc_traffic(config: str):
+    """HBM bytes per launch from the committed rocprofv3 PMC pass, if one exists."""
+    p = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        return d[config]["hbm_bytes_per_launch"]
+    except (OSError, KeyError, ValueError):
+        return None
+
+
+def cpu_threads() -> int:
+    n = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    if n <= 0:
+        n = os.cpu_count() or 1
+    return max(1, min(n, 16))
+
+
+def cpu_baseline(arena, gpu_res, kind, count, L, budget_s, var_layout):
+    """Reference CalculateChecksum on host cores over a bounded sample of the same images."""
+    from oracle import ref16 as R
+    nthr = cpu_threads()
+    if kind == "fixed":
+        n = min(count, max(1, (256 << 20) // L))
+        sample = arena[: n * L].cpu().numpy()
+        sargs = dict(stride=L, length=L, count=n)
+        sbytes = n * L
+        sdesc = f"first {n} of the batch's {L}-B images ({sbytes / 1e6:.0f} MB), repeated"
+    else:
+        off, ln = var_layout
+        n = min(count, 1 << 18)
+        end = int(off[n - 1] + ln[n - 1])
+        sample = arena[:end].cpu().numpy()
+        sargs = dict(offsets=off[:n], lengths=ln[:n])
+        sbytes = int(ln[:n].astype(np.int64).sum())
+        sdesc = f"first {n} images of the batch ({sbytes / 1e6:.0f} MB), repeated"
+    if R.RefLib.available("O3"):
+        ref, kind_s = R.RefLib("O3"), "reference"
+        run = lambda: ref.timed_batch(sample, threads=nthr, **sargs)
+    else:
+        c = R.Ref16C(build=False)
+        kind_s = "port"
+
+        def run():
+            t0 = time.perf_counter()
+            r = c.batch(sample, threads=nthr, **sargs)
+            return r, time.perf_counter() - t0
+    got, _ = run()
+    match = bool(np.array_equal(got, gpu_res[:n]))
+    secs, reps = 0.0, 0
+    while secs < budget_s and reps < 10000:
+        _, s = run()
+        secs += s
+        reps += 1
+    rate = sbytes * reps / secs / GIB
+    out = {"value": round(rate, 2), "unit": "GiB/s", "cores": nthr, "kind": kind_s,
+           "sample": sdesc + f" x{reps} ({secs:.1f} s); CalculateChecksum built -O3 -march=x86-64-v3; "
+                             f"results == GPU results: {match}"}
+    if R.RefLib.available("O0"):
+        # secondary: the reference as its makefile builds it (-O0 -g, makefile:2), 1 thread
+        ref0 = R.RefLib("O0")
+        m = min(n, 20000)
+        kw = dict(sargs)
+        if "count" in kw:
+            kw["count"] = m
+        else:
+            kw["offsets"], kw["lengths"] = kw["offsets"][:m], kw["lengths"][:m]
+        _, s0 = ref0.timed_batch(sample, threads=1, **kw)
+        b0 = m * L if L else int(kw["lengths"].astype(np.int64).sum())
+        out["reference_O0_1thread_GiBs"] = round(b0 / s0 / GIB, 3)
+    try:
+        out["cpu_model"] = open("/proc/cpuinfo").read().split("model name")[1].split("\n")[0].strip(": \t")
+    except Exception:
+        pass
+    return out
+
+
+def e2e_rate(ctx, arena, gpu_res, count, L):
+    """Host (pinned) -> GPU -> host rate of the same batch through tcpck_host_batch_fixed."""
+    import torch
+    import tcpck
+    h = torch.empty(count * L, dtype=torch.uint8).pin_memory()
+    h.copy_(arena.cpu())
+    hout = torch.empty(count, dtype=torch.int16).pin_memory()
+    ctx.set_chunk_bytes(64 << 20)
+    ctx.host_batch_fixed(tcpck.OP_CHECKSUM, h, L, L, count, hout)  # warm (staging alloc)
+    reps = 3
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        ctx.host_batch_fixed(tcpck.OP_CHECKSUM, h, L, L, count, hout)
+    dt = (time.perf_counter() - t0) / reps
+    ok = bool(np.array_equal(hout.numpy().view(np.uint16), gpu_res))
+    return {"value": round(count * L / dt / GIB, 2), "unit": "GiB/s",
+            "what": "pinned host arena -> 64 MiB chunks H2D on 2 streams -> kernel -> u16 results D2H",
+            "results_match_device_path": ok}
+
+
+if __name__ == "__main__":
+    main()

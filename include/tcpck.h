@@ -1,0 +1,162 @@
+/*
+ * tcpck.h -- C-ABI of the MI355X (gfx950) TCP checksum library, libtcpck.so.
+ *
+ * Drop-in boundary for the one per-byte hot path of filixi/TCP-stack:
+ *
+ *   friend uint16_t CalculateChecksum(const TcpPacket &)   include/tcp-header.h:252-263
+ *
+ * and its three call sites:
+ *
+ *   send, insert   src/socket-manager.cc:9-10, include/socket-manager.h:259-260
+ *                  (zero TcpHeader::Checksum(), compute, store raw)
+ *   receive,verify include/socket-manager.h:182   (CalculateChecksum(pkt) == 0)
+ *
+ * Plain pointers and sizes only.  Every entry point returns an int status
+ * (TCPCK_OK = 0, negative on error) and never throws.  The reference has no
+ * error path (odd sizes are an out-of-bounds read, tcp-header.h:259-260); here
+ * odd lengths are rejected with TCPCK_EINVAL where the host can see them, and
+ * documented as a precondition for device-resident descriptor arrays.
+ *
+ * Arithmetic (mode TCPCK_MODE_REF, the default and the parity mode):
+ *     checksum = ~(sum of little-endian u16 words of the image mod 2^16) & 0xFFFF
+ * i.e. the reference's u32 accumulation with no end-around-carry fold.  The
+ * opt-in TCPCK_MODE_RFC1071 folds carries (one's complement, RFC 1071); it is
+ * NOT what the reference computes.
+ *
+ * An "image" is the 32-byte TcpHeader (12-byte pseudo-header + 20-byte TCP
+ * header, tcp-header.h:188-190) followed by the payload, contiguous, exactly the
+ * bytes of TcpPacket::GetBuffer() (tcp-header.h:265-267).  The checksum field is
+ * bytes 28-29 (TcpHeader::Checksum(), tcp-header.h:177), stored raw (host order,
+ * no htons), as the reference does.
+ */
+#ifndef TCPCK_H_
+#define TCPCK_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TCPCK_ABI_VERSION 1
+
+/* ---- status codes ------------------------------------------------------ */
+#define TCPCK_OK 0
+#define TCPCK_EINVAL (-22)   /* bad argument: odd length/offset, null, overflow */
+#define TCPCK_ENOMEM (-12)   /* host or device allocation failed               */
+#define TCPCK_ENODEV (-19)   /* no such HIP device                             */
+#define TCPCK_EHIP (-1000)   /* HIP runtime error e: returned as TCPCK_EHIP - e */
+
+/* ---- arithmetic modes --------------------------------------------------- */
+#define TCPCK_MODE_REF 0     /* bit-exact to tcp-header.h:252-263 (mod 2^16)   */
+#define TCPCK_MODE_RFC1071 1 /* opt-in one's complement, end-around carry      */
+
+/* ---- batch operations --------------------------------------------------- */
+#define TCPCK_OP_CHECKSUM 0  /* out[k] (u16) = checksum of image k              */
+#define TCPCK_OP_FILL 1      /* zero bytes 28-29 of image k, compute, store the
+                                result there in place (send path); out[k] (u16)
+                                also receives it unless out == NULL.  len >= 30 */
+#define TCPCK_OP_VERIFY 2    /* out[k] (u8) = (checksum of image k == 0)
+                                (receive path, socket-manager.h:182)            */
+
+/* ---- layout hints (tcpck_layout.flags) ---------------------------------- */
+#define TCPCK_LAYOUT_PACKED 1u /* images are back to back in index order:
+                                  offsets[k+1] == offsets[k] + lengths[k]      */
+
+/* Optional description of a variable-length batch.  Zero fields = unknown.
+ * Used only to choose a kernel; a wrong hint never changes results, except
+ * that TCPCK_LAYOUT_PACKED must be true when set. */
+typedef struct tcpck_layout {
+  uint64_t total_bytes; /* sum of lengths                                     */
+  uint32_t min_len;     /* smallest image length                              */
+  uint32_t max_len;     /* largest image length                               */
+  uint32_t flags;       /* TCPCK_LAYOUT_*                                     */
+  uint32_t reserved;
+} tcpck_layout;
+
+typedef struct tcpck_ctx tcpck_ctx;
+typedef void *tcpck_stream; /* a hipStream_t; NULL = the device's null stream */
+
+/* ---- library ------------------------------------------------------------ */
+int tcpck_abi_version(void);
+const char *tcpck_strerror(int status);
+/* 1 when the library's gfx950 code object can run on `device`, else 0. */
+int tcpck_device_supported(int device);
+
+/* ---- context: one per device; owns no hidden global HIP state ------------ */
+int tcpck_ctx_create(int device, tcpck_ctx **out);
+int tcpck_ctx_destroy(tcpck_ctx *ctx);
+int tcpck_ctx_device(const tcpck_ctx *ctx);
+
+/* ---- single image, host memory (the per-packet drop-in) ------------------
+ * Replaces CalculateChecksum(const TcpPacket&) (tcp-header.h:252-263) for one
+ * packet at a time: one image is far below a kernel launch in cost, so it is
+ * computed on the calling thread.  Reentrant, no allocation. */
+int tcpck_checksum16(const void *image, size_t len, int mode, uint16_t *out);
+/* Send-side insertion on one host image (socket-manager.cc:9-10). */
+int tcpck_fill16(void *image, size_t len, int mode, uint16_t *out);
+/* Incremental update of a stored checksum when one aligned u16 word of the
+ * image changes from old_word to new_word (retransmit ACK rewrite,
+ * socket-internal.h:376-377), exact in the selected mode. */
+uint16_t tcpck_update16(uint16_t checksum, uint16_t old_word, uint16_t new_word, int mode);
+
+/* ---- batched, device-resident: the hot path ------------------------------
+ * Fixed stride: image k is d_arena[k*stride, k*stride + len).
+ * stride and len even (stride >= len); count images.
+ * d_out: u16[count] (CHECKSUM/FILL) or u8[count] (VERIFY).
+ * Asynchronous on `stream`; nothing is allocated; no host synchronisation. */
+int tcpck_batch_fixed(tcpck_ctx *ctx, int op, int mode, void *d_arena,
+                      uint64_t stride, uint32_t len, uint64_t count, void *d_out,
+                      tcpck_stream stream);
+
+/* Variable length: image k is d_arena[d_offsets[k], d_offsets[k] + d_lengths[k]).
+ * Offsets and lengths must be even (precondition: the device arrays are not
+ * read by the host).  `layout` may be NULL. */
+int tcpck_batch_var(tcpck_ctx *ctx, int op, int mode, void *d_arena,
+                    const uint64_t *d_offsets, const uint32_t *d_lengths,
+                    uint64_t count, void *d_out, const tcpck_layout *layout,
+                    tcpck_stream stream);
+
+/* ---- batched, host memory (end to end incl. PCIe) ------------------------
+ * Segments start and end in host memory (the loopback/socket buffers of
+ * network-service.cc / tcp-buffer.h).  The batch is split into chunks that are
+ * streamed H2D -> kernel -> D2H on two ctx-owned HIP streams with ctx-owned
+ * device staging buffers.  Synchronous: returns when h_out (and, for FILL,
+ * h_arena) hold the results.  Host buffers should be pinned
+ * (tcpck_host_alloc) for full PCIe rate.  offsets/lengths are host arrays. */
+int tcpck_host_batch_fixed(tcpck_ctx *ctx, int op, int mode, void *h_arena,
+                           uint64_t stride, uint32_t len, uint64_t count,
+                           void *h_out);
+int tcpck_host_batch_var(tcpck_ctx *ctx, int op, int mode, void *h_arena,
+                         const uint64_t *h_offsets, const uint32_t *h_lengths,
+                         uint64_t count, void *h_out);
+/* Bytes of device staging per chunk used by the host batch functions. */
+int tcpck_ctx_set_chunk_bytes(tcpck_ctx *ctx, uint64_t bytes);
+
+/* ---- memory helpers (for C/C++ callers without another allocator) -------- */
+int tcpck_host_alloc(size_t bytes, void **out);   /* pinned host memory   */
+int tcpck_host_free(void *p);
+int tcpck_device_alloc(tcpck_ctx *ctx, size_t bytes, void **out);
+int tcpck_device_free(tcpck_ctx *ctx, void *p);
+int tcpck_memcpy_h2d(tcpck_ctx *ctx, void *dst, const void *src, size_t bytes);
+int tcpck_memcpy_d2h(tcpck_ctx *ctx, void *dst, const void *src, size_t bytes);
+int tcpck_stream_sync(tcpck_ctx *ctx, tcpck_stream stream);
+
+/* ---- synthetic workload generator (benchmarks/tests; not the hot path) ----
+ * Writes images with the send path's 32-byte header (127.0.0.1:15500 ->
+ * 127.0.0.1:15501, PTCL 6, TcpLength = payload, seq = 1000 + index, ACK,
+ * window 1024, network order, checksum 0) and a payload drawn from splitmix64
+ * keyed by (seed, first_index + k) -- any shard is reproducible on its own.
+ * kind: 0 random payload, 1 all-zero payload, 2 all-0xFF payload. */
+int tcpck_synth_fixed(void *d_arena, uint64_t stride, uint32_t len, uint64_t count,
+                      uint64_t seed, uint64_t first_index, int kind, tcpck_stream stream);
+int tcpck_synth_var(void *d_arena, const uint64_t *d_offsets, const uint32_t *d_lengths,
+                    uint32_t max_len, uint64_t count, uint64_t seed, uint64_t first_index,
+                    int kind, tcpck_stream stream);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+
+#endif /* TCPCK_H_ */

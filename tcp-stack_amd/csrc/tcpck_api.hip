@@ -1,0 +1,462 @@
+// tcpck_api.hip -- the C-ABI of libtcpck.so (declared in include/tcpck.h).
+//
+// Replaces, for batches, the reference's per-packet checksum
+// (filixi/TCP-stack include/tcp-header.h:252-263) at its call sites
+// src/socket-manager.cc:9-10, include/socket-manager.h:259-260 (send: insert)
+// and include/socket-manager.h:182 (receive: verify).  See include/tcpck.h.
+//
+// Ownership and threading: callers own every buffer; the hot
+// batch calls allocate nothing and only enqueue work on the caller's stream;
+// the current HIP device of the calling thread is saved and restored around
+// every call (no hidden global device state).  The host-batch (end-to-end)
+// calls use ctx-owned streams and staging and are serialised per ctx.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <vector>
+
+#include "tcpck.h"
+#include "tcpck_internal.h"
+
+using tcpck::SegArgs;
+
+struct tcpck_ctx {
+  int device = 0;
+  int num_cus = 256;
+  uint32_t max_blocks = 2048;  // resident 256-thread blocks (8 per CU at <=64 VGPRs)
+  // end-to-end (host batch) pipeline state, created lazily
+  std::mutex mu;
+  hipStream_t s[2] = {nullptr, nullptr};
+  uint8_t *stage[2] = {nullptr, nullptr};     // image bytes
+  uint8_t *stage_out[2] = {nullptr, nullptr}; // results
+  uint64_t *stage_off[2] = {nullptr, nullptr};
+  uint32_t *stage_len[2] = {nullptr, nullptr};
+  uint64_t stage_bytes = 0;
+  uint64_t stage_images = 0;
+  uint64_t chunk_bytes = 64ull << 20;
+};
+
+namespace {
+
+int hip_status(hipError_t e) { return e == hipSuccess ? TCPCK_OK : TCPCK_EHIP - static_cast<int>(e); }
+
+// Saves the calling thread's current device, switches to ctx->device, restores.
+class DeviceGuard {
+ public:
+  explicit DeviceGuard(int device) {
+    if (hipGetDevice(&prev_) != hipSuccess) prev_ = -1;
+    if (prev_ != device) ok_ = hipSetDevice(device);
+  }
+  ~DeviceGuard() {
+    if (prev_ >= 0) (void)hipSetDevice(prev_);
+  }
+  hipError_t status() const { return ok_; }
+  DeviceGuard(const DeviceGuard &) = delete;
+  DeviceGuard &operator=(const DeviceGuard &) = delete;
+
+ private:
+  int prev_ = -1;
+  hipError_t ok_ = hipSuccess;
+};
+
+size_t out_elem(int op) { return op == TCPCK_OP_VERIFY ? 1 : 2; }
+
+bool valid_op_mode(int op, int mode) {
+  return (op == TCPCK_OP_CHECKSUM || op == TCPCK_OP_FILL || op == TCPCK_OP_VERIFY) &&
+         (mode == TCPCK_MODE_REF || mode == TCPCK_MODE_RFC1071);
+}
+
+// ---- host single-image path (product code, not the oracle) ---------------
+// SWAR over 8-byte words: the two u16 halves of each 32-bit lane are split
+// into 0x0000FFFF0000FFFF lanes and summed in u64; 2^14 iterations cannot
+// overflow a 32-bit lane (2^14 * 2 * 0xFFFF < 2^32), so lanes are folded every
+// 2^14 words into an exact u64 total.  Returns the exact sum of the LE u16
+// words (REF needs it mod 2^16, RFC 1071 mod 0xFFFF with zero-ness).
+uint64_t host_word_sum(const uint8_t *p, size_t n) {
+  constexpr uint64_t kLo = 0x0000FFFF0000FFFFull;
+  uint64_t total = 0;
+  size_t i = 0;
+  while (n - i >= 8) {
+    uint64_t a = 0;
+    const size_t stop = i + std::min<size_t>((n - i) & ~size_t{7}, size_t{8} << 14);
+    for (; i < stop; i += 8) {
+      uint64_t x;
+      std::memcpy(&x, p + i, 8);
+      a += (x & kLo) + ((x >> 16) & kLo);
+    }
+    total += (a & 0xFFFFFFFFull) + (a >> 32);
+  }
+  for (; i + 1 < n; i += 2) {
+    uint16_t w;
+    std::memcpy(&w, p + i, 2);
+    total += w;
+  }
+  return total;
+}
+
+uint16_t finish_host(uint64_t total, int mode) {
+  if (mode == TCPCK_MODE_REF) return static_cast<uint16_t>(~total);  // tcp-header.h:262
+  while (total >> 16) total = (total & 0xFFFF) + (total >> 16);
+  return static_cast<uint16_t>(~total);
+}
+
+int ensure_stage(tcpck_ctx *ctx, uint64_t bytes, uint64_t images) {
+  if (!ctx->s[0]) {
+    for (int i = 0; i < 2; ++i) {
+      hipError_t e = hipStreamCreateWithFlags(&ctx->s[i], hipStreamNonBlocking);
+      if (e != hipSuccess) return hip_status(e);
+    }
+  }
+  if (bytes > ctx->stage_bytes) {
+    for (int i = 0; i < 2; ++i) {
+      if (ctx->stage[i]) (void)hipFree(ctx->stage[i]);
+      ctx->stage[i] = nullptr;
+      hipError_t e = hipMalloc(&ctx->stage[i], bytes + 16);
+      if (e != hipSuccess) return TCPCK_ENOMEM;
+    }
+    ctx->stage_bytes = bytes;
+  }
+  if (images > ctx->stage_images) {
+    for (int i = 0; i < 2; ++i) {
+      if (ctx->stage_out[i]) (void)hipFree(ctx->stage_out[i]);
+      if (ctx->stage_off[i]) (void)hipFree(ctx->stage_off[i]);
+      if (ctx->stage_len[i]) (void)hipFree(ctx->stage_len[i]);
+      ctx->stage_out[i] = nullptr;
+      ctx->stage_off[i] = nullptr;
+      ctx->stage_len[i] = nullptr;
+      if (hipMalloc(&ctx->stage_out[i], images * 2) != hipSuccess ||
+          hipMalloc(&ctx->stage_off[i], images * 8) != hipSuccess ||
+          hipMalloc(&ctx->stage_len[i], images * 4) != hipSuccess)
+        return TCPCK_ENOMEM;
+    }
+    ctx->stage_images = images;
+  }
+  return TCPCK_OK;
+}
+
+void free_stage(tcpck_ctx *ctx) {
+  for (int i = 0; i < 2; ++i) {
+    if (ctx->stage[i]) (void)hipFree(ctx->stage[i]);
+    if (ctx->stage_out[i]) (void)hipFree(ctx->stage_out[i]);
+    if (ctx->stage_off[i]) (void)hipFree(ctx->stage_off[i]);
+    if (ctx->stage_len[i]) (void)hipFree(ctx->stage_len[i]);
+    if (ctx->s[i]) (void)hipStreamDestroy(ctx->s[i]);
+  }
+}
+
+// Patches bytes 28-29 of host images after a FILL computed on the device
+// (the device filled its staging copy; the host image is the caller's).
+void patch_fields(uint8_t *arena, uint64_t k0, uint64_t n, const uint16_t *res,
+                  const uint64_t *off, const uint32_t *len, uint64_t stride, uint32_t flen) {
+  for (uint64_t k = 0; k < n; ++k) {
+    const uint64_t o = off ? off[k0 + k] : (k0 + k) * stride;
+    const uint32_t l = len ? len[k0 + k] : flen;
+    if (l >= 30) std::memcpy(arena + o + 28, &res[k], 2);
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int tcpck_abi_version(void) { return TCPCK_ABI_VERSION; }
+
+const char *tcpck_strerror(int status) {
+  if (status == TCPCK_OK) return "ok";
+  if (status == TCPCK_EINVAL) return "invalid argument (odd length/offset, null pointer, overflow)";
+  if (status == TCPCK_ENOMEM) return "out of memory";
+  if (status == TCPCK_ENODEV) return "no such HIP device";
+  if (status <= TCPCK_EHIP) return hipGetErrorString(static_cast<hipError_t>(TCPCK_EHIP - status));
+  return "unknown status";
+}
+
+int tcpck_device_supported(int device) {
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return 0;
+  return std::strncmp(prop.gcnArchName, "gfx950", 6) == 0 ? 1 : 0;
+}
+
+int tcpck_ctx_create(int device, tcpck_ctx **out) {
+  if (!out) return TCPCK_EINVAL;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return TCPCK_ENODEV;
+  if (!tcpck_device_supported(device)) return TCPCK_ENODEV;  // gfx950 code object only
+  auto *ctx = new (std::nothrow) tcpck_ctx;
+  if (!ctx) return TCPCK_ENOMEM;
+  ctx->device = device;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+    ctx->num_cus = prop.multiProcessorCount;
+  ctx->max_blocks = static_cast<uint32_t>(ctx->num_cus) * 8u;
+  *out = ctx;
+  return TCPCK_OK;
+}
+
+int tcpck_ctx_destroy(tcpck_ctx *ctx) {
+  if (!ctx) return TCPCK_EINVAL;
+  {
+    DeviceGuard g(ctx->device);
+    free_stage(ctx);
+  }
+  delete ctx;
+  return TCPCK_OK;
+}
+
+int tcpck_ctx_device(const tcpck_ctx *ctx) { return ctx ? ctx->device : TCPCK_EINVAL; }
+
+int tcpck_ctx_set_chunk_bytes(tcpck_ctx *ctx, uint64_t bytes) {
+  if (!ctx || bytes < 4096) return TCPCK_EINVAL;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  ctx->chunk_bytes = bytes;
+  return TCPCK_OK;
+}
+
+// ---- single image, host ----------------------------------------------------
+int tcpck_checksum16(const void *image, size_t len, int mode, uint16_t *out) {
+  if ((!image && len) || !out || (len & 1) ||
+      (mode != TCPCK_MODE_REF && mode != TCPCK_MODE_RFC1071))
+    return TCPCK_EINVAL;
+  *out = finish_host(host_word_sum(static_cast<const uint8_t *>(image), len), mode);
+  return TCPCK_OK;
+}
+
+int tcpck_fill16(void *image, size_t len, int mode, uint16_t *out) {
+  if (!image || len < 30 || (len & 1)) return TCPCK_EINVAL;
+  auto *b = static_cast<uint8_t *>(image);
+  b[28] = 0;  // socket-manager.cc:9
+  b[29] = 0;
+  uint16_t c;
+  int rc = tcpck_checksum16(image, len, mode, &c);  // socket-manager.cc:10
+  if (rc) return rc;
+  std::memcpy(b + 28, &c, 2);
+  if (out) *out = c;
+  return TCPCK_OK;
+}
+
+uint16_t tcpck_update16(uint16_t checksum, uint16_t old_word, uint16_t new_word, int mode) {
+  if (mode == TCPCK_MODE_REF) {
+    // stored C = ~S (mod 2^16)  =>  C' = ~(S - old + new)
+    const uint16_t s = static_cast<uint16_t>(~checksum);
+    return static_cast<uint16_t>(~static_cast<uint16_t>(s - old_word + new_word));
+  }
+  // RFC 1624 eqn. 3: C' = ~(~C + ~m + m') in one's complement arithmetic.
+  uint32_t s = static_cast<uint16_t>(~checksum) + static_cast<uint32_t>(static_cast<uint16_t>(~old_word)) +
+               new_word;
+  s = (s & 0xFFFF) + (s >> 16);
+  s = (s & 0xFFFF) + (s >> 16);
+  if (s == 0) s = 0xFFFF;  // a real (non-all-zero) image never folds to +0
+  return static_cast<uint16_t>(~s);
+}
+
+// ---- batched, device-resident -------------------------------------------------
+int tcpck_batch_fixed(tcpck_ctx *ctx, int op, int mode, void *d_arena, uint64_t stride,
+                      uint32_t len, uint64_t count, void *d_out, tcpck_stream stream) {
+  if (!ctx || !valid_op_mode(op, mode)) return TCPCK_EINVAL;
+  if (count == 0) return TCPCK_OK;
+  if (!d_arena || (len & 1) || (stride & 1) || (count > 1 && stride < len)) return TCPCK_EINVAL;
+  if (!d_out && op != TCPCK_OP_FILL) return TCPCK_EINVAL;
+  if (op == TCPCK_OP_FILL && len < 30) return TCPCK_EINVAL;
+  if (count > 1 && stride > (UINT64_MAX - len) / (count - 1)) return TCPCK_EINVAL;
+  DeviceGuard g(ctx->device);
+  if (g.status() != hipSuccess) return hip_status(g.status());
+  SegArgs a{};
+  a.arena = static_cast<uint8_t *>(d_arena);
+  a.stride = stride;
+  a.len = len;
+  a.count = count;
+  a.out = d_out;
+  return hip_status(tcpck::launch_seg(op, mode, true, tcpck::shape_for_len(len), a, ctx->max_blocks,
+                                      static_cast<hipStream_t>(stream)));
+}
+
+int tcpck_batch_var(tcpck_ctx *ctx, int op, int mode, void *d_arena, const uint64_t *d_offsets,
+                    const uint32_t *d_lengths, uint64_t count, void *d_out,
+                    const tcpck_layout *layout, tcpck_stream stream) {
+  if (!ctx || !valid_op_mode(op, mode)) return TCPCK_EINVAL;
+  if (count == 0) return TCPCK_OK;
+  if (!d_arena || !d_offsets || !d_lengths) return TCPCK_EINVAL;
+  if (!d_out && op != TCPCK_OP_FILL) return TCPCK_EINVAL;
+  DeviceGuard g(ctx->device);
+  if (g.status() != hipSuccess) return hip_status(g.status());
+  uint64_t typical = 1500;
+  if (layout && layout->total_bytes) typical = layout->total_bytes / count;
+  SegArgs a{};
+  a.arena = static_cast<uint8_t *>(d_arena);
+  a.offsets = d_offsets;
+  a.lengths = d_lengths;
+  a.count = count;
+  a.out = d_out;
+  return hip_status(tcpck::launch_seg(op, mode, false, tcpck::shape_for_len(typical), a,
+                                      ctx->max_blocks, static_cast<hipStream_t>(stream)));
+}
+
+// ---- batched, host memory: chunked H2D -> kernel -> D2H on two streams ---------
+int tcpck_host_batch_fixed(tcpck_ctx *ctx, int op, int mode, void *h_arena, uint64_t stride,
+                           uint32_t len, uint64_t count, void *h_out) {
+  if (!ctx || !valid_op_mode(op, mode)) return TCPCK_EINVAL;
+  if (count == 0) return TCPCK_OK;
+  if (!h_arena || (len & 1) || (stride & 1) || (count > 1 && stride < len)) return TCPCK_EINVAL;
+  if (!h_out && op != TCPCK_OP_FILL) return TCPCK_EINVAL;
+  if (op == TCPCK_OP_FILL && len < 30) return TCPCK_EINVAL;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  DeviceGuard g(ctx->device);
+  if (g.status() != hipSuccess) return hip_status(g.status());
+  const uint64_t step = std::max<uint64_t>(stride, 2);
+  const uint64_t per = std::max<uint64_t>(1, ctx->chunk_bytes / step);
+  const uint64_t chunk_imgs = std::min(per, count);
+  int rc = ensure_stage(ctx, (chunk_imgs - 1) * stride + len, chunk_imgs);
+  if (rc) return rc;
+  std::vector<uint16_t> fill_res;
+  if (op == TCPCK_OP_FILL && !h_out) fill_res.resize(count);
+  auto *arena = static_cast<uint8_t *>(h_arena);
+  auto *out_bytes = h_out ? static_cast<uint8_t *>(h_out) : reinterpret_cast<uint8_t *>(fill_res.data());
+  const size_t es = out_elem(op);
+  hipError_t e = hipSuccess;
+  uint64_t c = 0;
+  for (uint64_t k0 = 0; k0 < count && e == hipSuccess; k0 += chunk_imgs, ++c) {
+    const int slot = static_cast<int>(c & 1);
+    const uint64_t n = std::min(chunk_imgs, count - k0);
+    const uint64_t bytes = (n - 1) * stride + len;
+    hipStream_t s = ctx->s[slot];
+    e = hipMemcpyAsync(ctx->stage[slot], arena + k0 * stride, bytes, hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) break;
+    SegArgs a{};
+    a.arena = ctx->stage[slot];
+    a.stride = stride;
+    a.len = len;
+    a.count = n;
+    a.out = ctx->stage_out[slot];
+    e = tcpck::launch_seg(op, mode, true, tcpck::shape_for_len(len), a, ctx->max_blocks, s);
+    if (e != hipSuccess) break;
+    e = hipMemcpyAsync(out_bytes + k0 * es, ctx->stage_out[slot], n * es, hipMemcpyDeviceToHost, s);
+  }
+  for (int i = 0; i < 2; ++i) {
+    hipError_t e2 = hipStreamSynchronize(ctx->s[i]);
+    if (e == hipSuccess) e = e2;
+  }
+  if (e != hipSuccess) return hip_status(e);
+  if (op == TCPCK_OP_FILL)
+    patch_fields(arena, 0, count, reinterpret_cast<const uint16_t *>(out_bytes), nullptr, nullptr,
+                 stride, len);
+  return TCPCK_OK;
+}
+
+int tcpck_host_batch_var(tcpck_ctx *ctx, int op, int mode, void *h_arena, const uint64_t *h_offsets,
+                         const uint32_t *h_lengths, uint64_t count, void *h_out) {
+  if (!ctx || !valid_op_mode(op, mode)) return TCPCK_EINVAL;
+  if (count == 0) return TCPCK_OK;
+  if (!h_arena || !h_offsets || !h_lengths) return TCPCK_EINVAL;
+  if (!h_out && op != TCPCK_OP_FILL) return TCPCK_EINVAL;
+  uint64_t max_len = 0;
+  for (uint64_t k = 0; k < count; ++k) {
+    if ((h_offsets[k] | h_lengths[k]) & 1) return TCPCK_EINVAL;
+    if (op == TCPCK_OP_FILL && h_lengths[k] < 30) return TCPCK_EINVAL;
+    max_len = std::max<uint64_t>(max_len, h_lengths[k]);
+  }
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  DeviceGuard g(ctx->device);
+  if (g.status() != hipSuccess) return hip_status(g.status());
+  const uint64_t cap = std::max<uint64_t>(ctx->chunk_bytes, max_len + 16);
+  const uint64_t max_imgs = std::min<uint64_t>(count, std::max<uint64_t>(cap / 32, 1));
+  int rc = ensure_stage(ctx, cap, max_imgs);
+  if (rc) return rc;
+  std::vector<uint16_t> fill_res;
+  if (op == TCPCK_OP_FILL && !h_out) fill_res.resize(count);
+  auto *arena = static_cast<uint8_t *>(h_arena);
+  auto *out_bytes = h_out ? static_cast<uint8_t *>(h_out) : reinterpret_cast<uint8_t *>(fill_res.data());
+  const size_t es = out_elem(op);
+  uint64_t total_bytes = 0;
+  for (uint64_t k = 0; k < count; ++k) total_bytes += h_lengths[k];
+  const tcpck::SegShape shape = tcpck::shape_for_len(total_bytes / count);
+  hipError_t e = hipSuccess;
+  uint64_t c = 0;
+  for (uint64_t k0 = 0; k0 < count && e == hipSuccess; ++c) {
+    // greedy chunk: extend while the hull [lo, hi) of the chunk fits the stage
+    uint64_t lo = h_offsets[k0] & ~uint64_t{15}, hi = h_offsets[k0] + h_lengths[k0];
+    uint64_t k1 = k0 + 1;
+    while (k1 < count && k1 - k0 < max_imgs) {
+      const uint64_t nlo = std::min(lo, h_offsets[k1] & ~uint64_t{15});
+      const uint64_t nhi = std::max(hi, h_offsets[k1] + h_lengths[k1]);
+      if (nhi - nlo > cap) break;
+      lo = nlo;
+      hi = nhi;
+      ++k1;
+    }
+    const uint64_t n = k1 - k0;
+    const int slot = static_cast<int>(c & 1);
+    hipStream_t s = ctx->s[slot];
+    e = hipMemcpyAsync(ctx->stage[slot], arena + lo, hi - lo, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(ctx->stage_off[slot], h_offsets + k0, n * 8, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(ctx->stage_len[slot], h_lengths + k0, n * 4, hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) break;
+    SegArgs a{};
+    a.arena = ctx->stage[slot];
+    a.offsets = ctx->stage_off[slot];
+    a.lengths = ctx->stage_len[slot];
+    a.base = lo;
+    a.count = n;
+    a.out = ctx->stage_out[slot];
+    e = tcpck::launch_seg(op, mode, false, shape, a, ctx->max_blocks, s);
+    if (e != hipSuccess) break;
+    e = hipMemcpyAsync(out_bytes + k0 * es, ctx->stage_out[slot], n * es, hipMemcpyDeviceToHost, s);
+    k0 = k1;
+  }
+  for (int i = 0; i < 2; ++i) {
+    hipError_t e2 = hipStreamSynchronize(ctx->s[i]);
+    if (e == hipSuccess) e = e2;
+  }
+  if (e != hipSuccess) return hip_status(e);
+  if (op == TCPCK_OP_FILL)
+    patch_fields(arena, 0, count, reinterpret_cast<const uint16_t *>(out_bytes), h_offsets, h_lengths,
+                 0, 0);
+  return TCPCK_OK;
+}
+
+// ---- memory helpers -----------------------------------------------------------
+int tcpck_host_alloc(size_t bytes, void **out) {
+  if (!out) return TCPCK_EINVAL;
+  *out = nullptr;
+  return hipHostMalloc(out, bytes, hipHostMallocDefault) == hipSuccess ? TCPCK_OK : TCPCK_ENOMEM;
+}
+
+int tcpck_host_free(void *p) { return hip_status(hipHostFree(p)); }
+
+int tcpck_device_alloc(tcpck_ctx *ctx, size_t bytes, void **out) {
+  if (!ctx || !out) return TCPCK_EINVAL;
+  DeviceGuard g(ctx->device);
+  *out = nullptr;
+  return hipMalloc(out, bytes) == hipSuccess ? TCPCK_OK : TCPCK_ENOMEM;
+}
+
+int tcpck_device_free(tcpck_ctx *ctx, void *p) {
+  if (!ctx) return TCPCK_EINVAL;
+  DeviceGuard g(ctx->device);
+  return hip_status(hipFree(p));
+}
+
+int tcpck_memcpy_h2d(tcpck_ctx *ctx, void *dst, const void *src, size_t bytes) {
+  if (!ctx) return TCPCK_EINVAL;
+  DeviceGuard g(ctx->device);
+  return hip_status(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+}
+
+int tcpck_memcpy_d2h(tcpck_ctx *ctx, void *dst, const void *src, size_t bytes) {
+  if (!ctx) return TCPCK_EINVAL;
+  DeviceGuard g(ctx->device);
+  return hip_status(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+}
+
+int tcpck_stream_sync(tcpck_ctx *ctx, tcpck_stream stream) {
+  if (!ctx) return TCPCK_EINVAL;
+  DeviceGuard g(ctx->device);
+  return hip_status(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+}
+
+}  // extern "C"

@@ -1,0 +1,206 @@
+// tcpck_kernels.hip -- gfx950 (CDNA4) kernels for the batched TCP checksum.
+//
+// Semantics (parity mode, Mode::kRef): the reference's CalculateChecksum,
+// filixi/TCP-stack include/tcp-header.h:252-263 -- little-endian u16 words
+// summed into a u32 with no end-around carry, result ~sum truncated to u16,
+// i.e. ~(sum mod 2^16).  Mode::kRfc1071 is the opt-in one's-complement sum.
+//
+// Shape of the work: a pure HBM-read streaming reduction (~0.5 integer add per
+// byte, far below any compute roof; no MFMA).  What matters is bytes in flight
+// and coalescing:
+//   * G consecutive lanes own one image; lane l of the group reads the image's
+//     16-byte chunks l, l+G, l+2G, ... so one wave-instruction reads 64/G
+//     contiguous runs of G*16 bytes (1 KiB per wave-instruction in total);
+//   * each lane issues U 16-byte nontemporal loads back to back before it
+//     consumes any of them (U*1 KiB in flight per wave, ~32 waves per CU);
+//   * chunk addresses past the image end are clamped to the image's last
+//     chunk (always a legal address) and their words masked to zero, so the
+//     loads are unconditional: no per-load branch, no per-load vmcnt(0);
+//   * images start at arbitrary even offsets: the first chunk is the image
+//     start rounded down to 16 B and its leading words are masked, the last
+//     chunk's trailing words likewise (word-granular masks: even lengths that
+//     are 2 mod 4 are exact);
+//   * the per-lane accumulator is a u32: acc += w + (w >> 16) per dword w
+//     keeps the low 16 bits equal to the sum of both u16 halves mod 2^16
+//     (the high half's carries land above bit 15 and are discarded), which is
+//     exactly the reference's arithmetic; RFC 1071 mode uses a u32 add with
+//     end-around carry (2^32 == 1 mod 0xFFFF);
+//   * the G partial sums are combined with cross-lane xor shuffles, and lane 0
+//     of the group stores the 2-byte result (or, for kFill, also writes it
+//     into bytes 28-29 of the image; for kVerify stores checksum == 0).
+#include "tcpck_internal.h"
+
+namespace tcpck {
+
+namespace {
+
+using u32x4 = __attribute__((ext_vector_type(4))) unsigned int;
+
+constexpr int kBlock = 256;
+
+__device__ __forceinline__ u32x4 load16_nt(const uint8_t *p) {
+  return __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
+}
+
+// 8-bit word-validity mask of one 16-byte chunk -> AND mask of dword j.
+__device__ __forceinline__ uint32_t dword_mask(uint32_t wm, int j) {
+  const uint32_t t = (wm >> (2 * j)) & 3u;
+  return ((t & 1u) ? 0x0000FFFFu : 0u) | ((t & 2u) ? 0xFFFF0000u : 0u);
+}
+
+template <int MODE>
+__device__ __forceinline__ uint32_t accumulate(uint32_t acc, uint32_t w) {
+  if constexpr (MODE == kRef) {
+    return acc + w + (w >> 16);
+  } else {
+    // one's-complement 32-bit add: fold the carry back in (2^32 == 1 mod 0xFFFF)
+    const uint32_t s = acc + w;
+    return s + (s < w ? 1u : 0u);
+  }
+}
+
+// Folds a per-lane accumulator to 16 significant bits without changing the
+// value mod 2^16 (REF) or mod 0xFFFF keeping zero-ness (RFC 1071).
+template <int MODE>
+__device__ __forceinline__ uint32_t fold_lane(uint32_t acc) {
+  if constexpr (MODE == kRef) {
+    return acc & 0xFFFFu;
+  } else {
+    acc = (acc & 0xFFFFu) + (acc >> 16);
+    return (acc & 0xFFFFu) + (acc >> 16);
+  }
+}
+
+template <int MODE>
+__device__ __forceinline__ uint16_t finish(uint32_t sum) {
+  if constexpr (MODE == kRef) {
+    return static_cast<uint16_t>(~sum);  // tcp-header.h:262
+  } else {
+    sum = (sum & 0xFFFFu) + (sum >> 16);
+    sum = (sum & 0xFFFFu) + (sum >> 16);
+    return static_cast<uint16_t>(~sum);
+  }
+}
+
+template <int G>
+__device__ __forceinline__ uint32_t group_sum(uint32_t x) {
+#pragma unroll
+  for (int m = G / 2; m >= 1; m >>= 1) x += __shfl_xor(x, m, 64);
+  return x;
+}
+
+template <int G, int U, int MODE, int OP, bool FIXED>
+__global__ void __launch_bounds__(kBlock) seg_kernel(SegArgs a) {
+  static_assert(G >= 1 && G <= 64 && (G & (G - 1)) == 0, "G must be a power of two <= 64");
+  const uint32_t gl = threadIdx.x & (G - 1);
+  const uint64_t groups_per_grid = static_cast<uint64_t>(gridDim.x) * (kBlock / G);
+  for (uint64_t k = (static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x) / G; k < a.count;
+       k += groups_per_grid) {
+    const uint64_t start = FIXED ? k * a.stride : a.offsets[k] - a.base;
+    const uint32_t len = FIXED ? a.len : a.lengths[k];
+    const uint8_t *p0 = a.arena + (start & ~uint64_t{15});
+    const int32_t lead = static_cast<int32_t>(start & 15);      // masked bytes before the image
+    const int32_t span = lead + static_cast<int32_t>(len);      // bytes from p0 to the image end
+    const uint32_t nch = static_cast<uint32_t>(span + 15) >> 4;  // 16-byte chunks touched
+    const int32_t field = (OP == kFill) ? lead + 28 : -64;       // checksum field, counts as 0
+
+    uint32_t acc = 0;
+    for (uint32_t i0 = gl; i0 < nch; i0 += G * U) {
+      u32x4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t i = i0 + u * G;
+        const uint32_t ic = i < nch ? i : nch - 1;  // clamp: always a legal address
+        v[u] = load16_nt(p0 + 16 * static_cast<uint64_t>(ic));
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int32_t rel = static_cast<int32_t>(16 * (i0 + u * G));
+        const int32_t lo = min(max(lead - rel, 0), 16);
+        const int32_t hi = min(max(span - rel, 0), 16);
+        uint32_t wm = ((1u << (hi >> 1)) - 1u) & ~((1u << (lo >> 1)) - 1u);
+        if (OP == kFill) {
+          const int32_t fb = field - rel;
+          if (fb >= 0 && fb < 16) wm &= ~(1u << (fb >> 1));
+        }
+        u32x4 w = v[u];
+        if (wm != 0xFFu) {
+          w.x &= dword_mask(wm, 0);
+          w.y &= dword_mask(wm, 1);
+          w.z &= dword_mask(wm, 2);
+          w.w &= dword_mask(wm, 3);
+        }
+        acc = accumulate<MODE>(acc, w.x);
+        acc = accumulate<MODE>(acc, w.y);
+        acc = accumulate<MODE>(acc, w.z);
+        acc = accumulate<MODE>(acc, w.w);
+      }
+      if (MODE == kRfc1071) acc = fold_lane<MODE>(acc);
+    }
+    const uint32_t sum = group_sum<G>(fold_lane<MODE>(acc));
+    if (gl == 0) {
+      const uint16_t c = finish<MODE>(sum);
+      if constexpr (OP == kVerify) {
+        static_cast<uint8_t *>(a.out)[k] = (c == 0) ? 1 : 0;
+      } else {
+        if (a.out) static_cast<uint16_t *>(a.out)[k] = c;
+        if (OP == kFill && len >= 30)
+          *reinterpret_cast<uint16_t *>(a.arena + start + 28) = c;  // stored raw, tcp-header.h:177
+      }
+    }
+  }
+}
+
+template <int G, int U, int MODE, int OP, bool FIXED>
+hipError_t launch_one(const SegArgs &a, uint32_t max_blocks, hipStream_t stream) {
+  const uint64_t groups_per_block = kBlock / G;
+  uint64_t blocks = (a.count + groups_per_block - 1) / groups_per_block;
+  if (blocks > max_blocks) blocks = max_blocks;
+  if (blocks == 0) return hipSuccess;
+  hipLaunchKernelGGL((seg_kernel<G, U, MODE, OP, FIXED>), dim3(static_cast<uint32_t>(blocks)),
+                     dim3(kBlock), 0, stream, a);
+  return hipGetLastError();
+}
+
+template <int G, int U, int MODE, int OP>
+hipError_t dispatch_fixed(bool fixed, const SegArgs &a, uint32_t mb, hipStream_t s) {
+  return fixed ? launch_one<G, U, MODE, OP, true>(a, mb, s)
+               : launch_one<G, U, MODE, OP, false>(a, mb, s);
+}
+
+template <int G, int U, int MODE>
+hipError_t dispatch_op(int op, bool fixed, const SegArgs &a, uint32_t mb, hipStream_t s) {
+  switch (op) {
+    case kChecksum: return dispatch_fixed<G, U, MODE, kChecksum>(fixed, a, mb, s);
+    case kFill: return dispatch_fixed<G, U, MODE, kFill>(fixed, a, mb, s);
+    case kVerify: return dispatch_fixed<G, U, MODE, kVerify>(fixed, a, mb, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+template <int G, int U>
+hipError_t dispatch_mode(int mode, int op, bool fixed, const SegArgs &a, uint32_t mb,
+                         hipStream_t s) {
+  return mode == kRef ? dispatch_op<G, U, kRef>(op, fixed, a, mb, s)
+                      : dispatch_op<G, U, kRfc1071>(op, fixed, a, mb, s);
+}
+
+}  // namespace
+
+SegShape shape_for_len(uint64_t typical_len) {
+  if (typical_len <= 256) return kShapeSmall;
+  if (typical_len <= 4096) return kShapeMss;
+  return kShapeJumbo;
+}
+
+hipError_t launch_seg(int op, int mode, bool fixed, SegShape shape, const SegArgs &a,
+                      uint32_t max_blocks, hipStream_t stream) {
+  switch (shape) {
+    case kShapeSmall: return dispatch_mode<8, 2>(mode, op, fixed, a, max_blocks, stream);
+    case kShapeMss: return dispatch_mode<16, 6>(mode, op, fixed, a, max_blocks, stream);
+    case kShapeJumbo: return dispatch_mode<64, 4>(mode, op, fixed, a, max_blocks, stream);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace tcpck

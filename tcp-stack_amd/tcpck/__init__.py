@@ -1,0 +1,235 @@
+"""tcpck -- Python binding of libtcpck.so (the MI355X TCP checksum library).
+
+A thin ctypes layer over the C ABI declared in include/tcpck.h, used by the
+parity tests and bench.py.  There is no Python or CPU fallback for the batched
+path: if libtcpck.so is missing or the device is not a gfx950, constructing a
+``Context`` raises.
+
+Reference API mirrored (filixi/TCP-stack):
+  * ``checksum16``   <- CalculateChecksum(const TcpPacket&), include/tcp-header.h:252-263
+  * OP_FILL          <- Checksum()=0; Checksum()=CalculateChecksum(pkt),
+                        src/socket-manager.cc:9-10, include/socket-manager.h:259-260
+  * OP_VERIFY        <- CalculateChecksum(pkt) == 0, include/socket-manager.h:182
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.dirname(HERE)
+LIB_PATH = os.path.join(PKG_ROOT, "libtcpck.so")
+
+OK = 0
+EINVAL = -22
+ENOMEM = -12
+ENODEV = -19
+EHIP = -1000
+
+MODE_REF = 0
+MODE_RFC1071 = 1
+
+OP_CHECKSUM = 0
+OP_FILL = 1
+OP_VERIFY = 2
+
+LAYOUT_PACKED = 1
+
+# Every symbol include/tcpck.h declares (checked by tests/test_abi.py).
+EXPORTS = (
+    "tcpck_abi_version", "tcpck_strerror", "tcpck_device_supported",
+    "tcpck_ctx_create", "tcpck_ctx_destroy", "tcpck_ctx_device",
+    "tcpck_checksum16", "tcpck_fill16", "tcpck_update16",
+    "tcpck_batch_fixed", "tcpck_batch_var",
+    "tcpck_host_batch_fixed", "tcpck_host_batch_var", "tcpck_ctx_set_chunk_bytes",
+    "tcpck_host_alloc", "tcpck_host_free", "tcpck_device_alloc", "tcpck_device_free",
+    "tcpck_memcpy_h2d", "tcpck_memcpy_d2h", "tcpck_stream_sync",
+    "tcpck_synth_fixed", "tcpck_synth_var",
+)
+
+
+class TcpckError(RuntimeError):
+    def __init__(self, status: int, what: str = ""):
+        self.status = status
+        super().__init__(f"{what}: status {status} ({strerror(status)})")
+
+
+class Layout(ctypes.Structure):
+    _fields_ = [("total_bytes", ctypes.c_uint64), ("min_len", ctypes.c_uint32),
+                ("max_len", ctypes.c_uint32), ("flags", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32)]
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Loads libtcpck.so (built in-tree by __graft_entry__.build()); raises if absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, u64, u32, i32, sz = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int, ctypes.c_size_t
+    sig = {
+        "tcpck_abi_version": (i32, []),
+        "tcpck_strerror": (ctypes.c_char_p, [i32]),
+        "tcpck_device_supported": (i32, [i32]),
+        "tcpck_ctx_create": (i32, [i32, ctypes.POINTER(vp)]),
+        "tcpck_ctx_destroy": (i32, [vp]),
+        "tcpck_ctx_device": (i32, [vp]),
+        "tcpck_checksum16": (i32, [vp, sz, i32, ctypes.POINTER(ctypes.c_uint16)]),
+        "tcpck_fill16": (i32, [vp, sz, i32, ctypes.POINTER(ctypes.c_uint16)]),
+        "tcpck_update16": (ctypes.c_uint16, [ctypes.c_uint16, ctypes.c_uint16, ctypes.c_uint16, i32]),
+        "tcpck_batch_fixed": (i32, [vp, i32, i32, vp, u64, u32, u64, vp, vp]),
+        "tcpck_batch_var": (i32, [vp, i32, i32, vp, vp, vp, u64, vp, ctypes.POINTER(Layout), vp]),
+        "tcpck_host_batch_fixed": (i32, [vp, i32, i32, vp, u64, u32, u64, vp]),
+        "tcpck_host_batch_var": (i32, [vp, i32, i32, vp, vp, vp, u64, vp]),
+        "tcpck_ctx_set_chunk_bytes": (i32, [vp, u64]),
+        "tcpck_host_alloc": (i32, [sz, ctypes.POINTER(vp)]),
+        "tcpck_host_free": (i32, [vp]),
+        "tcpck_device_alloc": (i32, [vp, sz, ctypes.POINTER(vp)]),
+        "tcpck_device_free": (i32, [vp, vp]),
+        "tcpck_memcpy_h2d": (i32, [vp, vp, vp, sz]),
+        "tcpck_memcpy_d2h": (i32, [vp, vp, vp, sz]),
+        "tcpck_stream_sync": (i32, [vp, vp]),
+        "tcpck_synth_fixed": (i32, [vp, u64, u32, u64, u64, u64, i32, vp]),
+        "tcpck_synth_var": (i32, [vp, vp, vp, u32, u64, u64, u64, i32, vp]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def strerror(status: int) -> str:
+    try:
+        return lib().tcpck_strerror(status).decode()
+    except ImportError:
+        return "libtcpck.so unavailable"
+
+
+def _check(status: int, what: str) -> None:
+    if status != OK:
+        raise TcpckError(status, what)
+
+
+def _ptr(x) -> int | None:
+    """Device/host address of a torch tensor, numpy array or int (None -> NULL)."""
+    if x is None:
+        return None
+    if isinstance(x, int):
+        return x
+    if hasattr(x, "data_ptr"):
+        return x.data_ptr()
+    if hasattr(x, "ctypes"):
+        return x.ctypes.data
+    raise TypeError(f"cannot take the address of {type(x)}")
+
+
+def _stream(s) -> int | None:
+    if s is None:
+        return None
+    if isinstance(s, int):
+        return s
+    return s.cuda_stream  # torch.cuda.Stream
+
+
+# ---- single image, host ------------------------------------------------------
+
+def _as_u8(buf):
+    import numpy as np
+    if isinstance(buf, (bytes, bytearray, memoryview)):
+        return np.frombuffer(bytes(buf), dtype=np.uint8)
+    return np.ascontiguousarray(buf, dtype=np.uint8)
+
+
+def checksum16(buf, mode: int = MODE_REF) -> int:
+    """CalculateChecksum of one host image (tcp-header.h:252-263)."""
+    a = _as_u8(buf)
+    out = ctypes.c_uint16()
+    _check(lib().tcpck_checksum16(a.ctypes.data, a.size, mode, ctypes.byref(out)), "tcpck_checksum16")
+    return out.value
+
+
+def fill16(img, mode: int = MODE_REF) -> int:
+    """Send-side insertion in place on a writable uint8 numpy image."""
+    out = ctypes.c_uint16()
+    _check(lib().tcpck_fill16(img.ctypes.data, img.size, mode, ctypes.byref(out)), "tcpck_fill16")
+    return out.value
+
+
+def update16(checksum: int, old_word: int, new_word: int, mode: int = MODE_REF) -> int:
+    return int(lib().tcpck_update16(checksum, old_word, new_word, mode))
+
+
+def synth_fixed(arena, stride: int, length: int, count: int, seed: int = 42,
+                first_index: int = 0, kind: int = 0, stream=None) -> None:
+    """Fills a device arena with a fixed-stride synthetic batch (see include/tcpck.h)."""
+    _check(lib().tcpck_synth_fixed(_ptr(arena), stride, length, count, seed, first_index, kind,
+                                   _stream(stream)), "tcpck_synth_fixed")
+
+
+def synth_var(arena, offsets, lengths, max_len: int, count: int, seed: int = 42,
+              first_index: int = 0, kind: int = 0, stream=None) -> None:
+    _check(lib().tcpck_synth_var(_ptr(arena), _ptr(offsets), _ptr(lengths), max_len, count, seed,
+                                 first_index, kind, _stream(stream)), "tcpck_synth_var")
+
+
+# ---- context -------------------------------------------------------------------
+
+class Context:
+    """One libtcpck context bound to a HIP device (gfx950 only)."""
+
+    def __init__(self, device: int = 0):
+        self._h = ctypes.c_void_p()
+        _check(lib().tcpck_ctx_create(device, ctypes.byref(self._h)), f"tcpck_ctx_create({device})")
+        self.device = device
+
+    def close(self) -> None:
+        if self._h:
+            lib().tcpck_ctx_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # device-resident batches (the hot path)
+    def batch_fixed(self, op: int, arena, stride: int, length: int, count: int, out,
+                    mode: int = MODE_REF, stream=None) -> None:
+        _check(lib().tcpck_batch_fixed(self._h, op, mode, _ptr(arena), stride, length, count,
+                                       _ptr(out), _stream(stream)), "tcpck_batch_fixed")
+
+    def batch_var(self, op: int, arena, offsets, lengths, count: int, out, mode: int = MODE_REF,
+                  total_bytes: int = 0, min_len: int = 0, max_len: int = 0, packed: bool = False,
+                  stream=None) -> None:
+        lay = Layout(total_bytes, min_len, max_len, LAYOUT_PACKED if packed else 0, 0)
+        _check(lib().tcpck_batch_var(self._h, op, mode, _ptr(arena), _ptr(offsets), _ptr(lengths),
+                                     count, _ptr(out), ctypes.byref(lay), _stream(stream)),
+               "tcpck_batch_var")
+
+    # host-memory batches (end to end, PCIe included)
+    def host_batch_fixed(self, op: int, arena, stride: int, length: int, count: int, out,
+                         mode: int = MODE_REF) -> None:
+        _check(lib().tcpck_host_batch_fixed(self._h, op, mode, _ptr(arena), stride, length, count,
+                                            _ptr(out)), "tcpck_host_batch_fixed")
+
+    def host_batch_var(self, op: int, arena, offsets, lengths, count: int, out,
+                       mode: int = MODE_REF) -> None:
+        _check(lib().tcpck_host_batch_var(self._h, op, mode, _ptr(arena), _ptr(offsets),
+                                          _ptr(lengths), count, _ptr(out)), "tcpck_host_batch_var")
+
+    def set_chunk_bytes(self, n: int) -> None:
+        _check(lib().tcpck_ctx_set_chunk_bytes(self._h, n), "tcpck_ctx_set_chunk_bytes")

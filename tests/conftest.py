@@ -1,0 +1,61 @@
+"""Test configuration: markers, import paths and shared fixtures.
+
+`-m "not gpu"` runs the oracle-vs-golden, ABI/host-logic and multi-process
+(gloo) tests on CPU; `-m gpu` runs the HIP parity tests through the C ABI.
+"""
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "tcp-stack_amd"), os.path.join(ROOT, "tests")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+GOLDEN_DIR = os.path.join(ROOT, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU and libtcpck.so")
+
+
+class Golden:
+    """tests/golden/golden.{bin,json}: reference outputs from tests/golden/gen_golden.cc."""
+
+    def __init__(self):
+        with open(os.path.join(GOLDEN_DIR, "golden.json")) as f:
+            meta = json.load(f)
+        self.blob = np.fromfile(os.path.join(GOLDEN_DIR, meta["blob"]), dtype=np.uint8)
+        assert self.blob.size == meta["blob_bytes"]
+        self.cases = meta["cases"]
+
+    def image(self, case, key="off"):
+        o = case[key]
+        return self.blob[o:o + case["len"]].copy()
+
+    def by_kind(self, kind):
+        return [c for c in self.cases if c["kind"] == kind]
+
+
+@pytest.fixture(scope="session")
+def golden():
+    return Golden()
+
+
+@pytest.fixture(scope="session")
+def oracle_c():
+    from oracle.ref16 import Ref16C
+    return Ref16C(build=True)
+
+
+@pytest.fixture(scope="session")
+def built_lib():
+    """libtcpck.so, built in-tree if missing (hipcc cross-compiles without a GPU)."""
+    import tcpck
+    if not os.path.exists(tcpck.LIB_PATH):
+        import subprocess
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tcp-stack_amd"), "-j8"], check=True)
+    return tcpck.lib()

@@ -1,0 +1,107 @@
+"""CPU tests of the C-ABI library: it loads, exports every symbol include/tcpck.h
+declares, and its host-side (single image) entry points match the golden
+vectors.  No compute call here touches a GPU."""
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+
+def declared_symbols():
+    with open(os.path.join(ROOT, "include", "tcpck.h")) as f:
+        text = f.read()
+    return sorted(set(re.findall(r"\b(tcpck_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_and_binding_agree(built_lib):
+    import tcpck
+    assert declared_symbols() == sorted(tcpck.EXPORTS)
+
+
+def test_library_exports_every_declared_symbol(built_lib):
+    for name in declared_symbols():
+        assert hasattr(built_lib, name), name
+    assert built_lib.tcpck_abi_version() == 1
+
+
+def test_library_has_gfx950_code_object(built_lib):
+    import tcpck
+    with open(tcpck.LIB_PATH, "rb") as f:
+        blob = f.read()
+    assert b"gfx950" in blob
+
+
+def test_host_checksum_matches_golden(golden, built_lib):
+    import tcpck
+    for c in golden.by_kind("checksum"):
+        assert tcpck.checksum16(golden.image(c)) == c["expected"], c["name"]
+
+
+def test_host_fill_matches_golden(golden, built_lib):
+    import tcpck
+    for c in golden.by_kind("fill"):
+        img = golden.image(c)
+        assert tcpck.fill16(img) == c["expected"]
+        np.testing.assert_array_equal(img, golden.blob[c["fill_off"]:c["fill_off"] + c["len"]])
+
+
+def test_host_rfc1071_mode(built_lib, oracle_c):
+    import tcpck
+    rng = np.random.default_rng(5)
+    for n in (0, 2, 30, 32, 1492, 65536, 200000):
+        img = rng.integers(0, 256, n, dtype=np.uint8)
+        assert tcpck.checksum16(img, tcpck.MODE_RFC1071) == oracle_c.one(img, 1)
+    ones = np.full(4096, 0xFF, np.uint8)
+    assert tcpck.checksum16(ones, tcpck.MODE_RFC1071) == oracle_c.one(ones, 1)
+
+
+def test_host_large_and_wrapping(built_lib, oracle_c):
+    import tcpck
+    ones = np.full(1 << 20, 0xFF, np.uint8)
+    assert tcpck.checksum16(ones) == oracle_c.one(ones)
+    rng = np.random.default_rng(9)
+    for n in (6, 8, 10, 14, 262144 + 6, (1 << 18) - 2):
+        img = rng.integers(0, 256, n, dtype=np.uint8)
+        assert tcpck.checksum16(img) == oracle_c.one(img), n
+
+
+def test_host_rejects_odd_and_null(built_lib):
+    import tcpck
+    with pytest.raises(tcpck.TcpckError) as e:
+        tcpck.checksum16(np.zeros(59, np.uint8))
+    assert e.value.status == tcpck.EINVAL
+    with pytest.raises(tcpck.TcpckError):
+        tcpck.fill16(np.zeros(28, np.uint8))  # no room for the checksum field
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_incremental_update_matches_recompute(built_lib, oracle_c, mode):
+    """Retransmit ACK rewrite (socket-internal.h:376-377) without a full pass."""
+    import tcpck
+    rng = np.random.default_rng(11 + mode)
+    for _ in range(300):
+        n = int(rng.integers(16, 400)) * 2
+        img = rng.integers(0, 256, n, dtype=np.uint8)
+        c0 = tcpck.fill16(img, mode)
+        w = int(rng.integers(0, n // 2))
+        if w == 14:  # the checksum field itself
+            continue
+        old = int(img[2 * w]) | int(img[2 * w + 1]) << 8
+        new = int(rng.integers(0, 1 << 16))
+        img[2 * w], img[2 * w + 1] = new & 0xFF, new >> 8
+        c1 = tcpck.update16(c0, old, new, mode)
+        img[28], img[29] = 0, 0
+        assert c1 == oracle_c.one(img, mode)
+
+
+def test_ctx_create_without_gpu_fails_cleanly(built_lib):
+    import torch
+    import tcpck
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(tcpck.TcpckError) as e:
+        tcpck.Context(0)
+    assert e.value.status in (tcpck.ENODEV,) or e.value.status <= tcpck.EHIP

@@ -1,0 +1,285 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the oracle.
+
+* golden vectors (the reference's own outputs) for checksum / fill / verify,
+  at unaligned offsets, through every kernel shape;
+* seeded random batches (fixed stride and variable length) against the C
+  oracle, bit-exact;
+* BASELINE.json's full configs (C2 1M x 1492 B, C3 4M mixed, C4 256K x 64 KiB)
+  against the oracle (C2, C3 in full; C4 on a sample of images) and through
+  size-independent properties (fill -> verify all true, single-byte
+  corruption detected exactly where injected);
+* the host-memory (PCIe, end-to-end) batch path.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def ctx(built_lib):
+    import tcpck
+    assert torch.cuda.is_available(), "gpu tests need a GPU"
+    c = tcpck.Context(0)
+    yield c
+    c.close()
+
+
+def dev(a: np.ndarray):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def host(t) -> np.ndarray:
+    torch.cuda.synchronize()
+    return t.cpu().numpy()
+
+
+SHAPE_HINTS = {"small": 100, "mss": 1500, "jumbo": 65536}
+
+
+def golden_arrays(golden, kind):
+    cases = golden.by_kind(kind)
+    off = np.array([c["off"] for c in cases], np.uint64)
+    ln = np.array([c["len"] for c in cases], np.uint32)
+    exp = np.array([c["expected"] for c in cases])
+    return cases, off, ln, exp
+
+
+@pytest.mark.parametrize("shape", list(SHAPE_HINTS))
+def test_golden_checksum(ctx, golden, shape):
+    import tcpck
+    cases, off, ln, exp = golden_arrays(golden, "checksum")
+    arena = dev(golden.blob)
+    out = torch.empty(len(cases), dtype=torch.int16, device="cuda")
+    ctx.batch_var(tcpck.OP_CHECKSUM, arena, dev(off), dev(ln), len(cases), out,
+                  total_bytes=SHAPE_HINTS[shape] * len(cases))
+    got = host(out).view(np.uint16)
+    bad = [(c["name"], int(g), c["expected"]) for c, g in zip(cases, got) if g != c["expected"]]
+    assert not bad, bad[:10]
+
+
+@pytest.mark.parametrize("shape", list(SHAPE_HINTS))
+def test_golden_fill_and_verify(ctx, golden, shape):
+    import tcpck
+    cases, off, ln, exp = golden_arrays(golden, "fill")
+    arena = dev(golden.blob)
+    out = torch.zeros(len(cases), dtype=torch.int16, device="cuda")
+    ctx.batch_var(tcpck.OP_FILL, arena, dev(off), dev(ln), len(cases), out,
+                  total_bytes=SHAPE_HINTS[shape] * len(cases))
+    got = host(out).view(np.uint16)
+    np.testing.assert_array_equal(got, exp.astype(np.uint16))
+    a = host(arena)
+    for c in cases:
+        np.testing.assert_array_equal(a[c["off"]:c["off"] + c["len"]],
+                                      golden.blob[c["fill_off"]:c["fill_off"] + c["len"]],
+                                      err_msg=c["name"])
+    vcases, voff, vln, vexp = golden_arrays(golden, "verify")
+    ok = torch.zeros(len(vcases), dtype=torch.uint8, device="cuda")
+    ctx.batch_var(tcpck.OP_VERIFY, dev(golden.blob), dev(voff), dev(vln), len(vcases), ok,
+                  total_bytes=SHAPE_HINTS[shape] * len(vcases))
+    np.testing.assert_array_equal(host(ok), vexp.astype(np.uint8))
+
+
+def test_synth_generator_matches_host_restatement(ctx):
+    import tcpck
+    import synth_np
+    for stride, length, kind in ((1492, 1492, 0), (104, 96, 0), (640, 608, 2), (96, 96, 1), (34, 34, 0)):
+        n = 37
+        a = torch.zeros(n * stride, dtype=torch.uint8, device="cuda")
+        tcpck.synth_fixed(a, stride, length, n, seed=42, first_index=1000, kind=kind)
+        np.testing.assert_array_equal(host(a), synth_np.arena_fixed(42, n, stride, length, 1000, kind))
+
+
+@pytest.mark.parametrize("stride,length", [(1492, 1492), (1504, 1492), (96, 96), (608, 608),
+                                           (1490, 1490), (1496, 1494), (32, 32), (34, 30),
+                                           (2, 2), (8, 0), (4096, 4094), (65536, 65536),
+                                           (65538, 65534)])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_fixed_random_vs_oracle(ctx, oracle_c, stride, length, mode):
+    import tcpck
+    rng = np.random.default_rng(stride * 7 + length + mode)
+    count = max(3, min(20000, (24 << 20) // stride))
+    arena_np = rng.integers(0, 256, count * stride, dtype=np.uint8)
+    if mode == 0 and length >= 4:
+        arena_np[:length] = 0xFF  # an adversarial all-ones image
+    arena = dev(arena_np)
+    out = torch.empty(count, dtype=torch.int16, device="cuda")
+    ctx.batch_fixed(tcpck.OP_CHECKSUM, arena, stride, length, count, out, mode=mode)
+    exp = oracle_c.batch(arena_np, stride=stride, length=length, count=count, mode=mode, threads=8)
+    np.testing.assert_array_equal(host(out).view(np.uint16), exp)
+    ok = torch.empty(count, dtype=torch.uint8, device="cuda")
+    ctx.batch_fixed(tcpck.OP_VERIFY, arena, stride, length, count, ok, mode=mode)
+    np.testing.assert_array_equal(host(ok), (exp == 0).astype(np.uint8))
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("shape", list(SHAPE_HINTS))
+def test_var_random_ragged_vs_oracle(ctx, oracle_c, mode, shape):
+    """Ragged lengths 0..3000 (even), unordered offsets, gaps: every kernel shape."""
+    import tcpck
+    rng = np.random.default_rng(100 + mode)
+    count = 30000
+    ln = (rng.integers(0, 1501, count) * 2).astype(np.uint32)
+    ln[:50] = np.arange(0, 100, 2)
+    gaps = (rng.integers(0, 9, count) * 2).astype(np.uint64)
+    off = np.zeros(count, np.uint64)
+    off[1:] = np.cumsum(ln[:-1].astype(np.uint64) + gaps[:-1])
+    total = int(off[-1] + ln[-1]) + 64
+    perm = rng.permutation(count)
+    off, ln = off[perm], ln[perm]
+    arena_np = rng.integers(0, 256, total, dtype=np.uint8)
+    out = torch.empty(count, dtype=torch.int16, device="cuda")
+    ctx.batch_var(tcpck.OP_CHECKSUM, dev(arena_np), dev(off), dev(ln), count, out, mode=mode,
+                  total_bytes=SHAPE_HINTS[shape] * count)
+    exp = oracle_c.batch(arena_np, off, ln, mode=mode, threads=8)
+    np.testing.assert_array_equal(host(out).view(np.uint16), exp)
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_fill_random_vs_oracle(ctx, oracle_c, mode):
+    """Send-side insertion: garbage in bytes 28-29 must not matter, result stored raw."""
+    import tcpck
+    from oracle import ref16 as R
+    rng = np.random.default_rng(200 + mode)
+    stride, length, count = 1500, 1492, 5000
+    arena_np = rng.integers(0, 256, stride * count, dtype=np.uint8)
+    arena = dev(arena_np)
+    out = torch.empty(count, dtype=torch.int16, device="cuda")
+    ctx.batch_fixed(tcpck.OP_FILL, arena, stride, length, count, out, mode=mode)
+    got_arena = host(arena)
+    exp = np.empty(count, np.uint16)
+    for k in range(count):
+        img = arena_np[k * stride:k * stride + length].copy()
+        exp[k] = R.fill_np(img, mode)
+        np.testing.assert_array_equal(got_arena[k * stride:k * stride + length], img)
+    np.testing.assert_array_equal(host(out).view(np.uint16), exp)
+    ok = torch.empty(count, dtype=torch.uint8, device="cuda")
+    ctx.batch_fixed(tcpck.OP_VERIFY, arena, stride, length, count, ok, mode=mode)
+    assert bool(host(ok).all())
+    # FILL with out == NULL writes only the arena
+    arena2 = dev(arena_np)
+    ctx.batch_fixed(tcpck.OP_FILL, arena2, stride, length, count, None, mode=mode)
+    np.testing.assert_array_equal(host(arena2), got_arena)
+
+
+def test_argument_errors(ctx):
+    import tcpck
+    a = torch.zeros(4096, dtype=torch.uint8, device="cuda")
+    o = torch.zeros(16, dtype=torch.int16, device="cuda")
+    with pytest.raises(tcpck.TcpckError) as e:
+        ctx.batch_fixed(tcpck.OP_CHECKSUM, a, 60, 59, 4, o)
+    assert e.value.status == tcpck.EINVAL
+    with pytest.raises(tcpck.TcpckError):
+        ctx.batch_fixed(tcpck.OP_FILL, a, 28, 28, 4, o)
+    with pytest.raises(tcpck.TcpckError):
+        ctx.batch_fixed(7, a, 64, 64, 4, o)
+    ctx.batch_fixed(tcpck.OP_CHECKSUM, a, 64, 64, 0, o)  # empty batch is a no-op
+
+
+# ---- BASELINE.json configs at full size ------------------------------------------
+
+def _synth_fixed_dev(count, stride, length, seed=42, first_index=0):
+    import tcpck
+    a = torch.empty(count * stride, dtype=torch.uint8, device="cuda")
+    tcpck.synth_fixed(a, stride, length, count, seed=seed, first_index=first_index)
+    return a
+
+
+def test_c2_full_1m_x_1492_vs_oracle(ctx, oracle_c):
+    import tcpck
+    count, L = 1 << 20, 1492
+    a = _synth_fixed_dev(count, L, L)
+    out = torch.empty(count, dtype=torch.int16, device="cuda")
+    ctx.batch_fixed(tcpck.OP_CHECKSUM, a, L, L, count, out)
+    exp = oracle_c.batch(host(a), stride=L, length=L, count=count, threads=16)
+    np.testing.assert_array_equal(host(out).view(np.uint16), exp)
+    # fill -> verify round trip at full size, then corruption is caught exactly
+    ctx.batch_fixed(tcpck.OP_FILL, a, L, L, count, None)
+    ok = torch.empty(count, dtype=torch.uint8, device="cuda")
+    ctx.batch_fixed(tcpck.OP_VERIFY, a, L, L, count, ok)
+    assert int(ok.sum().item()) == count
+    rng = np.random.default_rng(3)
+    bad = np.unique(rng.integers(0, count, 1000))
+    pos = torch.from_numpy(bad.astype(np.int64) * L + rng.integers(0, L, bad.size)).cuda()
+    a[pos] ^= 0x40
+    ctx.batch_fixed(tcpck.OP_VERIFY, a, L, L, count, ok)
+    fails = np.nonzero(host(ok) == 0)[0]
+    np.testing.assert_array_equal(fails, bad)
+
+
+def test_c3_full_4m_mixed_vs_oracle(ctx, oracle_c):
+    import tcpck
+    import synth_np
+    count = 4 << 20
+    off, ln, total = synth_np.mixed_layout(count, seed=42)
+    a = torch.empty(total, dtype=torch.uint8, device="cuda")
+    d_off, d_ln = dev(off), dev(ln)
+    tcpck.synth_var(a, d_off, d_ln, 1492, count, seed=42)
+    out = torch.empty(count, dtype=torch.int16, device="cuda")
+    ctx.batch_var(tcpck.OP_CHECKSUM, a, d_off, d_ln, count, out, total_bytes=int(ln.sum()),
+                  min_len=96, max_len=1492, packed=False)
+    exp = oracle_c.batch(host(a), off, ln, threads=16)
+    np.testing.assert_array_equal(host(out).view(np.uint16), exp)
+
+
+def test_c4_jumbo_256k_x_64k_sampled(ctx, oracle_c):
+    import tcpck
+    count, L = 256 << 10, 65536
+    a = _synth_fixed_dev(count, L, L)
+    out = torch.empty(count, dtype=torch.int16, device="cuda")
+    ctx.batch_fixed(tcpck.OP_CHECKSUM, a, L, L, count, out)
+    got = host(out).view(np.uint16)
+    idx = np.unique(np.concatenate([np.arange(0, count, 997), [count - 1]]))
+    sample = host(a.view(count, L)[torch.from_numpy(idx).cuda()]).reshape(-1)
+    exp = oracle_c.batch(sample, stride=L, length=L, count=idx.size, threads=16)
+    np.testing.assert_array_equal(got[idx], exp)
+    ctx.batch_fixed(tcpck.OP_FILL, a, L, L, count, None)
+    ok = torch.empty(count, dtype=torch.uint8, device="cuda")
+    ctx.batch_fixed(tcpck.OP_VERIFY, a, L, L, count, ok)
+    assert int(ok.sum().item()) == count
+    del a
+    torch.cuda.empty_cache()
+
+
+# ---- host-memory (end-to-end) path -------------------------------------------------
+
+@pytest.mark.parametrize("op", [0, 1, 2])
+def test_host_batch_fixed_vs_oracle(ctx, oracle_c, op):
+    import tcpck
+    from oracle import ref16 as R
+    rng = np.random.default_rng(300 + op)
+    stride, length, count = 1492, 1492, 50000
+    arena = rng.integers(0, 256, stride * count, dtype=np.uint8)
+    ctx.set_chunk_bytes(8 << 20)  # several chunks, both streams
+    if op == tcpck.OP_VERIFY:
+        for k in range(0, count, 2):
+            R.fill_np(arena[k * stride:(k + 1) * stride])
+    before = arena.copy()
+    out = np.zeros(count, np.uint8 if op == tcpck.OP_VERIFY else np.uint16)
+    ctx.host_batch_fixed(op, arena, stride, length, count, out)
+    if op == tcpck.OP_CHECKSUM:
+        np.testing.assert_array_equal(out, oracle_c.batch(before, stride=stride, length=length, count=count))
+    elif op == tcpck.OP_VERIFY:
+        exp = oracle_c.batch(before, stride=stride, length=length, count=count) == 0
+        np.testing.assert_array_equal(out, exp.astype(np.uint8))
+        assert out[::2].all()
+    else:
+        for k in range(0, count, 101):
+            img = before[k * stride:(k + 1) * stride].copy()
+            assert R.fill_np(img) == out[k]
+            np.testing.assert_array_equal(arena[k * stride:(k + 1) * stride], img)
+
+
+def test_host_batch_var_vs_oracle(ctx, oracle_c):
+    import tcpck
+    import synth_np
+    rng = np.random.default_rng(400)
+    count = 100000
+    off, ln, total = synth_np.mixed_layout(count, seed=7)
+    arena = rng.integers(0, 256, total, dtype=np.uint8)
+    out = np.zeros(count, np.uint16)
+    ctx.set_chunk_bytes(16 << 20)
+    ctx.host_batch_var(tcpck.OP_CHECKSUM, arena, off, ln, count, out)
+    np.testing.assert_array_equal(out, oracle_c.batch(arena, off, ln, threads=8))
