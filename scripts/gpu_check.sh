@@ -1,0 +1,26 @@
+#!/bin/bash
+# One GPU session: parity tests, smoke, bench, rocprofv3 kernel stats.
+# Each GPU step has its own time limit; a fault/abort/timeout ends the session.
+# A plain test failure (exit 1) does not stop the later steps.
+set -u
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+step() {  # step <name> <timeout> <cmd...>
+  local name=$1 t=$2; shift 2
+  echo "== $name: $*"
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"; tail -n 25 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "fatal rc=$rc, stopping"; exit $rc; fi
+  return 0
+}
+for s in ${STEPS:-tests smoke bench prof}; do
+  case $s in
+    tests) step pytest 900 python -m pytest tests -m gpu -x -q ;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) step bench 600 python bench.py ;;
+    bench_c3) step bench_c3 600 python bench.py --config c3 --no-cpu-baseline ;;
+    bench_c4) step bench_c4 600 python bench.py --config c4 --no-cpu-baseline ;;
+    prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-e2e ;;
+  esac
+done
