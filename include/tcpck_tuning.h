@@ -1,0 +1,35 @@
+/*
+ * tcpck_tuning.h -- kernel-selection entry points of libtcpck.so for
+ * benchmarking and tuning.  Not needed by a drop-in caller: tcpck_batch_fixed /
+ * tcpck_batch_var (tcpck.h) pick the kernel themselves.  Results never depend
+ * on the kernel chosen; an inapplicable choice returns an error.
+ */
+#ifndef TCPCK_TUNING_H_
+#define TCPCK_TUNING_H_
+
+#include "tcpck.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TCPCK_KERNEL_AUTO 0 /* library policy (what tcpck_batch_* use)              */
+#define TCPCK_KERNEL_SEG 1  /* G lanes per image, any layout; param = shape + 1
+                               (1: G8/U2, 2: G16/U6, 3: G64/U4, 4: G64/U2,
+                                5: G32/U3, 6: G4/U8), 0 = by length               */
+#define TCPCK_KERNEL_SPAN 2 /* packed images streamed per wave tile, MODE_REF only;
+                               param = images per tile (1..63), 0 = by length     */
+
+int tcpck_batch_fixed_ex(tcpck_ctx *ctx, int op, int mode, void *d_arena,
+                         uint64_t stride, uint32_t len, uint64_t count, void *d_out,
+                         int kernel, int param, tcpck_stream stream);
+int tcpck_batch_var_ex(tcpck_ctx *ctx, int op, int mode, void *d_arena,
+                       const uint64_t *d_offsets, const uint32_t *d_lengths,
+                       uint64_t count, void *d_out, const tcpck_layout *layout,
+                       int kernel, int param, tcpck_stream stream);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+
+#endif /* TCPCK_TUNING_H_ */

@@ -20,6 +20,7 @@ for s in ${STEPS:-tests smoke bench prof}; do
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py ;;
     bench_c3) step bench_c3 600 python bench.py --config c3 --no-cpu-baseline ;;
+    sweep) step sweep 900 python scripts/sweep.py ;;
     bench_c4) step bench_c4 600 python bench.py --config c4 --no-cpu-baseline ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-e2e ;;
   esac

@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "tcpck.h"
+#include "tcpck_tuning.h"
 #include "tcpck_internal.h"
 
 using tcpck::SegArgs;
@@ -27,7 +28,7 @@ using tcpck::SegArgs;
 struct tcpck_ctx {
   int device = 0;
   int num_cus = 256;
-  uint32_t max_blocks = 2048;  // resident 256-thread blocks (8 per CU at <=64 VGPRs)
+
   // end-to-end (host batch) pipeline state, created lazily
   std::mutex mu;
   hipStream_t s[2] = {nullptr, nullptr};
@@ -148,6 +149,71 @@ void free_stage(tcpck_ctx *ctx) {
   }
 }
 
+// ---- kernel selection --------------------------------------------------------
+// span: packed layouts in reference mode (the hot path for MSS-sized images);
+// seg:  everything else (gaps, unordered offsets, tiny images, RFC 1071 mode)
+//       and jumbo images, where one wave per image already streams 16-B-aligned
+//       1 KiB runs.
+constexpr uint64_t kSpanMaxLen = 16384;
+
+hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t stride, uint32_t len,
+                     uint64_t count, void *out, int kernel, int param, hipStream_t s) {
+  const bool span_ok = mode == TCPCK_MODE_REF && stride == len && len >= 16 && len <= (1u << 24);
+  if (kernel == TCPCK_KERNEL_AUTO) kernel = (span_ok && len <= kSpanMaxLen) ? TCPCK_KERNEL_SPAN : TCPCK_KERNEL_SEG;
+  if (kernel == TCPCK_KERNEL_SPAN) {
+    if (!span_ok) return hipErrorInvalidValue;
+    tcpck::SpanArgs a{};
+    a.arena = arena;
+    a.stride = stride;
+    a.count = count;
+    a.out = out;
+    a.tile = param > 0 ? static_cast<uint32_t>(param) : tcpck::span_tile_for_len(len);
+    return tcpck::launch_span(op, true, a, static_cast<uint32_t>(ctx->num_cus), s);
+  }
+  if (kernel != TCPCK_KERNEL_SEG) return hipErrorInvalidValue;
+  SegArgs a{};
+  a.arena = arena;
+  a.stride = stride;
+  a.len = len;
+  a.count = count;
+  a.out = out;
+  const auto shape = param > 0 ? static_cast<tcpck::SegShape>(param - 1) : tcpck::shape_for_len(len);
+  return tcpck::launch_seg(op, mode, true, shape, a, static_cast<uint32_t>(ctx->num_cus), s);
+}
+
+hipError_t run_var(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const uint64_t *off, const uint32_t *len,
+                   uint64_t base, uint64_t count, void *out, const tcpck_layout *layout, int kernel, int param,
+                   hipStream_t s) {
+  const uint64_t typical = (layout && layout->total_bytes) ? layout->total_bytes / count : 1500;
+  const bool span_ok = mode == TCPCK_MODE_REF && layout && (layout->flags & TCPCK_LAYOUT_PACKED) &&
+                       (layout->min_len == 0 || layout->min_len >= 16);
+  if (kernel == TCPCK_KERNEL_AUTO) kernel = (span_ok && typical <= kSpanMaxLen) ? TCPCK_KERNEL_SPAN : TCPCK_KERNEL_SEG;
+  if (kernel == TCPCK_KERNEL_SPAN) {
+    // the kernel re-checks packing and lengths per tile, so a wrong hint
+    // costs speed, never correctness
+    if (mode != TCPCK_MODE_REF) return hipErrorInvalidValue;
+    tcpck::SpanArgs a{};
+    a.arena = arena;
+    a.offsets = off;
+    a.lengths = len;
+    a.base = base;
+    a.count = count;
+    a.out = out;
+    a.tile = param > 0 ? static_cast<uint32_t>(param) : tcpck::span_tile_for_len(typical);
+    return tcpck::launch_span(op, false, a, static_cast<uint32_t>(ctx->num_cus), s);
+  }
+  if (kernel != TCPCK_KERNEL_SEG) return hipErrorInvalidValue;
+  SegArgs a{};
+  a.arena = arena;
+  a.offsets = off;
+  a.lengths = len;
+  a.base = base;
+  a.count = count;
+  a.out = out;
+  const auto shape = param > 0 ? static_cast<tcpck::SegShape>(param - 1) : tcpck::shape_for_len(typical);
+  return tcpck::launch_seg(op, mode, false, shape, a, static_cast<uint32_t>(ctx->num_cus), s);
+}
+
 // Patches bytes 28-29 of host images after a FILL computed on the device
 // (the device filled its staging copy; the host image is the caller's).
 void patch_fields(uint8_t *arena, uint64_t k0, uint64_t n, const uint16_t *res,
@@ -192,7 +258,6 @@ int tcpck_ctx_create(int device, tcpck_ctx **out) {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
     ctx->num_cus = prop.multiProcessorCount;
-  ctx->max_blocks = static_cast<uint32_t>(ctx->num_cus) * 8u;
   *out = ctx;
   return TCPCK_OK;
 }
@@ -256,6 +321,19 @@ uint16_t tcpck_update16(uint16_t checksum, uint16_t old_word, uint16_t new_word,
 // ---- batched, device-resident -------------------------------------------------
 int tcpck_batch_fixed(tcpck_ctx *ctx, int op, int mode, void *d_arena, uint64_t stride,
                       uint32_t len, uint64_t count, void *d_out, tcpck_stream stream) {
+  return tcpck_batch_fixed_ex(ctx, op, mode, d_arena, stride, len, count, d_out, TCPCK_KERNEL_AUTO, 0,
+                              stream);
+}
+
+int tcpck_batch_var(tcpck_ctx *ctx, int op, int mode, void *d_arena, const uint64_t *d_offsets,
+                    const uint32_t *d_lengths, uint64_t count, void *d_out,
+                    const tcpck_layout *layout, tcpck_stream stream) {
+  return tcpck_batch_var_ex(ctx, op, mode, d_arena, d_offsets, d_lengths, count, d_out, layout,
+                            TCPCK_KERNEL_AUTO, 0, stream);
+}
+
+int tcpck_batch_fixed_ex(tcpck_ctx *ctx, int op, int mode, void *d_arena, uint64_t stride, uint32_t len,
+                         uint64_t count, void *d_out, int kernel, int param, tcpck_stream stream) {
   if (!ctx || !valid_op_mode(op, mode)) return TCPCK_EINVAL;
   if (count == 0) return TCPCK_OK;
   if (!d_arena || (len & 1) || (stride & 1) || (count > 1 && stride < len)) return TCPCK_EINVAL;
@@ -264,35 +342,21 @@ int tcpck_batch_fixed(tcpck_ctx *ctx, int op, int mode, void *d_arena, uint64_t 
   if (count > 1 && stride > (UINT64_MAX - len) / (count - 1)) return TCPCK_EINVAL;
   DeviceGuard g(ctx->device);
   if (g.status() != hipSuccess) return hip_status(g.status());
-  SegArgs a{};
-  a.arena = static_cast<uint8_t *>(d_arena);
-  a.stride = stride;
-  a.len = len;
-  a.count = count;
-  a.out = d_out;
-  return hip_status(tcpck::launch_seg(op, mode, true, tcpck::shape_for_len(len), a, ctx->max_blocks,
-                                      static_cast<hipStream_t>(stream)));
+  return hip_status(run_fixed(ctx, op, mode, static_cast<uint8_t *>(d_arena), stride, len, count, d_out,
+                              kernel, param, static_cast<hipStream_t>(stream)));
 }
 
-int tcpck_batch_var(tcpck_ctx *ctx, int op, int mode, void *d_arena, const uint64_t *d_offsets,
-                    const uint32_t *d_lengths, uint64_t count, void *d_out,
-                    const tcpck_layout *layout, tcpck_stream stream) {
+int tcpck_batch_var_ex(tcpck_ctx *ctx, int op, int mode, void *d_arena, const uint64_t *d_offsets,
+                       const uint32_t *d_lengths, uint64_t count, void *d_out, const tcpck_layout *layout,
+                       int kernel, int param, tcpck_stream stream) {
   if (!ctx || !valid_op_mode(op, mode)) return TCPCK_EINVAL;
   if (count == 0) return TCPCK_OK;
   if (!d_arena || !d_offsets || !d_lengths) return TCPCK_EINVAL;
   if (!d_out && op != TCPCK_OP_FILL) return TCPCK_EINVAL;
   DeviceGuard g(ctx->device);
   if (g.status() != hipSuccess) return hip_status(g.status());
-  uint64_t typical = 1500;
-  if (layout && layout->total_bytes) typical = layout->total_bytes / count;
-  SegArgs a{};
-  a.arena = static_cast<uint8_t *>(d_arena);
-  a.offsets = d_offsets;
-  a.lengths = d_lengths;
-  a.count = count;
-  a.out = d_out;
-  return hip_status(tcpck::launch_seg(op, mode, false, tcpck::shape_for_len(typical), a,
-                                      ctx->max_blocks, static_cast<hipStream_t>(stream)));
+  return hip_status(run_var(ctx, op, mode, static_cast<uint8_t *>(d_arena), d_offsets, d_lengths, 0, count,
+                            d_out, layout, kernel, param, static_cast<hipStream_t>(stream)));
 }
 
 // ---- batched, host memory: chunked H2D -> kernel -> D2H on two streams ---------
@@ -325,13 +389,8 @@ int tcpck_host_batch_fixed(tcpck_ctx *ctx, int op, int mode, void *h_arena, uint
     hipStream_t s = ctx->s[slot];
     e = hipMemcpyAsync(ctx->stage[slot], arena + k0 * stride, bytes, hipMemcpyHostToDevice, s);
     if (e != hipSuccess) break;
-    SegArgs a{};
-    a.arena = ctx->stage[slot];
-    a.stride = stride;
-    a.len = len;
-    a.count = n;
-    a.out = ctx->stage_out[slot];
-    e = tcpck::launch_seg(op, mode, true, tcpck::shape_for_len(len), a, ctx->max_blocks, s);
+    e = run_fixed(ctx, op, mode, ctx->stage[slot], stride, len, n, ctx->stage_out[slot], TCPCK_KERNEL_AUTO,
+                  0, s);
     if (e != hipSuccess) break;
     e = hipMemcpyAsync(out_bytes + k0 * es, ctx->stage_out[slot], n * es, hipMemcpyDeviceToHost, s);
   }
@@ -352,11 +411,14 @@ int tcpck_host_batch_var(tcpck_ctx *ctx, int op, int mode, void *h_arena, const 
   if (count == 0) return TCPCK_OK;
   if (!h_arena || !h_offsets || !h_lengths) return TCPCK_EINVAL;
   if (!h_out && op != TCPCK_OP_FILL) return TCPCK_EINVAL;
-  uint64_t max_len = 0;
+  uint64_t max_len = 0, min_len = UINT64_MAX;
+  bool packed = true;
   for (uint64_t k = 0; k < count; ++k) {
     if ((h_offsets[k] | h_lengths[k]) & 1) return TCPCK_EINVAL;
     if (op == TCPCK_OP_FILL && h_lengths[k] < 30) return TCPCK_EINVAL;
     max_len = std::max<uint64_t>(max_len, h_lengths[k]);
+    min_len = std::min<uint64_t>(min_len, h_lengths[k]);
+    if (k + 1 < count && h_offsets[k] + h_lengths[k] != h_offsets[k + 1]) packed = false;
   }
   std::lock_guard<std::mutex> lk(ctx->mu);
   DeviceGuard g(ctx->device);
@@ -372,7 +434,11 @@ int tcpck_host_batch_var(tcpck_ctx *ctx, int op, int mode, void *h_arena, const 
   const size_t es = out_elem(op);
   uint64_t total_bytes = 0;
   for (uint64_t k = 0; k < count; ++k) total_bytes += h_lengths[k];
-  const tcpck::SegShape shape = tcpck::shape_for_len(total_bytes / count);
+  tcpck_layout lay{};
+  lay.total_bytes = total_bytes;
+  lay.min_len = static_cast<uint32_t>(std::min<uint64_t>(min_len, UINT32_MAX));
+  lay.max_len = static_cast<uint32_t>(std::min<uint64_t>(max_len, UINT32_MAX));
+  lay.flags = packed ? TCPCK_LAYOUT_PACKED : 0u;
   hipError_t e = hipSuccess;
   uint64_t c = 0;
   for (uint64_t k0 = 0; k0 < count && e == hipSuccess; ++c) {
@@ -396,14 +462,8 @@ int tcpck_host_batch_var(tcpck_ctx *ctx, int op, int mode, void *h_arena, const 
     if (e == hipSuccess)
       e = hipMemcpyAsync(ctx->stage_len[slot], h_lengths + k0, n * 4, hipMemcpyHostToDevice, s);
     if (e != hipSuccess) break;
-    SegArgs a{};
-    a.arena = ctx->stage[slot];
-    a.offsets = ctx->stage_off[slot];
-    a.lengths = ctx->stage_len[slot];
-    a.base = lo;
-    a.count = n;
-    a.out = ctx->stage_out[slot];
-    e = tcpck::launch_seg(op, mode, false, shape, a, ctx->max_blocks, s);
+    e = run_var(ctx, op, mode, ctx->stage[slot], ctx->stage_off[slot], ctx->stage_len[slot], lo, n,
+                ctx->stage_out[slot], &lay, TCPCK_KERNEL_AUTO, 0, s);
     if (e != hipSuccess) break;
     e = hipMemcpyAsync(out_bytes + k0 * es, ctx->stage_out[slot], n * es, hipMemcpyDeviceToHost, s);
     k0 = k1;

@@ -1,0 +1,172 @@
+// tcpck_device.h -- device helpers shared by the gfx950 checksum kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "tcpck_internal.h"
+
+namespace tcpck {
+namespace dev {
+
+using u32x4 = __attribute__((ext_vector_type(4))) unsigned int;
+
+constexpr int kBlock = 256;
+constexpr int kWavesPerBlock = kBlock / 64;
+
+// 256-thread blocks of `kernel` resident per CU (occupancy query, >= 1).  The
+// grid-stride kernels launch exactly num_cus x this many blocks, so every block
+// starts at once and none waits for a slot (no second, tail wave of blocks).
+template <typename Kernel>
+inline uint32_t resident_blocks_per_cu(Kernel kernel) {
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, kBlock, 0) != hipSuccess || nb < 1) nb = 1;
+  return static_cast<uint32_t>(nb);
+}
+
+// 16-byte streaming load, nontemporal (global_load_dwordx4 ... nt): the batch
+// is read exactly once, so keep it from displacing other lines.
+__device__ __forceinline__ u32x4 load16_nt(const uint8_t *p) {
+  return __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
+}
+
+// Word-validity mask of a 16-byte chunk for the byte range [lo, hi) (both even,
+// clamped to [0, 16]) -> 8-bit mask, bit i = u16 word i valid.
+__device__ __forceinline__ uint32_t word_mask(int32_t lo, int32_t hi) {
+  return ((1u << (hi >> 1)) - 1u) & ~((1u << (lo >> 1)) - 1u);
+}
+
+// 8-bit word mask -> AND mask for dword j of the chunk.
+__device__ __forceinline__ uint32_t dword_mask(uint32_t wm, int j) {
+  const uint32_t t = (wm >> (2 * j)) & 3u;
+  return ((t & 1u) ? 0x0000FFFFu : 0u) | ((t & 2u) ? 0xFFFF0000u : 0u);
+}
+
+__device__ __forceinline__ u32x4 apply_mask(u32x4 w, uint32_t wm) {
+  w.x &= dword_mask(wm, 0);
+  w.y &= dword_mask(wm, 1);
+  w.z &= dword_mask(wm, 2);
+  w.w &= dword_mask(wm, 3);
+  return w;
+}
+
+// Reference arithmetic (tcp-header.h:257-258): only the low 16 bits of the
+// accumulator matter, so each dword adds both of its u16 halves as w + (w >> 16)
+// (the high half's own carries land above bit 15).  Wrapping u32 adds keep the
+// low 16 bits exact for any number of terms.
+__device__ __forceinline__ uint32_t ref_add(uint32_t acc, uint32_t w) { return acc + w + (w >> 16); }
+
+__device__ __forceinline__ uint32_t ref_chunk_sum(u32x4 w) {
+  return ref_add(ref_add(ref_add(w.x + (w.x >> 16), w.y), w.z), w.w);
+}
+
+// RFC 1071: 32-bit one's-complement add (2^32 == 1 mod 0xFFFF).
+__device__ __forceinline__ uint32_t rfc_add(uint32_t acc, uint32_t w) {
+  const uint32_t s = acc + w;
+  return s + (s < w ? 1u : 0u);
+}
+
+template <int MODE>
+__device__ __forceinline__ uint32_t accumulate(uint32_t acc, uint32_t w) {
+  if constexpr (MODE == kRef) {
+    return ref_add(acc, w);
+  } else {
+    return rfc_add(acc, w);
+  }
+}
+
+// Folds an accumulator to 16 significant bits: unchanged mod 2^16 (REF), or
+// mod 0xFFFF keeping zero-ness (RFC 1071).
+template <int MODE>
+__device__ __forceinline__ uint32_t fold_lane(uint32_t acc) {
+  if constexpr (MODE == kRef) {
+    return acc & 0xFFFFu;
+  } else {
+    acc = (acc & 0xFFFFu) + (acc >> 16);
+    return (acc & 0xFFFFu) + (acc >> 16);
+  }
+}
+
+template <int MODE>
+__device__ __forceinline__ uint16_t finish(uint32_t sum) {
+  if constexpr (MODE == kRef) {
+    return static_cast<uint16_t>(~sum);  // tcp-header.h:262: ~ truncated to u16, no fold
+  } else {
+    sum = (sum & 0xFFFFu) + (sum >> 16);
+    sum = (sum & 0xFFFFu) + (sum >> 16);
+    return static_cast<uint16_t>(~sum);
+  }
+}
+
+template <int G>
+__device__ __forceinline__ uint32_t group_sum(uint32_t x) {
+#pragma unroll
+  for (int m = G / 2; m >= 1; m >>= 1) x += __shfl_xor(x, m, 64);
+  return x;
+}
+
+// 64-lane inclusive prefix sum with DPP (gfx9 family): row_shr 1,2,4,8 builds
+// 16-lane scans, row_bcast:15 / row_bcast:31 carry rows into the rows above.
+__device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t x) {
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, false);  // row_shr:1
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, false);  // row_shr:2
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, false);  // row_shr:4
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, false);  // row_shr:8
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);  // row_bcast:15
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);  // row_bcast:31
+  return x;
+}
+
+__device__ __forceinline__ uint32_t read_lane(uint32_t x, uint32_t lane) {
+  return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(x), static_cast<int>(lane)));
+}
+
+__device__ __forceinline__ uint64_t read_lane64(uint64_t x, uint32_t lane) {
+  const uint32_t lo = read_lane(static_cast<uint32_t>(x), lane);
+  const uint32_t hi = read_lane(static_cast<uint32_t>(x >> 32), lane);
+  return (static_cast<uint64_t>(hi) << 32) | lo;
+}
+
+// Sum (REF arithmetic, low 16 bits meaningful) of the image [start, start+len)
+// computed by one whole wave (64 lanes x U loads of 16 B in flight); the word at
+// byte `start + 28` is excluded when exclude_field (send-side fill).  Result is
+// the same in every lane.
+template <int U, int MODE>
+__device__ __forceinline__ uint32_t wave_image_sum(const uint8_t *arena, uint64_t start, uint32_t len,
+                                                   bool exclude_field) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint8_t *p0 = arena + (start & ~uint64_t{15});
+  const int32_t lead = static_cast<int32_t>(start & 15);
+  const int64_t span64 = lead + static_cast<int64_t>(len);
+  const uint32_t nch = static_cast<uint32_t>((span64 + 15) >> 4);
+  const int64_t field = exclude_field ? lead + 28 : -64;
+  uint32_t acc = 0;
+  for (uint32_t i0 = lane; i0 < nch; i0 += 64 * U) {
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t i = i0 + u * 64;
+      v[u] = load16_nt(p0 + 16 * static_cast<uint64_t>(i < nch ? i : nch - 1));
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t rel = 16 * static_cast<int64_t>(i0 + u * 64);
+      const int32_t lo = static_cast<int32_t>(min(max(lead - rel, int64_t{0}), int64_t{16}));
+      const int32_t hi = static_cast<int32_t>(min(max(span64 - rel, int64_t{0}), int64_t{16}));
+      uint32_t wm = word_mask(lo, hi);
+      const int64_t fb = field - rel;
+      if (fb >= 0 && fb < 16) wm &= ~(1u << (fb >> 1));
+      u32x4 w = v[u];
+      if (wm != 0xFFu) w = apply_mask(w, wm);
+      acc = accumulate<MODE>(acc, w.x);
+      acc = accumulate<MODE>(acc, w.y);
+      acc = accumulate<MODE>(acc, w.z);
+      acc = accumulate<MODE>(acc, w.w);
+    }
+    if (MODE == kRfc1071) acc = fold_lane<MODE>(acc);
+  }
+  return group_sum<64>(fold_lane<MODE>(acc));
+}
+
+}  // namespace dev
+}  // namespace tcpck

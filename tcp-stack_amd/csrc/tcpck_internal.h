@@ -1,5 +1,5 @@
 // tcpck_internal.h -- private interface between the C-ABI layer (tcpck_api.hip)
-// and the gfx950 kernels (tcpck_kernels.hip).  Not installed, not part of the ABI.
+// and the gfx950 kernels (tcpck_kernels.hip, tcpck_span.hip).  Not installed.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -10,13 +10,15 @@ namespace tcpck {
 enum Op : int { kChecksum = 0, kFill = 1, kVerify = 2 };
 enum Mode : int { kRef = 0, kRfc1071 = 1 };
 
-// Kernel shapes for the image-per-group kernel: G lanes cooperate on one
-// image, each lane keeps U 16-byte loads in flight per step.
+// ---- seg kernel: any layout, G lanes per image, U loads of 16 B in flight ----
 enum SegShape : int {
   kShapeSmall = 0,   // G = 8,  U = 2  : images up to ~256 B
-  kShapeMss = 1,     // G = 16, U = 6  : images up to ~2 KiB (Ethernet MSS)
+  kShapeMss = 1,     // G = 16, U = 6  : images up to ~4 KiB (Ethernet MSS)
   kShapeJumbo = 2,   // G = 64, U = 4  : larger images (64 KiB jumbo)
-  kNumShapes = 3
+  kShapeWave2 = 3,   // G = 64, U = 2  : tuning
+  kShapeG32 = 4,     // G = 32, U = 3  : tuning
+  kShapeG4 = 5,      // G = 4,  U = 8  : tuning
+  kNumShapes = 6
 };
 
 struct SegArgs {
@@ -30,12 +32,23 @@ struct SegArgs {
   uint32_t len;              // fixed layout: image length
 };
 
-// Chooses the shape from a representative image length.
 SegShape shape_for_len(uint64_t typical_len);
-
-// Launches the image-per-group kernel.  `max_blocks` caps the grid (the
-// kernel grid-strides over images).
 hipError_t launch_seg(int op, int mode, bool fixed, SegShape shape, const SegArgs &a,
-                      uint32_t max_blocks, hipStream_t stream);
+                      uint32_t num_cus, hipStream_t stream);
+
+// ---- span kernel: packed layouts, reference mode, tiles of whole images ------
+struct SpanArgs {
+  uint8_t *arena;
+  const uint64_t *offsets;   // variable layout (packed: offsets[k+1] == offsets[k] + lengths[k])
+  const uint32_t *lengths;
+  uint64_t stride;           // fixed layout: stride == image length (packed)
+  uint64_t base;
+  uint64_t count;
+  void *out;
+  uint32_t tile;             // images per wave tile, 1..63
+};
+
+uint32_t span_tile_for_len(uint64_t typical_len);
+hipError_t launch_span(int op, bool fixed, const SpanArgs &a, uint32_t num_cus, hipStream_t stream);
 
 }  // namespace tcpck

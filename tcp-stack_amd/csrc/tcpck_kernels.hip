@@ -1,18 +1,20 @@
-// tcpck_kernels.hip -- gfx950 (CDNA4) kernels for the batched TCP checksum.
+// tcpck_kernels.hip -- the image-per-group ("seg") kernel: any layout.
 //
-// Semantics (parity mode, Mode::kRef): the reference's CalculateChecksum,
+// Semantics (parity mode, kRef): the reference's CalculateChecksum,
 // filixi/TCP-stack include/tcp-header.h:252-263 -- little-endian u16 words
 // summed into a u32 with no end-around carry, result ~sum truncated to u16,
-// i.e. ~(sum mod 2^16).  Mode::kRfc1071 is the opt-in one's-complement sum.
+// i.e. ~(sum mod 2^16).  kRfc1071 is the opt-in one's-complement sum.
 //
+// This kernel accepts every layout the C ABI allows (fixed stride with gaps,
+// arbitrary even offsets/lengths in any order, zero-length images, both
+// modes); the packed-layout fast path is the span kernel (tcpck_span.hip).
 // Shape of the work: a pure HBM-read streaming reduction (~0.5 integer add per
-// byte, far below any compute roof; no MFMA).  What matters is bytes in flight
-// and coalescing:
+// byte, no MFMA):
 //   * G consecutive lanes own one image; lane l of the group reads the image's
 //     16-byte chunks l, l+G, l+2G, ... so one wave-instruction reads 64/G
 //     contiguous runs of G*16 bytes (1 KiB per wave-instruction in total);
 //   * each lane issues U 16-byte nontemporal loads back to back before it
-//     consumes any of them (U*1 KiB in flight per wave, ~32 waves per CU);
+//     consumes any of them (U KiB in flight per wave, 32 waves per CU);
 //   * chunk addresses past the image end are clamped to the image's last
 //     chunk (always a legal address) and their words masked to zero, so the
 //     loads are unconditional: no per-load branch, no per-load vmcnt(0);
@@ -20,74 +22,17 @@
 //     start rounded down to 16 B and its leading words are masked, the last
 //     chunk's trailing words likewise (word-granular masks: even lengths that
 //     are 2 mod 4 are exact);
-//   * the per-lane accumulator is a u32: acc += w + (w >> 16) per dword w
-//     keeps the low 16 bits equal to the sum of both u16 halves mod 2^16
-//     (the high half's carries land above bit 15 and are discarded), which is
-//     exactly the reference's arithmetic; RFC 1071 mode uses a u32 add with
-//     end-around carry (2^32 == 1 mod 0xFFFF);
 //   * the G partial sums are combined with cross-lane xor shuffles, and lane 0
-//     of the group stores the 2-byte result (or, for kFill, also writes it
-//     into bytes 28-29 of the image; for kVerify stores checksum == 0).
-#include "tcpck_internal.h"
+//     of the group stores the 2-byte result (kFill also writes it into bytes
+//     28-29 of the image, tcp-header.h:177; kVerify stores checksum == 0).
+#include "tcpck_device.h"
 
 namespace tcpck {
 
 namespace {
 
-using u32x4 = __attribute__((ext_vector_type(4))) unsigned int;
-
-constexpr int kBlock = 256;
-
-__device__ __forceinline__ u32x4 load16_nt(const uint8_t *p) {
-  return __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
-}
-
-// 8-bit word-validity mask of one 16-byte chunk -> AND mask of dword j.
-__device__ __forceinline__ uint32_t dword_mask(uint32_t wm, int j) {
-  const uint32_t t = (wm >> (2 * j)) & 3u;
-  return ((t & 1u) ? 0x0000FFFFu : 0u) | ((t & 2u) ? 0xFFFF0000u : 0u);
-}
-
-template <int MODE>
-__device__ __forceinline__ uint32_t accumulate(uint32_t acc, uint32_t w) {
-  if constexpr (MODE == kRef) {
-    return acc + w + (w >> 16);
-  } else {
-    // one's-complement 32-bit add: fold the carry back in (2^32 == 1 mod 0xFFFF)
-    const uint32_t s = acc + w;
-    return s + (s < w ? 1u : 0u);
-  }
-}
-
-// Folds a per-lane accumulator to 16 significant bits without changing the
-// value mod 2^16 (REF) or mod 0xFFFF keeping zero-ness (RFC 1071).
-template <int MODE>
-__device__ __forceinline__ uint32_t fold_lane(uint32_t acc) {
-  if constexpr (MODE == kRef) {
-    return acc & 0xFFFFu;
-  } else {
-    acc = (acc & 0xFFFFu) + (acc >> 16);
-    return (acc & 0xFFFFu) + (acc >> 16);
-  }
-}
-
-template <int MODE>
-__device__ __forceinline__ uint16_t finish(uint32_t sum) {
-  if constexpr (MODE == kRef) {
-    return static_cast<uint16_t>(~sum);  // tcp-header.h:262
-  } else {
-    sum = (sum & 0xFFFFu) + (sum >> 16);
-    sum = (sum & 0xFFFFu) + (sum >> 16);
-    return static_cast<uint16_t>(~sum);
-  }
-}
-
-template <int G>
-__device__ __forceinline__ uint32_t group_sum(uint32_t x) {
-#pragma unroll
-  for (int m = G / 2; m >= 1; m >>= 1) x += __shfl_xor(x, m, 64);
-  return x;
-}
+using dev::kBlock;
+using dev::u32x4;
 
 template <int G, int U, int MODE, int OP, bool FIXED>
 __global__ void __launch_bounds__(kBlock) seg_kernel(SegArgs a) {
@@ -99,10 +44,10 @@ __global__ void __launch_bounds__(kBlock) seg_kernel(SegArgs a) {
     const uint64_t start = FIXED ? k * a.stride : a.offsets[k] - a.base;
     const uint32_t len = FIXED ? a.len : a.lengths[k];
     const uint8_t *p0 = a.arena + (start & ~uint64_t{15});
-    const int32_t lead = static_cast<int32_t>(start & 15);      // masked bytes before the image
-    const int32_t span = lead + static_cast<int32_t>(len);      // bytes from p0 to the image end
-    const uint32_t nch = static_cast<uint32_t>(span + 15) >> 4;  // 16-byte chunks touched
-    const int32_t field = (OP == kFill) ? lead + 28 : -64;       // checksum field, counts as 0
+    const int64_t lead = static_cast<int64_t>(start & 15);    // masked bytes before the image
+    const int64_t span = lead + static_cast<int64_t>(len);    // bytes from p0 to the image end
+    const uint32_t nch = static_cast<uint32_t>((span + 15) >> 4);  // 16-byte chunks touched
+    const int64_t field = (OP == kFill) ? lead + 28 : -64;    // checksum field counts as 0
 
     uint32_t acc = 0;
     for (uint32_t i0 = gl; i0 < nch; i0 += G * U) {
@@ -111,35 +56,30 @@ __global__ void __launch_bounds__(kBlock) seg_kernel(SegArgs a) {
       for (int u = 0; u < U; ++u) {
         const uint32_t i = i0 + u * G;
         const uint32_t ic = i < nch ? i : nch - 1;  // clamp: always a legal address
-        v[u] = load16_nt(p0 + 16 * static_cast<uint64_t>(ic));
+        v[u] = dev::load16_nt(p0 + 16 * static_cast<uint64_t>(ic));
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int32_t rel = static_cast<int32_t>(16 * (i0 + u * G));
-        const int32_t lo = min(max(lead - rel, 0), 16);
-        const int32_t hi = min(max(span - rel, 0), 16);
-        uint32_t wm = ((1u << (hi >> 1)) - 1u) & ~((1u << (lo >> 1)) - 1u);
+        const int64_t rel = 16 * static_cast<int64_t>(i0 + u * G);
+        const int32_t lo = static_cast<int32_t>(min(max(lead - rel, int64_t{0}), int64_t{16}));
+        const int32_t hi = static_cast<int32_t>(min(max(span - rel, int64_t{0}), int64_t{16}));
+        uint32_t wm = dev::word_mask(lo, hi);
         if (OP == kFill) {
-          const int32_t fb = field - rel;
+          const int64_t fb = field - rel;
           if (fb >= 0 && fb < 16) wm &= ~(1u << (fb >> 1));
         }
         u32x4 w = v[u];
-        if (wm != 0xFFu) {
-          w.x &= dword_mask(wm, 0);
-          w.y &= dword_mask(wm, 1);
-          w.z &= dword_mask(wm, 2);
-          w.w &= dword_mask(wm, 3);
-        }
-        acc = accumulate<MODE>(acc, w.x);
-        acc = accumulate<MODE>(acc, w.y);
-        acc = accumulate<MODE>(acc, w.z);
-        acc = accumulate<MODE>(acc, w.w);
+        if (wm != 0xFFu) w = dev::apply_mask(w, wm);
+        acc = dev::accumulate<MODE>(acc, w.x);
+        acc = dev::accumulate<MODE>(acc, w.y);
+        acc = dev::accumulate<MODE>(acc, w.z);
+        acc = dev::accumulate<MODE>(acc, w.w);
       }
-      if (MODE == kRfc1071) acc = fold_lane<MODE>(acc);
+      if (MODE == kRfc1071) acc = dev::fold_lane<MODE>(acc);
     }
-    const uint32_t sum = group_sum<G>(fold_lane<MODE>(acc));
+    const uint32_t sum = dev::group_sum<G>(dev::fold_lane<MODE>(acc));
     if (gl == 0) {
-      const uint16_t c = finish<MODE>(sum);
+      const uint16_t c = dev::finish<MODE>(sum);
       if constexpr (OP == kVerify) {
         static_cast<uint8_t *>(a.out)[k] = (c == 0) ? 1 : 0;
       } else {
@@ -152,9 +92,12 @@ __global__ void __launch_bounds__(kBlock) seg_kernel(SegArgs a) {
 }
 
 template <int G, int U, int MODE, int OP, bool FIXED>
-hipError_t launch_one(const SegArgs &a, uint32_t max_blocks, hipStream_t stream) {
+hipError_t launch_one(const SegArgs &a, uint32_t num_cus, hipStream_t stream) {
   const uint64_t groups_per_block = kBlock / G;
   uint64_t blocks = (a.count + groups_per_block - 1) / groups_per_block;
+  // grid-stride kernel: launch exactly the resident blocks, never a second wave of them
+  static const uint32_t per_cu = dev::resident_blocks_per_cu(seg_kernel<G, U, MODE, OP, FIXED>);
+  const uint64_t max_blocks = static_cast<uint64_t>(per_cu) * num_cus;
   if (blocks > max_blocks) blocks = max_blocks;
   if (blocks == 0) return hipSuccess;
   hipLaunchKernelGGL((seg_kernel<G, U, MODE, OP, FIXED>), dim3(static_cast<uint32_t>(blocks)),
@@ -194,11 +137,14 @@ SegShape shape_for_len(uint64_t typical_len) {
 }
 
 hipError_t launch_seg(int op, int mode, bool fixed, SegShape shape, const SegArgs &a,
-                      uint32_t max_blocks, hipStream_t stream) {
+                      uint32_t num_cus, hipStream_t stream) {
   switch (shape) {
-    case kShapeSmall: return dispatch_mode<8, 2>(mode, op, fixed, a, max_blocks, stream);
-    case kShapeMss: return dispatch_mode<16, 6>(mode, op, fixed, a, max_blocks, stream);
-    case kShapeJumbo: return dispatch_mode<64, 4>(mode, op, fixed, a, max_blocks, stream);
+    case kShapeSmall: return dispatch_mode<8, 2>(mode, op, fixed, a, num_cus, stream);
+    case kShapeMss: return dispatch_mode<16, 6>(mode, op, fixed, a, num_cus, stream);
+    case kShapeJumbo: return dispatch_mode<64, 4>(mode, op, fixed, a, num_cus, stream);
+    case kShapeWave2: return dispatch_mode<64, 2>(mode, op, fixed, a, num_cus, stream);
+    case kShapeG32: return dispatch_mode<32, 3>(mode, op, fixed, a, num_cus, stream);
+    case kShapeG4: return dispatch_mode<4, 8>(mode, op, fixed, a, num_cus, stream);
     default: return hipErrorInvalidValue;
   }
 }

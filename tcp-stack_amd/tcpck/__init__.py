@@ -35,6 +35,13 @@ OP_VERIFY = 2
 
 LAYOUT_PACKED = 1
 
+# include/tcpck_tuning.h
+KERNEL_AUTO = 0
+KERNEL_SEG = 1    # param: seg shape + 1 (1..6), 0 = by length
+KERNEL_SPAN = 2   # param: images per tile (1..63), 0 = by length
+SEG_SHAPES = {1: "G8/U2", 2: "G16/U6", 3: "G64/U4", 4: "G64/U2", 5: "G32/U3", 6: "G4/U8"}
+TUNING_EXPORTS = ("tcpck_batch_fixed_ex", "tcpck_batch_var_ex")
+
 # Every symbol include/tcpck.h declares (checked by tests/test_abi.py).
 EXPORTS = (
     "tcpck_abi_version", "tcpck_strerror", "tcpck_device_supported",
@@ -96,6 +103,9 @@ def lib() -> ctypes.CDLL:
         "tcpck_stream_sync": (i32, [vp, vp]),
         "tcpck_synth_fixed": (i32, [vp, u64, u32, u64, u64, u64, i32, vp]),
         "tcpck_synth_var": (i32, [vp, vp, vp, u32, u64, u64, u64, i32, vp]),
+        # include/tcpck_tuning.h
+        "tcpck_batch_fixed_ex": (i32, [vp, i32, i32, vp, u64, u32, u64, vp, i32, i32, vp]),
+        "tcpck_batch_var_ex": (i32, [vp, i32, i32, vp, vp, vp, u64, vp, ctypes.POINTER(Layout), i32, i32, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -219,6 +229,20 @@ class Context:
         _check(lib().tcpck_batch_var(self._h, op, mode, _ptr(arena), _ptr(offsets), _ptr(lengths),
                                      count, _ptr(out), ctypes.byref(lay), _stream(stream)),
                "tcpck_batch_var")
+
+    # explicit kernel choice (include/tcpck_tuning.h)
+    def batch_fixed_ex(self, op: int, arena, stride: int, length: int, count: int, out, kernel: int,
+                       param: int = 0, mode: int = MODE_REF, stream=None) -> None:
+        _check(lib().tcpck_batch_fixed_ex(self._h, op, mode, _ptr(arena), stride, length, count,
+                                          _ptr(out), kernel, param, _stream(stream)), "tcpck_batch_fixed_ex")
+
+    def batch_var_ex(self, op: int, arena, offsets, lengths, count: int, out, kernel: int,
+                     param: int = 0, mode: int = MODE_REF, total_bytes: int = 0, min_len: int = 0,
+                     max_len: int = 0, packed: bool = False, stream=None) -> None:
+        lay = Layout(total_bytes, min_len, max_len, LAYOUT_PACKED if packed else 0, 0)
+        _check(lib().tcpck_batch_var_ex(self._h, op, mode, _ptr(arena), _ptr(offsets), _ptr(lengths),
+                                        count, _ptr(out), ctypes.byref(lay), kernel, param,
+                                        _stream(stream)), "tcpck_batch_var_ex")
 
     # host-memory batches (end to end, PCIe included)
     def host_batch_fixed(self, op: int, arena, stride: int, length: int, count: int, out,

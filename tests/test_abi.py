@@ -10,19 +10,21 @@ import pytest
 from conftest import ROOT
 
 
-def declared_symbols():
-    with open(os.path.join(ROOT, "include", "tcpck.h")) as f:
+def declared_symbols(header="tcpck.h"):
+    with open(os.path.join(ROOT, "include", header)) as f:
         text = f.read()
-    return sorted(set(re.findall(r"\b(tcpck_[a-z0-9_]+)\s*\(", text)))
+    decl = r"^(?:int|uint16_t|const char \*)\s*(tcpck_[a-z0-9_]+)\s*\("
+    return sorted(set(re.findall(decl, text, flags=re.M)))
 
 
 def test_header_and_binding_agree(built_lib):
     import tcpck
     assert declared_symbols() == sorted(tcpck.EXPORTS)
+    assert declared_symbols("tcpck_tuning.h") == sorted(tcpck.TUNING_EXPORTS)
 
 
 def test_library_exports_every_declared_symbol(built_lib):
-    for name in declared_symbols():
+    for name in declared_symbols() + declared_symbols("tcpck_tuning.h"):
         assert hasattr(built_lib, name), name
     assert built_lib.tcpck_abi_version() == 1
 

@@ -1,0 +1,148 @@
+"""GPU parity of every kernel variant (include/tcpck_tuning.h): each seg shape
+and span tile size must give the reference's answers bit for bit, including the
+span kernel's in-launch fallback for tiles that are not packed."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+SEG = [1, 2, 3, 4, 5, 6]
+TILES = [1, 2, 7, 16, 33, 63]
+
+
+@pytest.fixture(scope="module")
+def ctx(built_lib):
+    import tcpck
+    assert torch.cuda.is_available()
+    c = tcpck.Context(0)
+    yield c
+    c.close()
+
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def host(t):
+    torch.cuda.synchronize()
+    return t.cpu().numpy()
+
+
+def variants():
+    import tcpck
+    return [(tcpck.KERNEL_SEG, p) for p in SEG] + [(tcpck.KERNEL_SPAN, t) for t in TILES]
+
+
+def packed_golden(golden):
+    """All golden checksum images of length >= 16, re-packed back to back."""
+    cases = [c for c in golden.by_kind("checksum") if c["len"] >= 16]
+    imgs = [golden.image(c) for c in cases]
+    ln = np.array([c["len"] for c in cases], np.uint32)
+    off = np.zeros(len(cases), np.uint64)
+    off[1:] = np.cumsum(ln[:-1].astype(np.uint64))
+    return np.concatenate(imgs), off, ln, np.array([c["expected"] for c in cases], np.uint16)
+
+
+@pytest.mark.parametrize("kernel,param", variants())
+def test_packed_golden_all_kernels(ctx, golden, kernel, param):
+    import tcpck
+    arena, off, ln, exp = packed_golden(golden)
+    out = torch.empty(len(exp), dtype=torch.int16, device="cuda")
+    ctx.batch_var_ex(tcpck.OP_CHECKSUM, dev(arena), dev(off), dev(ln), len(exp), out, kernel, param,
+                     packed=True)
+    np.testing.assert_array_equal(host(out).view(np.uint16), exp)
+
+
+@pytest.mark.parametrize("kernel,param", variants())
+@pytest.mark.parametrize("length", [16, 32, 96, 606, 1492, 1494, 4096])
+def test_fixed_packed_all_kernels(ctx, oracle_c, kernel, param, length):
+    import tcpck
+    rng = np.random.default_rng(length + param)
+    count = 3001
+    arena_np = rng.integers(0, 256, count * length, dtype=np.uint8)
+    arena_np[length * 5:length * 6] = 0xFF
+    out = torch.empty(count, dtype=torch.int16, device="cuda")
+    ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, dev(arena_np), length, length, count, out, kernel, param)
+    exp = oracle_c.batch(arena_np, stride=length, length=length, count=count, threads=8)
+    np.testing.assert_array_equal(host(out).view(np.uint16), exp)
+
+
+@pytest.mark.parametrize("tile", TILES)
+def test_span_var_mixed_and_fallback(ctx, oracle_c, tile):
+    """Packed C3-style batch with some non-packed and short regions mixed in."""
+    import tcpck
+    import synth_np
+    rng = np.random.default_rng(tile)
+    count = 20000
+    off, ln, total = synth_np.mixed_layout(count, seed=tile)
+    # break packing in a few places (gaps) and shrink a few images below 16 B
+    off = off.copy()
+    ln = ln.copy()
+    for k in rng.integers(1, count, 40):
+        off[k:] += 6
+    ln[rng.integers(0, count, 15)] = 8
+    total = int(off[-1] + ln[-1]) + 64
+    arena_np = rng.integers(0, 256, total, dtype=np.uint8)
+    out = torch.empty(count, dtype=torch.int16, device="cuda")
+    ctx.batch_var_ex(tcpck.OP_CHECKSUM, dev(arena_np), dev(off), dev(ln), count, out,
+                     tcpck.KERNEL_SPAN, tile, packed=True)
+    exp = oracle_c.batch(arena_np, off, ln, threads=8)
+    np.testing.assert_array_equal(host(out).view(np.uint16), exp)
+
+
+@pytest.mark.parametrize("tile", [1, 16, 63])
+@pytest.mark.parametrize("fixed", [True, False])
+def test_span_fill_verify(ctx, oracle_c, tile, fixed):
+    import tcpck
+    import synth_np
+    from oracle import ref16 as R
+    rng = np.random.default_rng(50 + tile)
+    if fixed:
+        L, count = 1492, 4000
+        off = (np.arange(count, dtype=np.uint64) * L)
+        ln = np.full(count, L, np.uint32)
+        total = L * count
+    else:
+        count = 4000
+        off, ln, total = synth_np.mixed_layout(count, seed=tile)
+    arena_np = rng.integers(0, 256, total, dtype=np.uint8)
+    arena = dev(arena_np)
+    out = torch.empty(count, dtype=torch.int16, device="cuda")
+    if fixed:
+        ctx.batch_fixed_ex(tcpck.OP_FILL, arena, L, L, count, out, tcpck.KERNEL_SPAN, tile)
+    else:
+        ctx.batch_var_ex(tcpck.OP_FILL, arena, dev(off), dev(ln), count, out, tcpck.KERNEL_SPAN, tile,
+                         packed=True)
+    got = host(arena)
+    exp_arena = arena_np.copy()
+    exp = np.empty(count, np.uint16)
+    for k in range(count):
+        o, n = int(off[k]), int(ln[k])
+        exp[k] = R.fill_np(exp_arena[o:o + n])
+    np.testing.assert_array_equal(host(out).view(np.uint16), exp)
+    np.testing.assert_array_equal(got, exp_arena)
+    ok = torch.empty(count, dtype=torch.uint8, device="cuda")
+    bad = rng.choice(count, 50, replace=False)
+    for k in bad:
+        got[int(off[k]) + int(rng.integers(0, int(ln[k])))] ^= 0x11
+    arena2 = dev(got)
+    if fixed:
+        ctx.batch_fixed_ex(tcpck.OP_VERIFY, arena2, L, L, count, ok, tcpck.KERNEL_SPAN, tile)
+    else:
+        ctx.batch_var_ex(tcpck.OP_VERIFY, arena2, dev(off), dev(ln), count, ok, tcpck.KERNEL_SPAN, tile,
+                         packed=True)
+    np.testing.assert_array_equal(np.nonzero(host(ok) == 0)[0], np.unique(bad))
+
+
+def test_span_rejects_rfc_and_gaps(ctx):
+    import tcpck
+    a = torch.zeros(1 << 16, dtype=torch.uint8, device="cuda")
+    o = torch.zeros(64, dtype=torch.int16, device="cuda")
+    with pytest.raises(tcpck.TcpckError):
+        ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, a, 1000, 1000, 8, o, tcpck.KERNEL_SPAN, 4, mode=1)
+    with pytest.raises(tcpck.TcpckError):
+        ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, a, 1000, 996, 8, o, tcpck.KERNEL_SPAN, 4)
+    with pytest.raises(tcpck.TcpckError):
+        ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, a, 1000, 1000, 8, o, tcpck.KERNEL_SPAN, 64)
