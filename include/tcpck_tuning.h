@@ -19,6 +19,9 @@ extern "C" {
                                 5: G32/U3, 6: G4/U8), 0 = by length               */
 #define TCPCK_KERNEL_SPAN 2 /* packed images streamed per wave tile, MODE_REF only;
                                param = images per tile (1..63), 0 = by length     */
+#define TCPCK_KERNEL_STREAM 3 /* packed images, one byte-balanced run per wave,
+                                 MODE_REF only; param = variant (0: 4 loads in
+                                 flight nt, 1: 8 nt, 2: 4 plain, 3: 2 nt)        */
 
 int tcpck_batch_fixed_ex(tcpck_ctx *ctx, int op, int mode, void *d_arena,
                          uint64_t stride, uint32_t len, uint64_t count, void *d_out,

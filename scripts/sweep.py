@@ -50,6 +50,8 @@ def variants(w):
     if w["fixed"] and w["L"] >= 8192:
         tiles = [1, 2, 4]
     v += [(f"span T{t}", tcpck.KERNEL_SPAN, t) for t in tiles]
+    if not (w["fixed"] and w["L"] > 16384):
+        v += [(f"stream {n}", tcpck.KERNEL_STREAM, p) for p, n in tcpck.STREAM_VARIANTS.items()]
     return v
 
 

@@ -170,6 +170,15 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
     a.tile = param > 0 ? static_cast<uint32_t>(param) : tcpck::span_tile_for_len(len);
     return tcpck::launch_span(op, true, a, static_cast<uint32_t>(ctx->num_cus), s);
   }
+  if (kernel == TCPCK_KERNEL_STREAM) {
+    if (!span_ok) return hipErrorInvalidValue;
+    tcpck::SpanArgs a{};
+    a.arena = arena;
+    a.stride = stride;
+    a.count = count;
+    a.out = out;
+    return tcpck::launch_stream(op, true, param, a, static_cast<uint32_t>(ctx->num_cus), s);
+  }
   if (kernel != TCPCK_KERNEL_SEG) return hipErrorInvalidValue;
   SegArgs a{};
   a.arena = arena;
@@ -201,6 +210,19 @@ hipError_t run_var(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const uint6
     a.out = out;
     a.tile = param > 0 ? static_cast<uint32_t>(param) : tcpck::span_tile_for_len(typical);
     return tcpck::launch_span(op, false, a, static_cast<uint32_t>(ctx->num_cus), s);
+  }
+  if (kernel == TCPCK_KERNEL_STREAM) {
+    // offsets must be ascending (the run split searches them); each wave
+    // re-validates packing of its run and falls back per image if it fails
+    if (mode != TCPCK_MODE_REF) return hipErrorInvalidValue;
+    tcpck::SpanArgs a{};
+    a.arena = arena;
+    a.offsets = off;
+    a.lengths = len;
+    a.base = base;
+    a.count = count;
+    a.out = out;
+    return tcpck::launch_stream(op, false, param, a, static_cast<uint32_t>(ctx->num_cus), s);
   }
   if (kernel != TCPCK_KERNEL_SEG) return hipErrorInvalidValue;
   SegArgs a{};

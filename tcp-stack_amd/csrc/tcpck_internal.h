@@ -52,3 +52,10 @@ uint32_t span_tile_for_len(uint64_t typical_len);
 hipError_t launch_span(int op, bool fixed, const SpanArgs &a, uint32_t num_cus, hipStream_t stream);
 
 }  // namespace tcpck
+
+namespace tcpck {
+// ---- stream kernel: packed layouts, reference mode, one byte-balanced run per wave
+// variant: 0 = U4/nt (default), 1 = U8/nt, 2 = U4/plain loads, 3 = U2/nt
+hipError_t launch_stream(int op, bool fixed, int variant, const SpanArgs &a, uint32_t num_cus,
+                         hipStream_t stream);
+}  // namespace tcpck

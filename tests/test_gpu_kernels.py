@@ -10,6 +10,7 @@ torch = pytest.importorskip("torch")
 
 SEG = [1, 2, 3, 4, 5, 6]
 TILES = [1, 2, 7, 16, 33, 63]
+STREAM = [0, 1, 2, 3]
 
 
 @pytest.fixture(scope="module")
@@ -32,7 +33,8 @@ def host(t):
 
 def variants():
     import tcpck
-    return [(tcpck.KERNEL_SEG, p) for p in SEG] + [(tcpck.KERNEL_SPAN, t) for t in TILES]
+    return ([(tcpck.KERNEL_SEG, p) for p in SEG] + [(tcpck.KERNEL_SPAN, t) for t in TILES]
+            + [(tcpck.KERNEL_STREAM, v) for v in STREAM])
 
 
 def packed_golden(golden):
@@ -69,12 +71,15 @@ def test_fixed_packed_all_kernels(ctx, oracle_c, kernel, param, length):
     np.testing.assert_array_equal(host(out).view(np.uint16), exp)
 
 
-@pytest.mark.parametrize("tile", TILES)
-def test_span_var_mixed_and_fallback(ctx, oracle_c, tile):
+MIXED = [(2, t) for t in TILES] + [(3, v) for v in STREAM]
+
+
+@pytest.mark.parametrize("kernel,tile", MIXED)
+def test_span_var_mixed_and_fallback(ctx, oracle_c, kernel, tile):
     """Packed C3-style batch with some non-packed and short regions mixed in."""
     import tcpck
     import synth_np
-    rng = np.random.default_rng(tile)
+    rng = np.random.default_rng(tile + 100 * kernel)
     count = 20000
     off, ln, total = synth_np.mixed_layout(count, seed=tile)
     # break packing in a few places (gaps) and shrink a few images below 16 B
@@ -87,18 +92,44 @@ def test_span_var_mixed_and_fallback(ctx, oracle_c, tile):
     arena_np = rng.integers(0, 256, total, dtype=np.uint8)
     out = torch.empty(count, dtype=torch.int16, device="cuda")
     ctx.batch_var_ex(tcpck.OP_CHECKSUM, dev(arena_np), dev(off), dev(ln), count, out,
-                     tcpck.KERNEL_SPAN, tile, packed=True)
+                     kernel, tile, packed=True)
     exp = oracle_c.batch(arena_np, off, ln, threads=8)
     np.testing.assert_array_equal(host(out).view(np.uint16), exp)
 
 
-@pytest.mark.parametrize("tile", [1, 16, 63])
+@pytest.mark.parametrize("variant", STREAM)
+@pytest.mark.parametrize("count", [1, 2, 63, 64, 65, 127, 129, 1000, 70000])
+def test_stream_var_sizes(ctx, oracle_c, variant, count):
+    """Byte-balanced run split at every size, including fewer images than waves."""
+    import tcpck
+    import synth_np
+    off, ln, total = synth_np.mixed_layout(count, seed=count, payloads=(0, 64, 576, 1460, 9000))
+    rng = np.random.default_rng(count)
+    arena_np = rng.integers(0, 256, total + 16, dtype=np.uint8)
+    out = torch.empty(count, dtype=torch.int16, device="cuda")
+    ctx.batch_var_ex(tcpck.OP_CHECKSUM, dev(arena_np), dev(off), dev(ln), count, out,
+                     tcpck.KERNEL_STREAM, variant, packed=True)
+    np.testing.assert_array_equal(host(out).view(np.uint16), oracle_c.batch(arena_np, off, ln))
+    if count > 1:
+        out2 = torch.empty(count, dtype=torch.int16, device="cuda")
+        L = 16
+        ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, dev(arena_np), L, L, min(count, total // L), out2,
+                           tcpck.KERNEL_STREAM, variant)
+        n = min(count, total // L)
+        np.testing.assert_array_equal(host(out2).view(np.uint16)[:n],
+                                      oracle_c.batch(arena_np, stride=L, length=L, count=n))
+
+
+FV = [(2, t) for t in (1, 16, 63)] + [(3, v) for v in STREAM]
+
+
+@pytest.mark.parametrize("kernel,tile", FV)
 @pytest.mark.parametrize("fixed", [True, False])
-def test_span_fill_verify(ctx, oracle_c, tile, fixed):
+def test_span_fill_verify(ctx, oracle_c, kernel, tile, fixed):
     import tcpck
     import synth_np
     from oracle import ref16 as R
-    rng = np.random.default_rng(50 + tile)
+    rng = np.random.default_rng(50 + tile + 7 * kernel)
     if fixed:
         L, count = 1492, 4000
         off = (np.arange(count, dtype=np.uint64) * L)
@@ -111,9 +142,9 @@ def test_span_fill_verify(ctx, oracle_c, tile, fixed):
     arena = dev(arena_np)
     out = torch.empty(count, dtype=torch.int16, device="cuda")
     if fixed:
-        ctx.batch_fixed_ex(tcpck.OP_FILL, arena, L, L, count, out, tcpck.KERNEL_SPAN, tile)
+        ctx.batch_fixed_ex(tcpck.OP_FILL, arena, L, L, count, out, kernel, tile)
     else:
-        ctx.batch_var_ex(tcpck.OP_FILL, arena, dev(off), dev(ln), count, out, tcpck.KERNEL_SPAN, tile,
+        ctx.batch_var_ex(tcpck.OP_FILL, arena, dev(off), dev(ln), count, out, kernel, tile,
                          packed=True)
     got = host(arena)
     exp_arena = arena_np.copy()
@@ -129,9 +160,9 @@ def test_span_fill_verify(ctx, oracle_c, tile, fixed):
         got[int(off[k]) + int(rng.integers(0, int(ln[k])))] ^= 0x11
     arena2 = dev(got)
     if fixed:
-        ctx.batch_fixed_ex(tcpck.OP_VERIFY, arena2, L, L, count, ok, tcpck.KERNEL_SPAN, tile)
+        ctx.batch_fixed_ex(tcpck.OP_VERIFY, arena2, L, L, count, ok, kernel, tile)
     else:
-        ctx.batch_var_ex(tcpck.OP_VERIFY, arena2, dev(off), dev(ln), count, ok, tcpck.KERNEL_SPAN, tile,
+        ctx.batch_var_ex(tcpck.OP_VERIFY, arena2, dev(off), dev(ln), count, ok, kernel, tile,
                          packed=True)
     np.testing.assert_array_equal(np.nonzero(host(ok) == 0)[0], np.unique(bad))
 
