@@ -24,6 +24,15 @@ inline uint32_t resident_blocks_per_cu(Kernel kernel) {
   return static_cast<uint32_t>(nb);
 }
 
+// Offset (relative to `arena`, wrapping) of the 16-byte-aligned ADDRESS at or
+// below arena + off: loads stay naturally aligned even when the caller's arena
+// pointer is not (the few bytes read before an image are masked, and they lie
+// in the same 16-byte block -- hence the same page -- as a byte of the image).
+__device__ __forceinline__ uint64_t align16_rel(const uint8_t *arena, uint64_t off) {
+  const uint64_t mis = reinterpret_cast<uint64_t>(arena) & 15u;
+  return ((off + mis) & ~uint64_t{15}) - mis;
+}
+
 // 16-byte streaming load, nontemporal (global_load_dwordx4 ... nt): the batch
 // is read exactly once, so keep it from displacing other lines.
 __device__ __forceinline__ u32x4 load16_nt(const uint8_t *p) {
@@ -135,8 +144,9 @@ template <int U, int MODE>
 __device__ __forceinline__ uint32_t wave_image_sum(const uint8_t *arena, uint64_t start, uint32_t len,
                                                    bool exclude_field) {
   const uint32_t lane = threadIdx.x & 63;
-  const uint8_t *p0 = arena + (start & ~uint64_t{15});
-  const int32_t lead = static_cast<int32_t>(start & 15);
+  const uint64_t a0 = align16_rel(arena, start);
+  const uint8_t *p0 = arena + a0;
+  const int32_t lead = static_cast<int32_t>(start - a0);
   const int64_t span64 = lead + static_cast<int64_t>(len);
   const uint32_t nch = static_cast<uint32_t>((span64 + 15) >> 4);
   const int64_t field = exclude_field ? lead + 28 : -64;

@@ -43,8 +43,9 @@ __global__ void __launch_bounds__(kBlock) seg_kernel(SegArgs a) {
        k += groups_per_grid) {
     const uint64_t start = FIXED ? k * a.stride : a.offsets[k] - a.base;
     const uint32_t len = FIXED ? a.len : a.lengths[k];
-    const uint8_t *p0 = a.arena + (start & ~uint64_t{15});
-    const int64_t lead = static_cast<int64_t>(start & 15);    // masked bytes before the image
+    const uint64_t a0 = dev::align16_rel(a.arena, start);     // 16-B aligned in absolute terms
+    const uint8_t *p0 = a.arena + a0;
+    const int64_t lead = static_cast<int64_t>(start - a0);    // masked bytes before the image
     const int64_t span = lead + static_cast<int64_t>(len);    // bytes from p0 to the image end
     const uint32_t nch = static_cast<uint32_t>((span + 15) >> 4);  // 16-byte chunks touched
     const int64_t field = (OP == kFill) ? lead + 28 : -64;    // checksum field counts as 0

@@ -101,7 +101,7 @@ __global__ void __launch_bounds__(kBlock) span_kernel(SpanArgs a) {
     }
     const uint64_t s0 = dev::read_lane64(bj, 0);
     const uint64_t s1 = dev::read_lane64(bj, n - 1) + dev::read_lane(lj, n - 1);
-    const uint64_t A0 = s0 & ~uint64_t{15};
+    const uint64_t A0 = dev::align16_rel(a.arena, s0);
     bool packed = (s1 - A0) < (uint64_t{1} << 30);
     if (!FIXED) {
       const uint64_t nb = __shfl_down(static_cast<unsigned long long>(bj), 1, 64);

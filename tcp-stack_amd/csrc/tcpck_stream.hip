@@ -119,7 +119,7 @@ __global__ void __launch_bounds__(kBlock) stream_kernel(SpanArgs a) {
 
   const uint64_t s0 = start_of(kb);
   const uint64_t s1 = start_of(ke - 1) + len_of(ke - 1);
-  const uint64_t A0 = s0 & ~uint64_t{15};
+  const uint64_t A0 = dev::align16_rel(a.arena, s0);
 
   if (!FIXED) {
     // validate the run: packed, every image >= 16 B, run shorter than 2^31 B

@@ -71,6 +71,26 @@ def test_fixed_packed_all_kernels(ctx, oracle_c, kernel, param, length):
     np.testing.assert_array_equal(host(out).view(np.uint16), exp)
 
 
+@pytest.mark.parametrize("kernel,param", variants())
+@pytest.mark.parametrize("mis", [2, 6, 14])
+def test_misaligned_arena_pointer(ctx, oracle_c, kernel, param, mis):
+    """The arena pointer itself need not be 16-B aligned (e.g. a sliced buffer)."""
+    import tcpck
+    rng = np.random.default_rng(mis * 31 + param)
+    L, count = 1492, 2000
+    arena_np = rng.integers(0, 256, count * L + 64, dtype=np.uint8)
+    buf = dev(arena_np)
+    ptr = buf.data_ptr() + mis
+    out = torch.empty(count, dtype=torch.int16, device="cuda")
+    ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, ptr, L, L, count, out, kernel, param)
+    exp = oracle_c.batch(arena_np[mis:], stride=L, length=L, count=count)
+    np.testing.assert_array_equal(host(out).view(np.uint16), exp)
+    off = (np.arange(count, dtype=np.uint64) * L)
+    ln = np.full(count, L, np.uint32)
+    ctx.batch_var_ex(tcpck.OP_CHECKSUM, ptr, dev(off), dev(ln), count, out, kernel, param, packed=True)
+    np.testing.assert_array_equal(host(out).view(np.uint16), exp)
+
+
 MIXED = [(2, t) for t in TILES] + [(3, v) for v in STREAM]
 
 
