@@ -165,10 +165,18 @@ __global__ void __launch_bounds__(kBlock) stream_kernel(SpanArgs a) {
   const uint8_t *base = a.arena + A0;
 
   // ---- boundary batches: interior boundaries k = kb+1 .. ke-1, 64 per batch ----
-  // lane j of the current batch holds boundary kc + j: rb = start - A0 (or ~0u)
-  auto batch_rb = [&](uint64_t kc) -> uint32_t {
+  // Lane j of the current batch holds boundary kc + j as rb = start - A0 (~0u
+  // past ke).  The next batch's raw descriptors are prefetched a whole batch
+  // ahead and only turned into rb when the batch is activated, so the only
+  // wait on them is at activation (once per 64 images), never per step.
+  auto batch_raw = [&](uint64_t kc) -> uint64_t {  // raw descriptor load (variable layout)
     const uint64_t k = kc + lane;
-    return k < ke ? static_cast<uint32_t>(start_of(k) - A0) : 0xFFFFFFFFu;
+    return (FIXED || k >= ke) ? 0 : a.offsets[k];
+  };
+  auto batch_rb = [&](uint64_t kc, uint64_t raw) -> uint32_t {
+    const uint64_t k = kc + lane;
+    if (k >= ke) return 0xFFFFFFFFu;
+    return static_cast<uint32_t>((FIXED ? k * a.stride : raw - a.base) - A0);
   };
   auto batch_field = [&](uint64_t kc) -> uint32_t {  // field word of image kc + lane (kFill)
     const uint64_t k = kc + lane;
@@ -176,11 +184,11 @@ __global__ void __launch_bounds__(kBlock) stream_kernel(SpanArgs a) {
     return *reinterpret_cast<const uint16_t *>(a.arena + start_of(k) + 28);
   };
   uint64_t kc = kb + 1;
-  uint32_t rb = batch_rb(kc);
-  uint32_t nrb = batch_rb(kc + 64);        // prefetched next batch
+  uint32_t rb = batch_rb(kc, batch_raw(kc));
+  uint64_t nraw = batch_raw(kc + 64);      // prefetched next batch (not consumed until activation)
   uint32_t nfield = batch_field(kc + 64);
   if (OP == kFill) {
-    const uint32_t f0 = batch_field(kb);  // images kb .. kb+63: their own fields
+    const uint32_t f0 = batch_field(kb);  // image kb .. kb+63 fields (kb is not a routed boundary)
     if (kb + lane < ke) fld[(kb + lane) % kRing] = f0;
   }
   slot[lane] = 0;
@@ -197,25 +205,28 @@ __global__ void __launch_bounds__(kBlock) stream_kernel(SpanArgs a) {
     ring[u] = load16<NT>(base + 16 * static_cast<uint64_t>(ci));
   }
 
+  // Steps past nsteps in the last unrolled group are harmless no-ops: their
+  // words are masked (sb >= span), no boundary lies there, carry adds 0.  So the
+  // unrolled body has no per-step condition and the ring refill stays in place
+  // (a conditional refill made hipcc copy the freshly loaded slot, i.e. wait
+  // vmcnt(0) every step).
   for (uint32_t s0i = 0; s0i < nsteps; s0i += U) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint32_t st = s0i + u;
-      if (st < nsteps) {  // wave-uniform
+      {
         const uint32_t sb = st << 10;
         // post this step's boundaries (possibly from two consecutive batches)
         for (;;) {
           if (rb - sb < 1024u) slot[(rb - sb) >> 4] = 0x80000000u | (static_cast<uint32_t>(kc + lane - kb) << 3) | ((rb & 15u) >> 1);
           const uint32_t last = dev::read_lane(rb, 63);  // largest rb of the batch (or ~0u)
-          const uint32_t first_next = dev::read_lane(nrb, 0);
-          if (last == 0xFFFFFFFFu || last - sb >= 1024u || kc + 64 >= ke) break;
-          // whole batch posted: advance (the next batch may start in this step too)
+          if (last == 0xFFFFFFFFu || last - sb >= 1024u) break;
+          // whole batch posted: activate the next one (it may start in this step too)
           kc += 64;
-          rb = nrb;
+          rb = batch_rb(kc, nraw);
           if (OP == kFill && kc + lane < ke) fld[(kc + lane) % kRing] = nfield;
-          nrb = batch_rb(kc + 64);
+          nraw = batch_raw(kc + 64);
           nfield = batch_field(kc + 64);
-          if (first_next - sb >= 1024u) break;
         }
         __builtin_amdgcn_wave_barrier();
         const uint32_t route = slot[lane];
