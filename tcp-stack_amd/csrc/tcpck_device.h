@@ -33,6 +33,12 @@ __device__ __forceinline__ uint64_t align16_rel(const uint8_t *arena, uint64_t o
   return ((off + mis) & ~uint64_t{15}) - mis;
 }
 
+// Same for the 128-byte (cache line) aligned address at or below arena + off.
+__device__ __forceinline__ uint64_t align128_rel(const uint8_t *arena, uint64_t off) {
+  const uint64_t mis = reinterpret_cast<uint64_t>(arena) & 127u;
+  return ((off + mis) & ~uint64_t{127}) - mis;
+}
+
 // 16-byte streaming load, nontemporal (global_load_dwordx4 ... nt): the batch
 // is read exactly once, so keep it from displacing other lines.
 __device__ __forceinline__ u32x4 load16_nt(const uint8_t *p) {

@@ -83,7 +83,11 @@ __device__ __forceinline__ void emit(const SpanArgs &a, uint64_t k, uint32_t sum
   }
 }
 
-template <int U, int OP, bool FIXED, bool NT>
+// DIAG (timing experiments only; 2 and 3 produce wrong checksums):
+//   0 = product, runs 16-B aligned; 1 = runs 128-B aligned (whole cache lines
+//   per step); 2 = as 1 with boundary handling removed (stream + scan);
+//   3 = as 1 with boundaries and scan removed (pure stream + per-lane sums).
+template <int U, int OP, bool FIXED, bool NT, int DIAG = 0>
 __global__ void __launch_bounds__(kBlock) stream_kernel(SpanArgs a) {
   __shared__ uint32_t s_slot[kWavesPerBlock][64];
   __shared__ uint32_t s_pb[kWavesPerBlock][kRing];   // P(start_k), ring by k
@@ -119,7 +123,7 @@ __global__ void __launch_bounds__(kBlock) stream_kernel(SpanArgs a) {
 
   const uint64_t s0 = start_of(kb);
   const uint64_t s1 = start_of(ke - 1) + len_of(ke - 1);
-  const uint64_t A0 = dev::align16_rel(a.arena, s0);
+  const uint64_t A0 = DIAG ? dev::align128_rel(a.arena, s0) : dev::align16_rel(a.arena, s0);
 
   if (!FIXED) {
     // validate the run: packed, every image >= 16 B, run shorter than 2^31 B
@@ -217,7 +221,7 @@ __global__ void __launch_bounds__(kBlock) stream_kernel(SpanArgs a) {
       {
         const uint32_t sb = st << 10;
         // post this step's boundaries (possibly from two consecutive batches)
-        for (;;) {
+        for (; DIAG < 2;) {
           if (rb - sb < 1024u) slot[(rb - sb) >> 4] = 0x80000000u | (static_cast<uint32_t>(kc + lane - kb) << 3) | ((rb & 15u) >> 1);
           const uint32_t last = dev::read_lane(rb, 63);  // largest rb of the batch (or ~0u)
           if (last == 0xFFFFFFFFu || last - sb >= 1024u) break;
@@ -246,8 +250,12 @@ __global__ void __launch_bounds__(kBlock) stream_kernel(SpanArgs a) {
           ring[u] = load16<NT>(base + 16 * static_cast<uint64_t>(ci));
         }
         const uint32_t tot = dev::ref_chunk_sum(wv4);
+        if (DIAG == 3) {
+          carry += tot;
+          continue;
+        }
         const uint32_t incl = dev::wave_inclusive_scan(tot);
-        if (route) {
+        if (DIAG < 2 && route) {
           const uint32_t r = (route & 7u) << 1;  // boundary byte offset inside the chunk
           const uint32_t head = dev::ref_chunk_sum(dev::apply_mask(wv4, dev::word_mask(lo, r)));
           const uint64_t k = kb + ((route >> 3) & 0x0FFFFFFFu);
@@ -268,6 +276,10 @@ __global__ void __launch_bounds__(kBlock) stream_kernel(SpanArgs a) {
     }
   }
   __builtin_amdgcn_wave_barrier();
+  if (DIAG >= 2) {  // keep the stream alive for timing; results are not checksums
+    if (lane == 0 && a.out) static_cast<uint16_t *>(a.out)[kb] = static_cast<uint16_t>(carry);
+    return;
+  }
   if (lane == 0) {  // the last image ends at the end of the run
     const uint32_t km1 = static_cast<uint32_t>((ke - 1) % kRing);
     const uint32_t st_prev = pos[km1];
@@ -277,14 +289,14 @@ __global__ void __launch_bounds__(kBlock) stream_kernel(SpanArgs a) {
   }
 }
 
-template <int U, int OP, bool FIXED, bool NT>
+template <int U, int OP, bool FIXED, bool NT, int DIAG = 0>
 hipError_t launch_one(const SpanArgs &a, uint32_t num_cus, hipStream_t stream) {
-  static const uint32_t per_cu = dev::resident_blocks_per_cu(stream_kernel<U, OP, FIXED, NT>);
+  static const uint32_t per_cu = dev::resident_blocks_per_cu(stream_kernel<U, OP, FIXED, NT, DIAG>);
   uint64_t blocks = static_cast<uint64_t>(per_cu) * num_cus;
   const uint64_t need = (a.count + kWavesPerBlock - 1) / kWavesPerBlock;  // >= 1 image per wave
   if (blocks > need) blocks = need;
   if (blocks == 0) return hipSuccess;
-  hipLaunchKernelGGL((stream_kernel<U, OP, FIXED, NT>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0,
+  hipLaunchKernelGGL((stream_kernel<U, OP, FIXED, NT, DIAG>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0,
                      stream, a);
   return hipGetLastError();
 }
@@ -303,6 +315,13 @@ hipError_t dispatch(int op, bool fixed, const SpanArgs &a, uint32_t num_cus, hip
   }
 }
 
+template <int U, int DIAG>
+hipError_t launch_diag(int op, bool fixed, const SpanArgs &a, uint32_t num_cus, hipStream_t s) {
+  if (op != kChecksum) return hipErrorInvalidValue;
+  return fixed ? launch_one<U, kChecksum, true, true, DIAG>(a, num_cus, s)
+               : launch_one<U, kChecksum, false, true, DIAG>(a, num_cus, s);
+}
+
 }  // namespace
 
 // variant: 0 = default (U=4, nt), 1 = U=8 nt, 2 = U=4 plain loads, 3 = U=2 nt
@@ -312,6 +331,11 @@ hipError_t launch_stream(int op, bool fixed, int variant, const SpanArgs &a, uin
     case 1: return dispatch<8, true>(op, fixed, a, num_cus, stream);
     case 2: return dispatch<4, false>(op, fixed, a, num_cus, stream);
     case 3: return dispatch<2, true>(op, fixed, a, num_cus, stream);
+    // timing experiments (fixed-stride checksum only): see DIAG above
+    case 4: return launch_diag<4, 1>(op, fixed, a, num_cus, stream);
+    case 5: return launch_diag<2, 1>(op, fixed, a, num_cus, stream);
+    case 6: return launch_diag<4, 2>(op, fixed, a, num_cus, stream);
+    case 7: return launch_diag<4, 3>(op, fixed, a, num_cus, stream);
     default: return hipErrorInvalidValue;
   }
 }
