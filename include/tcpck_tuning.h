@@ -22,6 +22,10 @@ extern "C" {
 #define TCPCK_KERNEL_STREAM 3 /* packed images, one byte-balanced run per wave,
                                  MODE_REF only; param = variant (0: 4 loads in
                                  flight nt, 1: 8 nt, 2: 4 plain, 3: 2 nt)        */
+#define TCPCK_KERNEL_FSTREAM 4 /* fixed stride == len only, MODE_REF: interleaved
+                                  tiles, arithmetic boundaries; param = images
+                                  per tile (low 16 bits, 0 = auto) | variant << 16
+                                  (0: 4 loads in flight, 1: 2)                  */
 
 int tcpck_batch_fixed_ex(tcpck_ctx *ctx, int op, int mode, void *d_arena,
                          uint64_t stride, uint32_t len, uint64_t count, void *d_out,

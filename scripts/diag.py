@@ -17,7 +17,9 @@ import tcpck  # noqa: E402
 VARIANTS = [("stream U4 a16", tcpck.KERNEL_STREAM, 0), ("stream U4 a128", tcpck.KERNEL_STREAM, 4),
             ("stream U2 a128", tcpck.KERNEL_STREAM, 5), ("scan only a128", tcpck.KERNEL_STREAM, 6),
             ("pure a128", tcpck.KERNEL_STREAM, 7), ("span T16", tcpck.KERNEL_SPAN, 16),
-            ("seg G64U4", tcpck.KERNEL_SEG, 3), ("seg G16U6", tcpck.KERNEL_SEG, 2)]
+            ("seg G64U4", tcpck.KERNEL_SEG, 3), ("seg G16U6", tcpck.KERNEL_SEG, 2),
+            ("fstream U4", tcpck.KERNEL_FSTREAM, 0), ("fstream U2", tcpck.KERNEL_FSTREAM, 1 << 16),
+            ("fstream U4 T32", tcpck.KERNEL_FSTREAM, 32), ("fstream U4 T8", tcpck.KERNEL_FSTREAM, 8)]
 
 
 def main():

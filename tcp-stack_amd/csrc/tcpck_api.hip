@@ -179,6 +179,18 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
     a.out = out;
     return tcpck::launch_stream(op, true, param, a, static_cast<uint32_t>(ctx->num_cus), s);
   }
+  if (kernel == TCPCK_KERNEL_FSTREAM) {
+    if (!span_ok || len > (1u << 20)) return hipErrorInvalidValue;
+    const int variant = (param >> 16) & 0xFF;
+    const uint32_t tile = static_cast<uint32_t>(param & 0xFFFF);
+    tcpck::FixedStreamArgs a{};
+    a.arena = arena;
+    a.stride = stride;
+    a.count = count;
+    a.out = out;
+    a.tile = tile ? tile : tcpck::fstream_tile_for_len(len, variant);
+    return tcpck::launch_fstream(op, variant, a, static_cast<uint32_t>(ctx->num_cus), s);
+  }
   if (kernel != TCPCK_KERNEL_SEG) return hipErrorInvalidValue;
   SegArgs a{};
   a.arena = arena;

@@ -58,4 +58,18 @@ namespace tcpck {
 // variant: 0 = U4/nt (default), 1 = U8/nt, 2 = U4/plain loads, 3 = U2/nt
 hipError_t launch_stream(int op, bool fixed, int variant, const SpanArgs &a, uint32_t num_cus,
                          hipStream_t stream);
+
+// ---- fixed-stride stream kernel: packed fixed stride (stride == len >= 16),
+// reference mode, interleaved tiles, arithmetic boundaries
+struct FixedStreamArgs {
+  uint8_t *arena;
+  uint64_t stride;  // == image length
+  uint64_t count;
+  void *out;
+  uint32_t tile;    // images per tile (>= fstream_min_tile)
+};
+uint32_t fstream_min_tile(uint32_t stride, int variant);
+uint32_t fstream_tile_for_len(uint32_t stride, int variant);
+// variant: 0 = 4 loads in flight per lane, 1 = 2
+hipError_t launch_fstream(int op, int variant, const FixedStreamArgs &a, uint32_t num_cus, hipStream_t stream);
 }  // namespace tcpck

@@ -197,3 +197,67 @@ def test_span_rejects_rfc_and_gaps(ctx):
         ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, a, 1000, 996, 8, o, tcpck.KERNEL_SPAN, 4)
     with pytest.raises(tcpck.TcpckError):
         ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, a, 1000, 1000, 8, o, tcpck.KERNEL_SPAN, 64)
+
+
+# ---- fixed-stride stream kernel (KERNEL_FSTREAM = 4: fixed stride == len only) ----
+FSTREAM = [(0, 0), (1 << 16, 0), (0, 3), (0, 5), (1 << 16, 2), (0, 64)]  # (variant << 16, tile)
+
+
+@pytest.mark.parametrize("vt", FSTREAM)
+@pytest.mark.parametrize("length", [16, 30, 32, 96, 606, 1024, 1026, 1492, 1494, 4096, 9000, 65536])
+@pytest.mark.parametrize("count", [1, 7, 3001])
+def test_fstream_fixed_vs_oracle(ctx, oracle_c, vt, length, count):
+    import tcpck
+    variant, tile = vt
+    lo = (4 if variant == 0 else 2) * 1024
+    if tile and tile * length < lo:
+        pytest.skip("tile shorter than the load ring (rejected by design)")
+    rng = np.random.default_rng(length * 3 + count + tile)
+    arena_np = rng.integers(0, 256, count * length + 32, dtype=np.uint8)
+    arena_np[:length] = 0xFF
+    buf = dev(arena_np)
+    for mis in (0, 2, 14):
+        out = torch.empty(count, dtype=torch.int16, device="cuda")
+        ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, buf.data_ptr() + mis, length, length, count, out,
+                           tcpck.KERNEL_FSTREAM, variant | tile)
+        exp = oracle_c.batch(arena_np[mis:], stride=length, length=length, count=count)
+        np.testing.assert_array_equal(host(out).view(np.uint16), exp)
+
+
+@pytest.mark.parametrize("vt", [(0, 0), (1 << 16, 0), (0, 3)])
+@pytest.mark.parametrize("length", [30, 96, 1492, 2000])
+def test_fstream_fill_verify(ctx, vt, length):
+    import tcpck
+    from oracle import ref16 as R
+    variant, tile = vt
+    if tile and tile * length < 4096:
+        tile = 0
+    rng = np.random.default_rng(length + variant)
+    count = 5000
+    arena_np = rng.integers(0, 256, count * length, dtype=np.uint8)
+    arena = dev(arena_np)
+    out = torch.empty(count, dtype=torch.int16, device="cuda")
+    ctx.batch_fixed_ex(tcpck.OP_FILL, arena, length, length, count, out, tcpck.KERNEL_FSTREAM, variant | tile)
+    exp_arena = arena_np.copy()
+    exp = np.array([R.fill_np(exp_arena[k * length:(k + 1) * length]) for k in range(count)], np.uint16)
+    np.testing.assert_array_equal(host(out).view(np.uint16), exp)
+    got = host(arena)
+    np.testing.assert_array_equal(got, exp_arena)
+    bad = rng.choice(count, 64, replace=False)
+    for k in bad:
+        got[k * length + int(rng.integers(0, length))] ^= 0x24
+    ok = torch.empty(count, dtype=torch.uint8, device="cuda")
+    ctx.batch_fixed_ex(tcpck.OP_VERIFY, dev(got), length, length, count, ok, tcpck.KERNEL_FSTREAM, variant | tile)
+    np.testing.assert_array_equal(np.nonzero(host(ok) == 0)[0], np.sort(bad))
+
+
+def test_fstream_rejects(ctx):
+    import tcpck
+    a = torch.zeros(1 << 20, dtype=torch.uint8, device="cuda")
+    o = torch.zeros(1024, dtype=torch.int16, device="cuda")
+    with pytest.raises(tcpck.TcpckError):  # gaps between images
+        ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, a, 1500, 1492, 100, o, tcpck.KERNEL_FSTREAM, 0)
+    with pytest.raises(tcpck.TcpckError):  # RFC 1071 mode
+        ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, a, 1492, 1492, 100, o, tcpck.KERNEL_FSTREAM, 0, mode=1)
+    with pytest.raises(tcpck.TcpckError):  # tile shorter than the ring
+        ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, a, 1492, 1492, 100, o, tcpck.KERNEL_FSTREAM, 1)
