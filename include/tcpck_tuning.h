@@ -26,10 +26,18 @@ extern "C" {
                                   tiles, arithmetic boundaries; param = images
                                   per tile (low 16 bits, 0 = auto) | variant << 16
                                   (0: 4 loads in flight, 1: 2)                  */
+#define TCPCK_KERNEL_RSTREAM 5 /* fixed stride == len only, MODE_REF: one run per
+                                  wave, scalar boundary walk; param = variant
+                                  (0: 4 loads in flight, 1: 2, 2: 8, 3: 4 with
+                                  per-wave time stamps, checksum only)          */
 
 int tcpck_batch_fixed_ex(tcpck_ctx *ctx, int op, int mode, void *d_arena,
                          uint64_t stride, uint32_t len, uint64_t count, void *d_out,
                          int kernel, int param, tcpck_stream stream);
+/* Device buffer of 2 x u64 per wave receiving {start, end} s_memrealtime
+ * (100 MHz) stamps from kernels built with stamps (NULL = off). */
+int tcpck_ctx_set_debug(tcpck_ctx *ctx, void *d_buf);
+
 int tcpck_batch_var_ex(tcpck_ctx *ctx, int op, int mode, void *d_arena,
                        const uint64_t *d_offsets, const uint32_t *d_lengths,
                        uint64_t count, void *d_out, const tcpck_layout *layout,

@@ -19,7 +19,8 @@ VARIANTS = [("stream U4 a16", tcpck.KERNEL_STREAM, 0), ("stream U4 a128", tcpck.
             ("pure a128", tcpck.KERNEL_STREAM, 7), ("span T16", tcpck.KERNEL_SPAN, 16),
             ("seg G64U4", tcpck.KERNEL_SEG, 3), ("seg G16U6", tcpck.KERNEL_SEG, 2),
             ("fstream U4", tcpck.KERNEL_FSTREAM, 0), ("fstream U2", tcpck.KERNEL_FSTREAM, 1 << 16),
-            ("fstream U4 T32", tcpck.KERNEL_FSTREAM, 32), ("fstream U4 T8", tcpck.KERNEL_FSTREAM, 8)]
+            ("rstream U4", tcpck.KERNEL_RSTREAM, 0), ("rstream U2", tcpck.KERNEL_RSTREAM, 1),
+            ("rstream U8", tcpck.KERNEL_RSTREAM, 2)]
 
 
 def main():
@@ -28,6 +29,7 @@ def main():
     arena = torch.empty(17 << 30, dtype=torch.uint8, device="cuda")
     tcpck.synth_fixed(arena, 65536, 65536, (17 << 30) // 65536, seed=3)
     out = torch.empty(12 << 20, dtype=torch.int16, device="cuda")
+    stamps(ctx, arena, out, stream)
     for L, total in ((1492, 1 << 30), (1492, int(1.5 * (1 << 30))), (1492, 16 << 30), (65536, 16 << 30)):
         n = total // L
         times = {v[0]: [] for v in VARIANTS}
@@ -47,6 +49,31 @@ def main():
             med = float(np.median(times[name]))
             print(f"L={L:5d} {algo / 1e9:6.2f} GB  {name:15s} {med:8.4f} ms  {algo / med / 1e6:7.1f} GB/s "
                   f"({algo / med / 1e6 / 80:.1f}%)", flush=True)
+
+
+def stamps(ctx, arena, out, stream):
+    """Per-wave start/end times of one C2-sized rstream launch (tail analysis)."""
+    L, n = 1492, 1 << 20
+    dbg = torch.zeros(2 * 256 * 8 * 4 * 2, dtype=torch.int64, device="cuda")
+    ctx.set_debug(dbg)
+    for _ in range(3):
+        ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, arena, L, L, n, out, tcpck.KERNEL_RSTREAM, 3, stream=stream)
+    torch.cuda.synchronize()
+    ctx.set_debug(None)
+    d = dbg.cpu().numpy().reshape(-1, 2)
+    d = d[d[:, 1] > 0]
+    t0 = d[:, 0].min()
+    st, en = (d[:, 0] - t0) / 100.0, (d[:, 1] - t0) / 100.0  # 100 MHz -> us
+    dur = en - st
+    print(f"stamps: waves {len(d)}  start max {st.max():.2f} us  end min/median/p99/max "
+          f"{en.min():.1f}/{np.median(en):.1f}/{np.percentile(en, 99):.1f}/{en.max():.1f} us  "
+          f"wave duration min/median/max {dur.min():.1f}/{np.median(dur):.1f}/{dur.max():.1f} us", flush=True)
+    wid = np.nonzero(dbg.cpu().numpy().reshape(-1, 2)[:, 1] > 0)[0]
+    by = {}
+    for x in range(8):
+        sel = (wid % 8) == x
+        by[x] = float(np.median(en[sel])) if sel.any() else 0.0
+    print("stamps: median end by block-id mod 8 (XCD group):", {k: round(v, 1) for k, v in by.items()}, flush=True)
 
 
 if __name__ == "__main__":

@@ -39,6 +39,7 @@ struct tcpck_ctx {
   uint64_t stage_bytes = 0;
   uint64_t stage_images = 0;
   uint64_t chunk_bytes = 64ull << 20;
+  void *dbg = nullptr;  // tuning: per-wave time stamp buffer (tcpck_ctx_set_debug)
 };
 
 namespace {
@@ -190,6 +191,16 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
     a.out = out;
     a.tile = tile ? tile : tcpck::fstream_tile_for_len(len, variant);
     return tcpck::launch_fstream(op, variant, a, static_cast<uint32_t>(ctx->num_cus), s);
+  }
+  if (kernel == TCPCK_KERNEL_RSTREAM) {
+    if (!span_ok) return hipErrorInvalidValue;
+    tcpck::FixedStreamArgs a{};
+    a.arena = arena;
+    a.stride = stride;
+    a.count = count;
+    a.out = out;
+    a.dbg = static_cast<uint64_t *>(ctx->dbg);
+    return tcpck::launch_rstream(op, param, a, static_cast<uint32_t>(ctx->num_cus), s);
   }
   if (kernel != TCPCK_KERNEL_SEG) return hipErrorInvalidValue;
   SegArgs a{};
@@ -364,6 +375,12 @@ int tcpck_batch_var(tcpck_ctx *ctx, int op, int mode, void *d_arena, const uint6
                     const tcpck_layout *layout, tcpck_stream stream) {
   return tcpck_batch_var_ex(ctx, op, mode, d_arena, d_offsets, d_lengths, count, d_out, layout,
                             TCPCK_KERNEL_AUTO, 0, stream);
+}
+
+int tcpck_ctx_set_debug(tcpck_ctx *ctx, void *d_buf) {
+  if (!ctx) return TCPCK_EINVAL;
+  ctx->dbg = d_buf;
+  return TCPCK_OK;
 }
 
 int tcpck_batch_fixed_ex(tcpck_ctx *ctx, int op, int mode, void *d_arena, uint64_t stride, uint32_t len,

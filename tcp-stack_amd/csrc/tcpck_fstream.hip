@@ -113,9 +113,9 @@ __global__ void __launch_bounds__(kBlock) fstream_kernel(FixedStreamArgs a) {
     if (x >= 0) {
       q = x / static_cast<int32_t>(S);
       m = static_cast<uint32_t>(x) - static_cast<uint32_t>(q) * S;
-    } else {  // x in [-127, 0): one image before the run
-      q = -1;
-      m = static_cast<uint32_t>(x + static_cast<int32_t>(S));
+    } else {  // x in [-127, 0): before the run, possibly several short images back
+      q = -static_cast<int32_t>((static_cast<uint32_t>(-x) + S - 1) / S);
+      m = static_cast<uint32_t>(x - q * static_cast<int32_t>(S));
     }
   };
   lane_init();

@@ -67,7 +67,11 @@ struct FixedStreamArgs {
   uint64_t count;
   void *out;
   uint32_t tile;    // images per tile (>= fstream_min_tile)
+  uint64_t *dbg;    // optional per-wave {start, end} s_memrealtime stamps (timing builds)
 };
+// ---- run-stream kernel (fixed stride == len): one run per wave, scalar boundaries
+// variant: 0 = 4 loads in flight, 1 = 2, 2 = 8, 3 = 4 with per-wave time stamps
+hipError_t launch_rstream(int op, int variant, const FixedStreamArgs &a, uint32_t num_cus, hipStream_t stream);
 uint32_t fstream_min_tile(uint32_t stride, int variant);
 uint32_t fstream_tile_for_len(uint32_t stride, int variant);
 // variant: 0 = 4 loads in flight per lane, 1 = 2

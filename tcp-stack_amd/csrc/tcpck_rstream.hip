@@ -1,0 +1,206 @@
+// tcpck_rstream.hip -- fixed-stride packed batches (stride == image length):
+// one contiguous run of whole images per wave, image boundaries walked in
+// scalar registers.
+//
+// Reference semantics: CalculateChecksum, include/tcp-header.h:252-263:
+// ~(sum of the image's LE u16 words mod 2^16).  Images are back to back at a
+// fixed stride S, so sum(k) = P((k+1)S) - P(kS) (mod 2^16) where P(x) is the
+// word sum of the wave's run before byte x: the run is read as one flat stream.
+//
+//   * wave w owns images [w N / W, (w+1) N / W): one contiguous run per wave
+//     (measured faster than interleaved tiles on this part), its start rounded
+//     down to a 128-B line so that every 1 KiB step covers exactly eight whole
+//     lines;
+//   * lane l reads the 16 B at 1024 s + 16 l of step s; U steps stay in flight
+//     in a register ring refilled at the end of each step (the slot's data is
+//     dead by then, so the load lands in the same registers -- no copies, no
+//     vmcnt(0) drains);
+//   * per step: the lane's word sum, a 64-lane DPP inclusive scan, the step
+//     total by readlane 63 -- the only per-step vector work;
+//   * the next image boundary is wave-uniform (next = previous + S), so the
+//     boundary walk is scalar: when it falls in this step, P(boundary) =
+//     carry + scan(lane) - sum(lane) + the lane's words before the byte,
+//     each read with v_readlane into SGPRs; the image that ends there gets
+//     ~(P - P_prev), written into lane (k mod 64) of a staging VGPR with
+//     v_writelane, and 64 results leave as one coalesced store;
+//   * kFill zeroes each image's checksum word (bytes 28-29) in the stream, so
+//     the differences are the checksums of the zero-field images, and writes
+//     them into bytes 28-29 (tcp-header.h:177); kVerify stores checksum == 0.
+#include "tcpck_device.h"
+
+namespace tcpck {
+
+namespace {
+
+using dev::kBlock;
+using dev::kWavesPerBlock;
+using dev::u32x4;
+
+// Sum (low 16 bits meaningful) of the first r/2 words of a 16-byte chunk given
+// as four dwords; r even in [0, 16).  Wave-uniform inputs: scalar code.
+__device__ __forceinline__ uint32_t words_before(uint32_t r, uint32_t x, uint32_t y, uint32_t z, uint32_t w) {
+  const uint32_t nw = r >> 1;
+  uint32_t h = 0;
+  if (nw >= 2) h += x + (x >> 16);
+  if (nw >= 4) h += y + (y >> 16);
+  if (nw >= 6) h += z + (z >> 16);
+  if (nw & 1) {
+    const uint32_t d = nw == 1 ? x : (nw == 3 ? y : (nw == 5 ? z : w));
+    h += d & 0xFFFFu;
+  }
+  return h;
+}
+
+template <int U, int OP, bool STAMP>
+__global__ void __launch_bounds__(kBlock) rstream_kernel(FixedStreamArgs a) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t W = static_cast<uint64_t>(gridDim.x) * kWavesPerBlock;
+  const uint64_t wid = static_cast<uint64_t>(blockIdx.x) * kWavesPerBlock + (threadIdx.x >> 6);
+  uint64_t t_start = 0;
+  if (STAMP) t_start = __builtin_amdgcn_s_memrealtime();
+  const uint64_t N = a.count;
+  const uint64_t kb = wid * N / W;
+  const uint64_t ke = (wid + 1) * N / W;
+  if (kb >= ke) return;
+  const uint32_t S = static_cast<uint32_t>(a.stride);
+  const uint64_t s0 = kb * S;
+  const uint64_t A0 = dev::align128_rel(a.arena, s0);
+  const uint32_t lead = static_cast<uint32_t>(s0 - A0);
+  const uint32_t span = lead + static_cast<uint32_t>(ke - kb) * S;
+  const uint32_t nsteps = (span + 1023) >> 10;
+  const uint32_t last_chunk = (span - 1) >> 4;
+  const uint8_t *base = a.arena + A0;
+
+  auto load_step = [&](uint32_t st) -> u32x4 {
+    const uint32_t ci = min((st << 6) + lane, last_chunk);  // clamp: always a legal address
+    return dev::load16_nt(base + 16 * static_cast<uint64_t>(ci));
+  };
+
+  // wave-uniform boundary walk (relative to A0)
+  uint32_t nb = lead + S;   // next interior boundary = start of image kn
+  uint64_t kn = kb + 1;
+  uint32_t nf = lead + 28;  // kFill: next checksum field to zero (image kn - 1)
+  uint32_t carry = 0;       // P at the step start
+  uint32_t p_last = 0;      // P at the latest boundary (run start: 0)
+  // results staged in lane (k - out_base) until 64 are ready
+  uint32_t stage = 0;
+  uint64_t out_base = kb;
+
+  auto flush = [&](uint32_t n) {  // store staged results for images out_base .. out_base + n - 1
+    if (lane < n) {
+      const uint64_t k = out_base + lane;
+      const uint16_t c = static_cast<uint16_t>(stage);
+      if constexpr (OP == kVerify) {
+        static_cast<uint8_t *>(a.out)[k] = (c == 0) ? 1 : 0;
+      } else {
+        if (a.out) static_cast<uint16_t *>(a.out)[k] = c;
+        if (OP == kFill) *reinterpret_cast<uint16_t *>(a.arena + k * S + 28) = c;  // tcp-header.h:177
+      }
+    }
+  };
+  auto emit = [&](uint64_t k, uint32_t sum) {  // k = image index, sum = its word sum
+    const uint32_t j = static_cast<uint32_t>(k - out_base);
+    stage = lane == j ? (~sum & 0xFFFFu) : stage;  // j, sum wave-uniform: v_cmp + v_cndmask
+    if (j == 63) {
+      flush(64);
+      out_base += 64;
+    }
+  };
+
+  u32x4 ring[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) ring[u] = load_step(static_cast<uint32_t>(u));
+
+  for (uint32_t g = 0; g < nsteps; g += U) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t st = g + u;  // steps past nsteps: masked to zero, no boundary, harmless
+      const uint32_t sb = st << 10;
+      u32x4 w = ring[u];
+      if (sb == 0 || sb + 1024 > span) {  // run edge (wave-uniform): keep words of [lead, span) only
+        const int32_t crel = static_cast<int32_t>(sb + (lane << 4));
+        const int32_t lo = min(max(static_cast<int32_t>(lead) - crel, 0), 16);
+        const int32_t hi = min(max(static_cast<int32_t>(span) - crel, 0), 16);
+        w = dev::apply_mask(w, dev::word_mask(lo, hi));
+      }
+      if constexpr (OP == kFill) {  // zero the checksum fields passing through this step
+        while (nf < sb + 1024 && nf < span) {
+          const uint32_t rel = nf - sb;
+          if (lane == (rel >> 4)) {
+            const uint32_t wi = (rel & 15u) >> 1;
+            const uint32_t keep = (wi & 1u) ? 0x0000FFFFu : 0xFFFF0000u;
+            const uint32_t di = wi >> 1;
+            if (di == 0) w.x &= keep;
+            if (di == 1) w.y &= keep;
+            if (di == 2) w.z &= keep;
+            if (di == 3) w.w &= keep;
+          }
+          nf += S;
+        }
+      }
+      const uint32_t tot = dev::ref_chunk_sum(w);
+      const uint32_t incl = dev::wave_inclusive_scan(tot);
+      while (nb < sb + 1024 && kn < ke) {  // scalar: boundaries in this step
+        const uint32_t rel = nb - sb;
+        const uint32_t lb = rel >> 4;
+        const uint32_t r = rel & 15u;
+        uint32_t P = carry + dev::read_lane(incl, lb) - dev::read_lane(tot, lb);
+        if (r)
+          P += words_before(r, dev::read_lane(w.x, lb), dev::read_lane(w.y, lb), dev::read_lane(w.z, lb),
+                            dev::read_lane(w.w, lb));
+        emit(kn - 1, P - p_last);
+        p_last = P;
+        nb += S;
+        ++kn;
+      }
+      carry += dev::read_lane(incl, 63);
+      ring[u] = load_step(st + U);  // the slot's data is dead: refill in place
+    }
+  }
+  emit(ke - 1, carry - p_last);  // the last image ends at the run end
+  const uint32_t pending = static_cast<uint32_t>(ke - out_base);
+  if (pending) flush(pending);
+  if (STAMP && lane == 0 && a.dbg) {
+    a.dbg[2 * wid] = t_start;
+    a.dbg[2 * wid + 1] = __builtin_amdgcn_s_memrealtime();
+  }
+}
+
+template <int U, int OP, bool STAMP>
+hipError_t launch_one(const FixedStreamArgs &a, uint32_t num_cus, hipStream_t stream) {
+  static const uint32_t per_cu = dev::resident_blocks_per_cu(rstream_kernel<U, OP, STAMP>);
+  uint64_t blocks = static_cast<uint64_t>(per_cu) * num_cus;
+  const uint64_t need = (a.count + kWavesPerBlock - 1) / kWavesPerBlock;  // >= 1 image per wave
+  if (blocks > need) blocks = need;
+  if (blocks == 0) return hipSuccess;
+  hipLaunchKernelGGL((rstream_kernel<U, OP, STAMP>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0, stream, a);
+  return hipGetLastError();
+}
+
+template <int U, bool STAMP>
+hipError_t dispatch(int op, const FixedStreamArgs &a, uint32_t num_cus, hipStream_t s) {
+  switch (op) {
+    case kChecksum: return launch_one<U, kChecksum, STAMP>(a, num_cus, s);
+    case kFill: return launch_one<U, kFill, STAMP>(a, num_cus, s);
+    case kVerify: return launch_one<U, kVerify, STAMP>(a, num_cus, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace
+
+hipError_t launch_rstream(int op, int variant, const FixedStreamArgs &a, uint32_t num_cus, hipStream_t stream) {
+  // per-wave run must stay below 2^31 bytes (u32 run arithmetic)
+  if (a.stride < 16 || a.count == 0) return hipErrorInvalidValue;
+  const uint64_t max_run = ((a.count + 2047) / 2048 + 1) * a.stride + 128;
+  if (max_run >= (uint64_t{1} << 31)) return hipErrorInvalidValue;
+  switch (variant) {
+    case 0: return dispatch<4, false>(op, a, num_cus, stream);
+    case 1: return dispatch<2, false>(op, a, num_cus, stream);
+    case 2: return dispatch<8, false>(op, a, num_cus, stream);
+    case 3: return op == kChecksum ? launch_one<4, kChecksum, true>(a, num_cus, stream) : hipErrorInvalidValue;
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace tcpck

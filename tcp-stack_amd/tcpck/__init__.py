@@ -42,8 +42,9 @@ KERNEL_SPAN = 2   # param: images per tile (1..63), 0 = by length
 KERNEL_STREAM = 3  # param: variant 0 (U4 nt), 1 (U8 nt), 2 (U4 plain), 3 (U2 nt)
 STREAM_VARIANTS = {0: "U4/nt", 1: "U8/nt", 2: "U4/plain", 3: "U2/nt"}
 KERNEL_FSTREAM = 4  # fixed stride == len: param = tile (low 16 bits, 0 = auto) | variant << 16
+KERNEL_RSTREAM = 5  # fixed stride == len: param = variant 0 (U4), 1 (U2), 2 (U8), 3 (U4 + stamps)
 SEG_SHAPES = {1: "G8/U2", 2: "G16/U6", 3: "G64/U4", 4: "G64/U2", 5: "G32/U3", 6: "G4/U8"}
-TUNING_EXPORTS = ("tcpck_batch_fixed_ex", "tcpck_batch_var_ex")
+TUNING_EXPORTS = ("tcpck_batch_fixed_ex", "tcpck_batch_var_ex", "tcpck_ctx_set_debug")
 
 # Every symbol include/tcpck.h declares (checked by tests/test_abi.py).
 EXPORTS = (
@@ -109,6 +110,7 @@ def lib() -> ctypes.CDLL:
         # include/tcpck_tuning.h
         "tcpck_batch_fixed_ex": (i32, [vp, i32, i32, vp, u64, u32, u64, vp, i32, i32, vp]),
         "tcpck_batch_var_ex": (i32, [vp, i32, i32, vp, vp, vp, u64, vp, ctypes.POINTER(Layout), i32, i32, vp]),
+        "tcpck_ctx_set_debug": (i32, [vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -257,6 +259,10 @@ class Context:
                        mode: int = MODE_REF) -> None:
         _check(lib().tcpck_host_batch_var(self._h, op, mode, _ptr(arena), _ptr(offsets),
                                           _ptr(lengths), count, _ptr(out)), "tcpck_host_batch_var")
+
+    def set_debug(self, buf) -> None:
+        """Per-wave {start, end} stamp buffer for timing builds (None = off)."""
+        _check(lib().tcpck_ctx_set_debug(self._h, _ptr(buf)), "tcpck_ctx_set_debug")
 
     def set_chunk_bytes(self, n: int) -> None:
         _check(lib().tcpck_ctx_set_chunk_bytes(self._h, n), "tcpck_ctx_set_chunk_bytes")
