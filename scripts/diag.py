@@ -71,7 +71,7 @@ def stamps(ctx, arena, out, stream):
     wid = np.nonzero(dbg.cpu().numpy().reshape(-1, 2)[:, 1] > 0)[0]
     by = {}
     for x in range(8):
-        sel = (wid % 8) == x
+        sel = ((wid // 4) % 8) == x
         by[x] = float(np.median(en[sel])) if sel.any() else 0.0
     print("stamps: median end by block-id mod 8 (XCD group):", {k: round(v, 1) for k, v in by.items()}, flush=True)
 
