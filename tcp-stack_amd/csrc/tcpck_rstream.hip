@@ -161,8 +161,13 @@ __global__ void __launch_bounds__(kBlock) rstream_kernel(FixedStreamArgs a) {
   const uint32_t pending = static_cast<uint32_t>(ke - out_base);
   if (pending) flush(pending);
   if (STAMP && lane == 0 && a.dbg) {
-    a.dbg[2 * wid] = t_start;
-    a.dbg[2 * wid + 1] = __builtin_amdgcn_s_memrealtime();
+    uint32_t hw_id, xcc_id;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw_id));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc_id));
+    a.dbg[4 * wid] = t_start;
+    a.dbg[4 * wid + 1] = __builtin_amdgcn_s_memrealtime();
+    a.dbg[4 * wid + 2] = hw_id;
+    a.dbg[4 * wid + 3] = xcc_id;
   }
 }
 

@@ -261,7 +261,7 @@ class Context:
                                           _ptr(lengths), count, _ptr(out)), "tcpck_host_batch_var")
 
     def set_debug(self, buf) -> None:
-        """Per-wave {start, end} stamp buffer for timing builds (None = off)."""
+        """Per-wave {start, end, hw_id, xcc_id} stamp buffer for timing builds (None = off)."""
         _check(lib().tcpck_ctx_set_debug(self._h, _ptr(buf)), "tcpck_ctx_set_debug")
 
     def set_chunk_bytes(self, n: int) -> None:

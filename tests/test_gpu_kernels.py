@@ -275,7 +275,7 @@ def test_rstream_fixed_vs_oracle(ctx, oracle_c, variant, length, count):
     if count * length > (64 << 20):
         count = (64 << 20) // length
     rng = np.random.default_rng(length * 7 + count + variant)
-    arena_np = rng.integers(0, 256, count * length + 32, dtype=np.uint8)
+    arena_np = rng.integers(0, 256, count * length + 128, dtype=np.uint8)  # room for mis <= 126
     arena_np[:length] = 0xFF
     buf = dev(arena_np)
     for mis in (0, 2, 14, 126):
