@@ -29,7 +29,10 @@ extern "C" {
 #define TCPCK_KERNEL_RSTREAM 5 /* fixed stride == len only, MODE_REF: one run per
                                   wave, scalar boundary walk; param = variant
                                   (0: 4 loads in flight, 1: 2, 2: 8, 3: 4 with
-                                  per-wave time stamps, checksum only)          */
+                                  per-wave time stamps, checksum only; 4/6/8:
+                                  4/8/2 loads with slot-graded s_setprio, 5: 4
+                                  with s_setprio 1 for slots >= 4, 7: 3 + graded
+                                  priority) | (blocks per CU cap << 8)          */
 
 int tcpck_batch_fixed_ex(tcpck_ctx *ctx, int op, int mode, void *d_arena,
                          uint64_t stride, uint32_t len, uint64_t count, void *d_out,

@@ -200,7 +200,8 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
     a.count = count;
     a.out = out;
     a.dbg = static_cast<uint64_t *>(ctx->dbg);
-    return tcpck::launch_rstream(op, param, a, static_cast<uint32_t>(ctx->num_cus), s);
+    a.blocks_per_cu = static_cast<uint32_t>(param >> 8) & 0xFFu;
+    return tcpck::launch_rstream(op, param & 0xFF, a, static_cast<uint32_t>(ctx->num_cus), s);
   }
   if (kernel != TCPCK_KERNEL_SEG) return hipErrorInvalidValue;
   SegArgs a{};

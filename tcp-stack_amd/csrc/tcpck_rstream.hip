@@ -51,13 +51,33 @@ __device__ __forceinline__ uint32_t words_before(uint32_t r, uint32_t x, uint32_
   return h;
 }
 
-template <int U, int OP, bool STAMP>
+// PRIO: 0 = default arbitration; 1 = s_setprio(wave slot / 2), 2 = s_setprio(1)
+// for slots >= 4 -- the SIMD issues by priority, then age, so younger waves
+// (higher slots) otherwise starve: identical runs took 105 us in slot 0 and
+// 224 us in slot 7 of a C2 launch (scripts/stamps.py).
+template <int U, int OP, bool STAMP, int PRIO = 0>
 __global__ void __launch_bounds__(kBlock) rstream_kernel(FixedStreamArgs a) {
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t W = static_cast<uint64_t>(gridDim.x) * kWavesPerBlock;
   const uint64_t wid = static_cast<uint64_t>(blockIdx.x) * kWavesPerBlock + (threadIdx.x >> 6);
   uint64_t t_start = 0;
   if (STAMP) t_start = __builtin_amdgcn_s_memrealtime();
+  if (PRIO) {
+    uint32_t hw;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    const uint32_t slot = hw & 0xFu;
+    if (PRIO == 1) {
+      if (slot >= 6) {
+        __builtin_amdgcn_s_setprio(3);
+      } else if (slot >= 4) {
+        __builtin_amdgcn_s_setprio(2);
+      } else if (slot >= 2) {
+        __builtin_amdgcn_s_setprio(1);
+      }
+    } else if (slot >= 4) {
+      __builtin_amdgcn_s_setprio(1);
+    }
+  }
   const uint64_t N = a.count;
   const uint64_t kb = wid * N / W;
   const uint64_t ke = (wid + 1) * N / W;
@@ -171,23 +191,25 @@ __global__ void __launch_bounds__(kBlock) rstream_kernel(FixedStreamArgs a) {
   }
 }
 
-template <int U, int OP, bool STAMP>
+template <int U, int OP, bool STAMP, int PRIO = 0>
 hipError_t launch_one(const FixedStreamArgs &a, uint32_t num_cus, hipStream_t stream) {
-  static const uint32_t per_cu = dev::resident_blocks_per_cu(rstream_kernel<U, OP, STAMP>);
-  uint64_t blocks = static_cast<uint64_t>(per_cu) * num_cus;
+  static const uint32_t per_cu = dev::resident_blocks_per_cu(rstream_kernel<U, OP, STAMP, PRIO>);
+  const uint32_t cap = (a.blocks_per_cu && a.blocks_per_cu < per_cu) ? a.blocks_per_cu : per_cu;
+  uint64_t blocks = static_cast<uint64_t>(cap) * num_cus;
   const uint64_t need = (a.count + kWavesPerBlock - 1) / kWavesPerBlock;  // >= 1 image per wave
   if (blocks > need) blocks = need;
   if (blocks == 0) return hipSuccess;
-  hipLaunchKernelGGL((rstream_kernel<U, OP, STAMP>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0, stream, a);
+  hipLaunchKernelGGL((rstream_kernel<U, OP, STAMP, PRIO>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0,
+                     stream, a);
   return hipGetLastError();
 }
 
-template <int U, bool STAMP>
+template <int U, bool STAMP, int PRIO = 0>
 hipError_t dispatch(int op, const FixedStreamArgs &a, uint32_t num_cus, hipStream_t s) {
   switch (op) {
-    case kChecksum: return launch_one<U, kChecksum, STAMP>(a, num_cus, s);
-    case kFill: return launch_one<U, kFill, STAMP>(a, num_cus, s);
-    case kVerify: return launch_one<U, kVerify, STAMP>(a, num_cus, s);
+    case kChecksum: return launch_one<U, kChecksum, STAMP, PRIO>(a, num_cus, s);
+    case kFill: return launch_one<U, kFill, STAMP, PRIO>(a, num_cus, s);
+    case kVerify: return launch_one<U, kVerify, STAMP, PRIO>(a, num_cus, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -204,6 +226,11 @@ hipError_t launch_rstream(int op, int variant, const FixedStreamArgs &a, uint32_
     case 1: return dispatch<2, false>(op, a, num_cus, stream);
     case 2: return dispatch<8, false>(op, a, num_cus, stream);
     case 3: return op == kChecksum ? launch_one<4, kChecksum, true>(a, num_cus, stream) : hipErrorInvalidValue;
+    case 4: return dispatch<4, false, 1>(op, a, num_cus, stream);
+    case 5: return dispatch<4, false, 2>(op, a, num_cus, stream);
+    case 6: return dispatch<8, false, 1>(op, a, num_cus, stream);
+    case 7: return op == kChecksum ? launch_one<4, kChecksum, true, 1>(a, num_cus, stream) : hipErrorInvalidValue;
+    case 8: return dispatch<2, false, 1>(op, a, num_cus, stream);
     default: return hipErrorInvalidValue;
   }
 }
