@@ -41,6 +41,12 @@ int tcpck_batch_fixed_ex(tcpck_ctx *ctx, int op, int mode, void *d_arena,
  * (100 MHz) stamps from kernels built with stamps (NULL = off). */
 int tcpck_ctx_set_debug(tcpck_ctx *ctx, void *d_buf);
 
+/* Timing-only streaming micro-kernel over d_buf (results are not checksums):
+ * variant = chunks per lane per step x steps in flight x scan, see
+ * tcp-stack_amd/csrc/tcpck_diag.hip.  d_out: u32 per wave. */
+int tcpck_diag_stream(tcpck_ctx *ctx, int variant, const void *d_buf, uint64_t bytes, void *d_out,
+                      tcpck_stream stream);
+
 int tcpck_batch_var_ex(tcpck_ctx *ctx, int op, int mode, void *d_arena,
                        const uint64_t *d_offsets, const uint32_t *d_lengths,
                        uint64_t count, void *d_out, const tcpck_layout *layout,

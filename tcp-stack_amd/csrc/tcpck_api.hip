@@ -378,6 +378,15 @@ int tcpck_batch_var(tcpck_ctx *ctx, int op, int mode, void *d_arena, const uint6
                             TCPCK_KERNEL_AUTO, 0, stream);
 }
 
+int tcpck_diag_stream(tcpck_ctx *ctx, int variant, const void *d_buf, uint64_t bytes, void *d_out,
+                      tcpck_stream stream) {
+  if (!ctx || !d_buf || !d_out || bytes < 4096) return TCPCK_EINVAL;
+  DeviceGuard g(ctx->device);
+  return hip_status(tcpck::launch_diag_stream(variant, static_cast<const uint8_t *>(d_buf), bytes,
+                                              static_cast<uint32_t *>(d_out), static_cast<uint32_t>(ctx->num_cus),
+                                              static_cast<hipStream_t>(stream)));
+}
+
 int tcpck_ctx_set_debug(tcpck_ctx *ctx, void *d_buf) {
   if (!ctx) return TCPCK_EINVAL;
   ctx->dbg = d_buf;

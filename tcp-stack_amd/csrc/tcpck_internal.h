@@ -73,6 +73,9 @@ struct FixedStreamArgs {
 // ---- run-stream kernel (fixed stride == len): one run per wave, scalar boundaries
 // variant: 0 = 4 loads in flight, 1 = 2, 2 = 8, 3 = 4 with per-wave time stamps
 hipError_t launch_rstream(int op, int variant, const FixedStreamArgs &a, uint32_t num_cus, hipStream_t stream);
+// timing-only streaming micro-kernels (tcpck_diag.hip)
+hipError_t launch_diag_stream(int variant, const uint8_t *buf, uint64_t bytes, uint32_t *out, uint32_t num_cus,
+                              hipStream_t s);
 uint32_t fstream_min_tile(uint32_t stride, int variant);
 uint32_t fstream_tile_for_len(uint32_t stride, int variant);
 // variant: 0 = 4 loads in flight per lane, 1 = 2

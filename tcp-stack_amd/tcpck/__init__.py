@@ -44,7 +44,7 @@ STREAM_VARIANTS = {0: "U4/nt", 1: "U8/nt", 2: "U4/plain", 3: "U2/nt"}
 KERNEL_FSTREAM = 4  # fixed stride == len: param = tile (low 16 bits, 0 = auto) | variant << 16
 KERNEL_RSTREAM = 5  # fixed stride == len: param = variant 0 (U4), 1 (U2), 2 (U8), 3 (U4 + stamps)
 SEG_SHAPES = {1: "G8/U2", 2: "G16/U6", 3: "G64/U4", 4: "G64/U2", 5: "G32/U3", 6: "G4/U8"}
-TUNING_EXPORTS = ("tcpck_batch_fixed_ex", "tcpck_batch_var_ex", "tcpck_ctx_set_debug")
+TUNING_EXPORTS = ("tcpck_batch_fixed_ex", "tcpck_batch_var_ex", "tcpck_ctx_set_debug", "tcpck_diag_stream")
 
 # Every symbol include/tcpck.h declares (checked by tests/test_abi.py).
 EXPORTS = (
@@ -111,6 +111,7 @@ def lib() -> ctypes.CDLL:
         "tcpck_batch_fixed_ex": (i32, [vp, i32, i32, vp, u64, u32, u64, vp, i32, i32, vp]),
         "tcpck_batch_var_ex": (i32, [vp, i32, i32, vp, vp, vp, u64, vp, ctypes.POINTER(Layout), i32, i32, vp]),
         "tcpck_ctx_set_debug": (i32, [vp, vp]),
+        "tcpck_diag_stream": (i32, [vp, i32, vp, u64, vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -259,6 +260,11 @@ class Context:
                        mode: int = MODE_REF) -> None:
         _check(lib().tcpck_host_batch_var(self._h, op, mode, _ptr(arena), _ptr(offsets),
                                           _ptr(lengths), count, _ptr(out)), "tcpck_host_batch_var")
+
+    def diag_stream(self, variant: int, buf, nbytes: int, out, stream=None) -> None:
+        """Timing-only streaming micro-kernel (include/tcpck_tuning.h)."""
+        _check(lib().tcpck_diag_stream(self._h, variant, _ptr(buf), nbytes, _ptr(out), _stream(stream)),
+               "tcpck_diag_stream")
 
     def set_debug(self, buf) -> None:
         """Per-wave {start, end, hw_id, xcc_id} stamp buffer for timing builds (None = off)."""
