@@ -59,7 +59,11 @@ template <int U, int OP, bool STAMP, int PRIO = 0>
 __global__ void __launch_bounds__(kBlock) rstream_kernel(FixedStreamArgs a) {
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t W = static_cast<uint64_t>(gridDim.x) * kWavesPerBlock;
-  const uint64_t wid = static_cast<uint64_t>(blockIdx.x) * kWavesPerBlock + (threadIdx.x >> 6);
+  // readfirstlane: the wave index is uniform, but hipcc cannot prove anything
+  // derived from threadIdx is; without it every boundary variable below lives
+  // in VGPRs and each uniform test becomes an exec-masked region
+  const uint64_t wid = static_cast<uint64_t>(blockIdx.x) * kWavesPerBlock +
+                       static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6)));
   uint64_t t_start = 0;
   if (STAMP) t_start = __builtin_amdgcn_s_memrealtime();
   if (PRIO) {
@@ -96,19 +100,21 @@ __global__ void __launch_bounds__(kBlock) rstream_kernel(FixedStreamArgs a) {
     return dev::load16_nt(base + 16 * static_cast<uint64_t>(ci));
   };
 
-  // wave-uniform boundary walk (relative to A0)
-  uint32_t nb = lead + S;   // next interior boundary = start of image kn
-  uint64_t kn = kb + 1;
-  uint32_t nf = lead + 28;  // kFill: next checksum field to zero (image kn - 1)
+  // wave-uniform boundary walk, all in 32-bit run-relative terms (SGPRs):
+  // image jn of the run starts at byte nb (relative to A0)
+  const uint32_t nimg = static_cast<uint32_t>(ke - kb);
+  uint32_t nb = lead + S;
+  uint32_t jn = 1;
+  uint32_t nf = lead + 28;  // kFill: next checksum field to zero
   uint32_t carry = 0;       // P at the step start
   uint32_t p_last = 0;      // P at the latest boundary (run start: 0)
-  // results staged in lane (k - out_base) until 64 are ready
+  // results staged in lane (j - out_rel) until 64 are ready
   uint32_t stage = 0;
-  uint64_t out_base = kb;
+  uint32_t out_rel = 0;
 
-  auto flush = [&](uint32_t n) {  // store staged results for images out_base .. out_base + n - 1
+  auto flush = [&](uint32_t n) {  // store staged results for run images out_rel .. out_rel + n - 1
     if (lane < n) {
-      const uint64_t k = out_base + lane;
+      const uint64_t k = kb + out_rel + lane;
       const uint16_t c = static_cast<uint16_t>(stage);
       if constexpr (OP == kVerify) {
         static_cast<uint8_t *>(a.out)[k] = (c == 0) ? 1 : 0;
@@ -118,12 +124,12 @@ __global__ void __launch_bounds__(kBlock) rstream_kernel(FixedStreamArgs a) {
       }
     }
   };
-  auto emit = [&](uint64_t k, uint32_t sum) {  // k = image index, sum = its word sum
-    const uint32_t j = static_cast<uint32_t>(k - out_base);
+  auto emit = [&](uint32_t jr, uint32_t sum) {  // jr = run-relative image index, sum = its word sum
+    const uint32_t j = jr - out_rel;
     stage = lane == j ? (~sum & 0xFFFFu) : stage;  // j, sum wave-uniform: v_cmp + v_cndmask
     if (j == 63) {
       flush(64);
-      out_base += 64;
+      out_rel += 64;
     }
   };
 
@@ -160,7 +166,7 @@ __global__ void __launch_bounds__(kBlock) rstream_kernel(FixedStreamArgs a) {
       }
       const uint32_t tot = dev::ref_chunk_sum(w);
       const uint32_t incl = dev::wave_inclusive_scan(tot);
-      while (nb < sb + 1024 && kn < ke) {  // scalar: boundaries in this step
+      while (nb < sb + 1024 && jn < nimg) {  // scalar: boundaries in this step
         const uint32_t rel = nb - sb;
         const uint32_t lb = rel >> 4;
         const uint32_t r = rel & 15u;
@@ -168,17 +174,17 @@ __global__ void __launch_bounds__(kBlock) rstream_kernel(FixedStreamArgs a) {
         if (r)
           P += words_before(r, dev::read_lane(w.x, lb), dev::read_lane(w.y, lb), dev::read_lane(w.z, lb),
                             dev::read_lane(w.w, lb));
-        emit(kn - 1, P - p_last);
+        emit(jn - 1, P - p_last);
         p_last = P;
         nb += S;
-        ++kn;
+        ++jn;
       }
       carry += dev::read_lane(incl, 63);
       ring[u] = load_step(st + U);  // the slot's data is dead: refill in place
     }
   }
-  emit(ke - 1, carry - p_last);  // the last image ends at the run end
-  const uint32_t pending = static_cast<uint32_t>(ke - out_base);
+  emit(nimg - 1, carry - p_last);  // the last image ends at the run end
+  const uint32_t pending = nimg - out_rel;
   if (pending) flush(pending);
   if (STAMP && lane == 0 && a.dbg) {
     uint32_t hw_id, xcc_id;
