@@ -160,7 +160,10 @@ constexpr uint64_t kSpanMaxLen = 16384;
 hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t stride, uint32_t len,
                      uint64_t count, void *out, int kernel, int param, hipStream_t s) {
   const bool span_ok = mode == TCPCK_MODE_REF && stride == len && len >= 16 && len <= (1u << 24);
-  if (kernel == TCPCK_KERNEL_AUTO) kernel = (span_ok && len <= kSpanMaxLen) ? TCPCK_KERNEL_SPAN : TCPCK_KERNEL_SEG;
+  // packed fixed stride, reference mode: the run-stream kernel (82.6% of the
+  // HBM roof on C2, scripts/prio.py); jumbo images stay on seg (G64/U4), which
+  // streams whole 16-B-aligned images per wave at the same rate
+  if (kernel == TCPCK_KERNEL_AUTO) kernel = (span_ok && len <= kSpanMaxLen) ? TCPCK_KERNEL_RSTREAM : TCPCK_KERNEL_SEG;
   if (kernel == TCPCK_KERNEL_SPAN) {
     if (!span_ok) return hipErrorInvalidValue;
     tcpck::SpanArgs a{};
