@@ -23,5 +23,9 @@ for s in ${STEPS:-tests smoke bench prof}; do
     sweep) step sweep 900 python scripts/sweep.py ;;
     bench_c4) step bench_c4 600 python bench.py --config c4 --no-cpu-baseline ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-e2e ;;
+    pmc_c2|pmc_c3|pmc_c4)  # separate FETCH_SIZE / WRITE_SIZE passes (TCC slots), kernel trace only
+      c=${s#pmc_}
+      step ${s}_fetch 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d gpurun_out/pmc_${c}_fetch -o run --output-format csv -- python3 bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline --no-e2e
+      step ${s}_write 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d gpurun_out/pmc_${c}_write -o run --output-format csv -- python3 bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline --no-e2e ;;
   esac
 done
