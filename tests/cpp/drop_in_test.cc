@@ -1,0 +1,162 @@
+// drop_in_test.cc -- exercises the drop-in C++ header (include/tcp_stack/) the
+// way the reference's call sites use it.  Driven by tests/test_drop_in.py.
+//
+//   drop_in_test golden <blob> <manifest>   one output line per manifest case
+//       manifest line: <kind> <off> <len>; kind checksum|fill|verify
+//       checksum -> CalculateChecksum(*MakeNetPacket(image))        (tcp-header.h:252-263)
+//       fill     -> Checksum()=0; Checksum()=CalculateChecksum(...)  (socket-manager.cc:9-10)
+//                   prints the stored value, then CalculateChecksum of the result
+//       verify   -> CalculateChecksum(...) == 0                      (socket-manager.h:182)
+//   drop_in_test layout                      header field layout / H2N / flags / operator<<
+//   drop_in_test batch <n> <seed>            PacketBatch (GPU) vs per-packet CalculateChecksum
+#include <tcp_stack/packet-batch.h>
+#include <tcp_stack/tcp-header.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <iostream>
+#include <random>
+#include <sstream>
+#include <vector>
+
+using namespace tcp_stack;
+
+static int Golden(const char *blob_path, const char *manifest) {
+  std::ifstream bf(blob_path, std::ios::binary);
+  std::vector<char> blob((std::istreambuf_iterator<char>(bf)), std::istreambuf_iterator<char>());
+  std::ifstream mf(manifest);
+  std::string kind;
+  size_t off, len;
+  while (mf >> kind >> off >> len) {
+    if (off + len > blob.size()) return 2;
+    auto pkt = MakeNetPacket(blob.data() + off, len);
+    if (kind == "checksum") {
+      std::printf("%u\n", CalculateChecksum(*pkt));
+    } else if (kind == "fill") {
+      auto &h = pkt->GetHeader();
+      h.Checksum() = 0;
+      h.Checksum() = CalculateChecksum(*pkt);
+      std::printf("%u %u\n", h.Checksum(), CalculateChecksum(*pkt));
+    } else if (kind == "verify") {
+      std::printf("%d\n", CalculateChecksum(*pkt) == 0 ? 1 : 0);
+    } else {
+      return 3;
+    }
+  }
+  return 0;
+}
+
+static int Layout() {
+  // The structured header of SURVEY.md §8c / tests/golden (struct_hdr/32).
+  auto pkt = MakeTcpPacket(0);
+  TcpHeader &h = pkt->GetHeader();
+  h.SourceAddress() = 0x7f000001u;       // 127.0.0.1
+  h.DestinationAddress() = 0x0a000002u;  // 10.0.0.2
+  h.PTCL() = 6;
+  h.TcpLength() = 0x1234;
+  h.SourcePort() = 0xabcd;
+  h.DestinationPort() = 10;
+  h.SequenceNumber() = 0x11223344u;
+  h.AcknowledgementNumber() = 0x55667788u;
+  h.Window() = 1024;
+  h.UrgentPointer() = 0x0102;
+  h.SetAck(true);
+  h.SetSyn(true);
+  std::ostringstream text;
+  text << h;
+  std::printf("text %s\n", text.str().c_str());
+  TcpHeaderH2N(h);
+  h.Checksum() = 0;
+  const auto buf = pkt->GetBuffer();
+  std::printf("size %zu\nbytes", buf.second);
+  for (size_t i = 0; i < buf.second; ++i) std::printf(" %02x", static_cast<unsigned char>(buf.first[i]));
+  std::printf("\n");
+  h.Checksum() = CalculateChecksum(*pkt);
+  std::printf("checksum %u\nreverify %u\n", h.Checksum(), CalculateChecksum(*pkt));
+  TcpHeaderN2H(h);
+  std::printf("n2h %x %x %u %x\n", h.SourceAddress(), h.SequenceNumber(), h.Window(), h.TcpLength());
+  // flag bits land in byte 25 exactly as the reference's bit positions 106..111
+  auto p2 = MakeTcpPacket(0);
+  const unsigned char *b = reinterpret_cast<const unsigned char *>(p2->GetBuffer().first);
+  TcpHeader &g = p2->GetHeader();
+  g.SetUrg(true); std::printf("urg %02x\n", b[25]); g.SetUrg(false);
+  g.SetAck(true); std::printf("ack %02x\n", b[25]); g.SetAck(false);
+  g.SetPsh(true); std::printf("psh %02x\n", b[25]); g.SetPsh(false);
+  g.SetRst(true); std::printf("rst %02x\n", b[25]); g.SetRst(false);
+  g.SetSyn(true); std::printf("syn %02x\n", b[25]); g.SetSyn(false);
+  g.SetFin(true); std::printf("fin %02x\n", b[25]); g.SetFin(false);
+  std::printf("cleared %02x\n", b[25]);
+  // payload constructor: zeroed header + copied payload
+  const char payload[6] = {1, 2, 3, 4, 5, 6};
+  auto p3 = MakeTcpPacket(payload, sizeof(payload));
+  std::printf("payload %zu %d %d\n", p3->GetBuffer().second, p3->begin()[0], p3->end()[-1]);
+  // odd length: defined here (zero-padded last word), verifies after fill
+  const char odd[5] = {9, 8, 7, 6, 5};
+  auto p4 = MakeTcpPacket(odd, sizeof(odd));
+  p4->GetHeader().Checksum() = 0;
+  p4->GetHeader().Checksum() = CalculateChecksum(*p4);
+  std::printf("odd %u %u\n", p4->GetHeader().Checksum(), CalculateChecksum(*p4));
+  return 0;
+}
+
+static int Batch(size_t n, unsigned seed) {
+  std::mt19937_64 rng(seed);
+  const size_t lens[] = {0, 64, 576, 1460, 1461, 7, 4000};
+  std::vector<std::shared_ptr<TcpPacket>> pkts, copy;
+  for (size_t k = 0; k < n; ++k) {
+    const size_t pl = lens[rng() % (sizeof(lens) / sizeof(lens[0]))];
+    std::vector<char> payload(pl);
+    for (auto &c : payload) c = static_cast<char>(rng());
+    auto p = MakeTcpPacket(payload.data(), pl);
+    TcpHeader &h = p->GetHeader();
+    h.SourceAddress() = 0x7f000001u;
+    h.DestinationAddress() = 0x7f000001u;
+    h.PTCL() = 6;
+    h.TcpLength() = static_cast<uint16_t>(pl);
+    h.SourcePort() = 15500;
+    h.DestinationPort() = 15501;
+    h.SequenceNumber() = static_cast<uint32_t>(1000 + k);
+    h.SetAck(true);
+    h.Window() = 1024;
+    TcpHeaderH2N(h);
+    h.Checksum() = static_cast<uint16_t>(rng());  // stale field: fill must ignore it
+    auto b = p->GetBuffer();
+    copy.push_back(MakeNetPacket(b.first, b.second));
+    pkts.push_back(std::move(p));
+  }
+  PacketBatch batch(0, PacketBatch::Thresholds{1, 1});
+  // checksums as-is
+  const std::vector<uint16_t> sums = batch.Checksums(pkts);
+  size_t bad = 0;
+  for (size_t k = 0; k < n; ++k) bad += sums[k] != CalculateChecksum(*copy[k]);
+  const size_t gpu_images = batch.last_gpu_images();
+  // send path: fill in place, compare with the per-packet reference sequence
+  batch.Fill(pkts);
+  for (size_t k = 0; k < n; ++k) {
+    TcpHeader &h = copy[k]->GetHeader();
+    h.Checksum() = 0;
+    h.Checksum() = CalculateChecksum(*copy[k]);
+    bad += pkts[k]->GetHeader().Checksum() != h.Checksum();
+  }
+  // receive path: every filled packet verifies; a flipped payload byte does not
+  std::vector<uint8_t> ok = batch.Verify(pkts);
+  for (size_t k = 0; k < n; ++k) bad += ok[k] != 1;
+  for (size_t k = 0; k < n; k += 3) {
+    auto b = pkts[k]->GetBuffer();
+    b.first[b.second - 1] ^= 0x10;
+  }
+  ok = batch.Verify(pkts);
+  for (size_t k = 0; k < n; ++k) bad += ok[k] != (k % 3 != 0);
+  std::printf("batch n=%zu gpu_images=%zu mismatches=%zu\n", n, gpu_images, bad);
+  return bad == 0 ? 0 : 1;
+}
+
+int main(int argc, char **argv) {
+  if (argc >= 4 && !std::strcmp(argv[1], "golden")) return Golden(argv[2], argv[3]);
+  if (argc >= 2 && !std::strcmp(argv[1], "layout")) return Layout();
+  if (argc >= 4 && !std::strcmp(argv[1], "batch")) return Batch(std::strtoull(argv[2], nullptr, 10), std::atoi(argv[3]));
+  std::fprintf(stderr, "usage: %s golden <blob> <manifest> | layout | batch <n> <seed>\n", argv[0]);
+  return 2;
+}

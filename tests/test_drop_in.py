@@ -1,0 +1,90 @@
+"""Drop-in C++ header (include/tcp_stack/tcp-header.h, packet-batch.h).
+
+Compiles tests/cpp/drop_in_test.cc against the headers and libtcpck.so and
+checks it against the reference's golden vectors (tests/golden, generated from
+/root/reference/include/tcp-header.h by tests/golden/gen_golden.cc) and the
+structured-header known answer (0x4ba4).  The CPU tests use
+only the host single-image path (tcpck_checksum16); the batch test runs
+PacketBatch on the GPU through tcpck_host_batch_var.
+"""
+import os
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+
+BUILD = os.path.join(ROOT, "tests", "cpp", "build")
+SRC = os.path.join(ROOT, "tests", "cpp", "drop_in_test.cc")
+LIBDIR = os.path.join(ROOT, "tcp-stack_amd")
+
+
+def build(variant: str) -> str:
+    """variant: 'asan' (host sanitizers, CPU tests) or 'opt'."""
+    os.makedirs(BUILD, exist_ok=True)
+    exe = os.path.join(BUILD, f"drop_in_test_{variant}")
+    deps = [SRC] + [os.path.join(ROOT, "include", "tcp_stack", f) for f in ("tcp-header.h", "packet-batch.h")]
+    if os.path.exists(exe) and all(os.path.getmtime(exe) >= os.path.getmtime(d) for d in deps):
+        return exe
+    flags = ["-O1", "-g", "-fsanitize=address,undefined", "-fno-sanitize-recover=all"] if variant == "asan" else ["-O2"]
+    cmd = (["g++", "-std=c++17", "-Wall", "-Wextra", "-Werror"] + flags +
+           ["-I", os.path.join(ROOT, "include"), SRC, "-o", exe, "-L", LIBDIR, "-ltcpck",
+            f"-Wl,-rpath,{LIBDIR}", "-Wl,-rpath-link,/opt/rocm/lib"])
+    subprocess.run(cmd, check=True)
+    return exe
+
+
+@pytest.fixture(scope="module")
+def exe(built_lib):
+    return build("asan")
+
+
+def run(exe, *args):
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0")
+    r = subprocess.run([exe, *map(str, args)], capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode == 0, r.stderr
+    return r.stdout.splitlines()
+
+
+def test_golden_vectors(exe, golden, tmp_path):
+    manifest = tmp_path / "manifest.txt"
+    manifest.write_text("".join(f"{c['kind']} {c['off']} {c['len']}\n" for c in golden.cases))
+    blob = os.path.join(ROOT, "tests", "golden", "golden.bin")
+    lines = run(exe, "golden", blob, manifest)
+    assert len(lines) == len(golden.cases)
+    for c, line in zip(golden.cases, lines):
+        vals = [int(v) for v in line.split()]
+        if c["kind"] == "fill":
+            assert vals == [c["expected"], 0], c["name"]
+        else:
+            assert vals[0] == c["expected"], c["name"]
+
+
+def test_layout_and_known_answer(exe, golden):
+    out = dict(line.split(" ", 1) for line in run(exe, "layout"))
+    assert out["text"] == "Ack Syn 43981->10 S287454020 A1432778632 L4660"
+    assert out["size"] == "32"
+    img = bytes(int(b, 16) for b in out["bytes"].split())
+    ref = [c for c in golden.cases if c["name"] == "struct_hdr/32" and c["kind"] == "checksum"][0]
+    assert img == bytes(golden.image(ref)), "header bytes differ from the reference's struct_hdr image"
+    assert int(out["checksum"]) == 0x4BA4
+    assert out["reverify"] == "0"
+    assert out["n2h"] == "7f000001 11223344 1024 1234"
+    assert [out[f] for f in ("urg", "ack", "psh", "rst", "syn", "fin", "cleared")] == \
+        ["04", "08", "10", "20", "40", "80", "00"]
+    assert out["payload"] == "38 1 6"
+    odd_sum, odd_verify = map(int, out["odd"].split())
+    assert odd_verify == 0
+    # odd rule: last byte is the low byte of a zero-padded word
+    from oracle.ref16 import ref16_np
+    import numpy as np
+    img = bytearray(32) + bytes([9, 8, 7, 6, 5]) + b"\0"
+    assert odd_sum == ref16_np(np.frombuffer(bytes(img), np.uint8))
+
+
+@pytest.mark.gpu
+def test_packet_batch_gpu(built_lib):
+    exe = build("opt")
+    lines = run(exe, "batch", 20000, 7)
+    assert lines[-1].endswith("mismatches=0"), lines
+    assert "gpu_images=0" not in lines[-1]
