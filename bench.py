@@ -49,7 +49,11 @@ CONFIGS = {
     "c3": ("C3: 4M images, payload uniform over {64,576,1460} B (96/608/1492-B images), packed, u64 offsets",
            "mixed", 4 << 20, None),
     "c4": ("C4: 256K x 64-KiB jumbo images (payload 65504), fixed stride", "fixed", 256 << 10, 65536),
+    # strong scaling: one 8M-image batch split evenly over the ranks (at N=8 each rank holds a C2)
+    "c5": ("C5: 8M x 1460-B payload (1492-B images) sharded evenly across the GPUs, fixed stride",
+           "fixed", 8 << 20, 1492),
 }
+STRONG = {"c5"}  # configs whose total work is fixed as N grows; the rest are per-GPU (weak)
 
 
 def log(*a):
@@ -83,10 +87,15 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
+    from tcpck.shard import max_over_ranks, shard_range
     desc, kind, count, L = CONFIGS[args.config]
     ctx = tcpck.Context(local)
     stream = torch.cuda.current_stream()
-    first = rank * count
+    if args.config in STRONG:
+        first, stop = shard_range(count, world, rank)  # independent contiguous shard, no exchange
+        count = stop - first
+    else:
+        first = rank * count  # weak: every rank checksums its own batch of the config's size
     if kind == "fixed":
         arena = torch.empty(count * L, dtype=torch.uint8, device="cuda")
         tcpck.synth_fixed(arena, L, L, count, seed=42, first_index=first, stream=stream)
@@ -129,11 +138,11 @@ def main():
     elapsed = time.perf_counter() - t0
     launch_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts, ends)]))
 
-    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    tmax = max_over_ranks(elapsed, device="cuda")
+    shard_bytes = torch.tensor([img_bytes], dtype=torch.int64, device="cuda")
     if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    tmax = float(t.item())
-    total_bytes = img_bytes * world * args.steps
+        dist.all_reduce(shard_bytes)  # bytes all ranks processed per step (shards may differ by one image)
+    total_bytes = int(shard_bytes.item()) * args.steps
     value = total_bytes / tmax / GIB
 
     # Checksum digest of this rank's results (parity spot-check on the host below).
@@ -154,7 +163,8 @@ def main():
     rec = {
         "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(tmax / args.steps * 1e3, 5),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u16",
+        "higher_is_better": True,
+        "scaling": "strong" if args.config in STRONG else "weak", "vs_baseline": None, "dtype": "u16",
         "data": "synthetic (device-generated: send-path headers + splitmix64 payloads, seed 42)",
         "config": {"workload": desc, "images_per_gpu": count, "image_bytes": L if L else "96/608/1492",
                    "bytes_per_gpu": img_bytes, "parallelism": f"shard{world} (independent per-GPU batches, no collective)"},
@@ -163,7 +173,7 @@ def main():
     if world == 1 and not args.no_cpu_baseline:
         rec["cpu_baseline"] = cpu_baseline(arena, res, kind, count, L, args.cpu_seconds,
                                            None if kind == "fixed" else (off, ln))
-    if world == 1 and not args.no_e2e and kind == "fixed":
+    if world == 1 and not args.no_e2e and kind == "fixed" and args.config not in STRONG:
         rec["e2e"] = e2e_rate(ctx, arena, res, count, L)
     print(json.dumps(rec), flush=True)
     if world > 1:
