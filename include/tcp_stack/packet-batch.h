@@ -30,6 +30,19 @@
 
 namespace tcp_stack {
 
+// Incremental update of a stored checksum when one aligned u32 field of the
+// image (raw, as stored: network order) changes, e.g. the ACK-number rewrite
+// of a retransmit (socket-internal.h:376-377), instead of the full recompute
+// that SendPacket then does (socket-manager.cc:9-10).  Exact in the
+// reference's mod-2^16 arithmetic: C' = ~(~C - old + new).
+inline uint16_t UpdateChecksum32(uint16_t checksum, uint32_t old_raw, uint32_t new_raw) {
+  uint16_t o[2], n[2];
+  std::memcpy(o, &old_raw, 4);
+  std::memcpy(n, &new_raw, 4);
+  checksum = tcpck_update16(checksum, o[0], n[0], TCPCK_MODE_REF);
+  return tcpck_update16(checksum, o[1], n[1], TCPCK_MODE_REF);
+}
+
 class PacketBatch {
  public:
   // Batches with fewer images or bytes than these stay on the CPU.

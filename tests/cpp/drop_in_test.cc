@@ -75,6 +75,17 @@ static int Layout() {
   std::printf("\n");
   h.Checksum() = CalculateChecksum(*pkt);
   std::printf("checksum %u\nreverify %u\n", h.Checksum(), CalculateChecksum(*pkt));
+  {
+    // retransmit ACK rewrite (socket-internal.h:376-377): incremental == full recompute
+    auto rp = MakeNetPacket(pkt->GetBuffer().first, pkt->GetBuffer().second);
+    TcpHeader &r = rp->GetHeader();
+    const uint32_t old_ack = r.AcknowledgementNumber();
+    r.AcknowledgementNumber() = htonl(0xdeadbeefu);
+    const uint16_t inc = UpdateChecksum32(r.Checksum(), old_ack, r.AcknowledgementNumber());
+    r.Checksum() = 0;
+    const uint16_t full = CalculateChecksum(*rp);
+    std::printf("update %u %u\n", inc, full);
+  }
   TcpHeaderN2H(h);
   std::printf("n2h %x %x %u %x\n", h.SourceAddress(), h.SequenceNumber(), h.Window(), h.TcpLength());
   // flag bits land in byte 25 exactly as the reference's bit positions 106..111

@@ -69,6 +69,8 @@ def test_layout_and_known_answer(exe, golden):
     assert img == bytes(golden.image(ref)), "header bytes differ from the reference's struct_hdr image"
     assert int(out["checksum"]) == 0x4BA4
     assert out["reverify"] == "0"
+    inc, full = out["update"].split()
+    assert inc == full
     assert out["n2h"] == "7f000001 11223344 1024 1234"
     assert [out[f] for f in ("urg", "ack", "psh", "rst", "syn", "fin", "cleared")] == \
         ["04", "08", "10", "20", "40", "80", "00"]
