@@ -33,6 +33,10 @@ extern "C" {
                                   4/8/2 loads with slot-graded s_setprio, 5: 4
                                   with s_setprio 1 for slots >= 4, 7: 3 + graded
                                   priority) | (blocks per CU cap << 8)          */
+#define TCPCK_KERNEL_RVSTREAM 6 /* packed variable layouts, MODE_REF: byte-balanced
+                                   run per wave, scalar walk over the lengths;
+                                   param = variant (0: 4 loads in flight, 1: 2,
+                                   2: 8) | (blocks per CU cap << 8)             */
 
 int tcpck_batch_fixed_ex(tcpck_ctx *ctx, int op, int mode, void *d_arena,
                          uint64_t stride, uint32_t len, uint64_t count, void *d_out,

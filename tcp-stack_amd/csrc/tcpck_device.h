@@ -142,6 +142,22 @@ __device__ __forceinline__ uint64_t read_lane64(uint64_t x, uint32_t lane) {
   return (static_cast<uint64_t>(hi) << 32) | lo;
 }
 
+// Sum (REF arithmetic, low 16 bits meaningful) of the first r/2 words of a
+// 16-byte chunk given as four dwords; r even in [0, 16).  Used by the scalar
+// boundary walks with wave-uniform inputs (readlane'd dwords): scalar code.
+__device__ __forceinline__ uint32_t words_before(uint32_t r, uint32_t x, uint32_t y, uint32_t z, uint32_t w) {
+  const uint32_t nw = r >> 1;
+  uint32_t h = 0;
+  if (nw >= 2) h += x + (x >> 16);
+  if (nw >= 4) h += y + (y >> 16);
+  if (nw >= 6) h += z + (z >> 16);
+  if (nw & 1) {
+    const uint32_t d = nw == 1 ? x : (nw == 3 ? y : (nw == 5 ? z : w));
+    h += d & 0xFFFFu;
+  }
+  return h;
+}
+
 // Sum (REF arithmetic, low 16 bits meaningful) of the image [start, start+len)
 // computed by one whole wave (64 lanes x U loads of 16 B in flight); the word at
 // byte `start + 28` is excluded when exclude_field (send-side fill).  Result is
@@ -182,6 +198,26 @@ __device__ __forceinline__ uint32_t wave_image_sum(const uint8_t *arena, uint64_
     if (MODE == kRfc1071) acc = fold_lane<MODE>(acc);
   }
   return group_sum<64>(fold_lane<MODE>(acc));
+}
+
+// First k in [0, count) with offsets[k] - base >= target (count if none);
+// offsets ascending.  64-ary search: one probe per lane per level.
+__device__ __forceinline__ uint64_t find_first_ge(const uint64_t *offsets, uint64_t base, uint64_t count, uint64_t target) {
+  const uint32_t lane = threadIdx.x & 63;
+  uint64_t lo = 0, hi = count;  // answer in [lo, hi]
+  while (hi - lo > 64) {
+    const uint64_t step = (hi - lo + 63) / 64;
+    const uint64_t idx = lo + lane * step;
+    const bool below = idx < hi && offsets[idx] - base < target;
+    const uint32_t c = __popcll(__ballot(below));  // probes are sorted: lanes [0, c) are below
+    const uint64_t nlo = c ? lo + (c - 1) * step + 1 : lo;
+    const uint64_t nhi = min(hi, lo + c * step);
+    lo = nlo;
+    hi = nhi;
+  }
+  const uint64_t idx = lo + lane;
+  const bool below = idx < hi && offsets[idx] - base < target;
+  return lo + __popcll(__ballot(below));
 }
 
 }  // namespace dev

@@ -21,8 +21,8 @@
 //     boundary walk is scalar: when it falls in this step, P(boundary) =
 //     carry + scan(lane) - sum(lane) + the lane's words before the byte,
 //     each read with v_readlane into SGPRs; the image that ends there gets
-//     ~(P - P_prev), written into lane (k mod 64) of a staging VGPR with
-//     v_writelane, and 64 results leave as one coalesced store;
+//     ~(P - P_prev), selected into lane (k mod 64) of a staging VGPR, and 64
+//     results leave as one coalesced store;
 //   * kFill zeroes each image's checksum word (bytes 28-29) in the stream, so
 //     the differences are the checksums of the zero-field images, and writes
 //     them into bytes 28-29 (tcp-header.h:177); kVerify stores checksum == 0.
@@ -35,21 +35,6 @@ namespace {
 using dev::kBlock;
 using dev::kWavesPerBlock;
 using dev::u32x4;
-
-// Sum (low 16 bits meaningful) of the first r/2 words of a 16-byte chunk given
-// as four dwords; r even in [0, 16).  Wave-uniform inputs: scalar code.
-__device__ __forceinline__ uint32_t words_before(uint32_t r, uint32_t x, uint32_t y, uint32_t z, uint32_t w) {
-  const uint32_t nw = r >> 1;
-  uint32_t h = 0;
-  if (nw >= 2) h += x + (x >> 16);
-  if (nw >= 4) h += y + (y >> 16);
-  if (nw >= 6) h += z + (z >> 16);
-  if (nw & 1) {
-    const uint32_t d = nw == 1 ? x : (nw == 3 ? y : (nw == 5 ? z : w));
-    h += d & 0xFFFFu;
-  }
-  return h;
-}
 
 // PRIO: 0 = default arbitration; 1 = s_setprio(wave slot / 2), 2 = s_setprio(1)
 // for slots >= 4 -- the SIMD issues by priority, then age, so younger waves
@@ -172,7 +157,7 @@ __global__ void __launch_bounds__(kBlock) rstream_kernel(FixedStreamArgs a) {
         const uint32_t r = rel & 15u;
         uint32_t P = carry + dev::read_lane(incl, lb) - dev::read_lane(tot, lb);
         if (r)
-          P += words_before(r, dev::read_lane(w.x, lb), dev::read_lane(w.y, lb), dev::read_lane(w.z, lb),
+          P += dev::words_before(r, dev::read_lane(w.x, lb), dev::read_lane(w.y, lb), dev::read_lane(w.z, lb),
                             dev::read_lane(w.w, lb));
         emit(jn - 1, P - p_last);
         p_last = P;

@@ -52,26 +52,6 @@ __device__ __forceinline__ u32x4 load16(const uint8_t *p) {
   }
 }
 
-// First k in [0, count) with offsets[k] - base >= target (count if none);
-// offsets ascending.  64-ary search: one probe per lane per level.
-__device__ uint64_t find_first_ge(const uint64_t *offsets, uint64_t base, uint64_t count, uint64_t target) {
-  const uint32_t lane = threadIdx.x & 63;
-  uint64_t lo = 0, hi = count;  // answer in [lo, hi]
-  while (hi - lo > 64) {
-    const uint64_t step = (hi - lo + 63) / 64;
-    const uint64_t idx = lo + lane * step;
-    const bool below = idx < hi && offsets[idx] - base < target;
-    const uint32_t c = __popcll(__ballot(below));  // probes are sorted: lanes [0, c) are below
-    const uint64_t nlo = c ? lo + (c - 1) * step + 1 : lo;
-    const uint64_t nhi = min(hi, lo + c * step);
-    lo = nlo;
-    hi = nhi;
-  }
-  const uint64_t idx = lo + lane;
-  const bool below = idx < hi && offsets[idx] - base < target;
-  return lo + __popcll(__ballot(below));
-}
-
 template <int OP>
 __device__ __forceinline__ void emit(const SpanArgs &a, uint64_t k, uint32_t sum, uint8_t *field_ptr) {
   const uint16_t c = static_cast<uint16_t>(~sum);  // tcp-header.h:262
@@ -111,9 +91,9 @@ __global__ void __launch_bounds__(kBlock) stream_kernel(SpanArgs a) {
   } else {
     const uint64_t first = a.offsets[0] - a.base;
     const uint64_t total = a.offsets[N - 1] - a.base + a.lengths[N - 1] - first;
-    kb = w == 0 ? 0 : find_first_ge(a.offsets, a.base, N, first + total / nw * w + (total % nw) * w / nw);
+    kb = w == 0 ? 0 : dev::find_first_ge(a.offsets, a.base, N, first + total / nw * w + (total % nw) * w / nw);
     ke = w + 1 == nw ? N
-                     : find_first_ge(a.offsets, a.base, N,
+                     : dev::find_first_ge(a.offsets, a.base, N,
                                      first + total / nw * (w + 1) + (total % nw) * (w + 1) / nw);
   }
   if (kb >= ke) return;  // no block-level synchronisation below: waves may leave early

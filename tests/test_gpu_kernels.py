@@ -308,3 +308,101 @@ def test_rstream_fill_verify(ctx, variant, length):
     ok = torch.empty(count, dtype=torch.uint8, device="cuda")
     ctx.batch_fixed_ex(tcpck.OP_VERIFY, dev(got), length, length, count, ok, tcpck.KERNEL_RSTREAM, variant)
     np.testing.assert_array_equal(np.nonzero(host(ok) == 0)[0], np.sort(bad))
+
+
+# ---- run-stream kernel for packed variable layouts (KERNEL_RVSTREAM = 6) ----
+RVSTREAM = [0, 1, 2]
+TINY = (0, 2, 4, 6, 8, 10, 12, 14)  # payloads below 16 B: several boundaries per chunk
+
+
+def packed_layout(count, seed, payloads, header=32):
+    rng = np.random.default_rng(seed)
+    ln = (np.asarray(payloads, np.int64)[rng.integers(0, len(payloads), count)] + header).astype(np.uint32)
+    off = np.zeros(count, np.uint64)
+    if count > 1:
+        off[1:] = np.cumsum(ln[:-1].astype(np.uint64))
+    return off, ln, int(ln.astype(np.int64).sum())
+
+
+@pytest.mark.parametrize("variant", RVSTREAM)
+def test_rvstream_golden_all_lengths(ctx, golden, variant):
+    """Every golden checksum image (0..65536 B, incl. < 16 B) packed back to back."""
+    import tcpck
+    cases = golden.by_kind("checksum")
+    imgs = [golden.image(c) for c in cases]
+    ln = np.array([c["len"] for c in cases], np.uint32)
+    off = np.zeros(len(cases), np.uint64)
+    off[1:] = np.cumsum(ln[:-1].astype(np.uint64))
+    exp = np.array([c["expected"] for c in cases], np.uint16)
+    out = torch.empty(len(exp), dtype=torch.int16, device="cuda")
+    ctx.batch_var_ex(tcpck.OP_CHECKSUM, dev(np.concatenate(imgs)), dev(off), dev(ln), len(exp), out,
+                     tcpck.KERNEL_RVSTREAM, variant, packed=True)
+    np.testing.assert_array_equal(host(out).view(np.uint16), exp)
+
+
+@pytest.mark.parametrize("variant", RVSTREAM)
+@pytest.mark.parametrize("payloads", [(64, 576, 1460), TINY + (64, 1460), (0,), (-32, -30, 0, 9000, 65504)])
+@pytest.mark.parametrize("count", [1, 2, 63, 64, 65, 1000, 70001])
+def test_rvstream_var_vs_oracle(ctx, oracle_c, variant, payloads, count):
+    import tcpck
+    off, ln, total = packed_layout(count, count * 7 + len(payloads), payloads)
+    if total > (96 << 20):
+        return
+    rng = np.random.default_rng(count + variant)
+    arena_np = rng.integers(0, 256, total + 128, dtype=np.uint8)
+    buf = dev(arena_np)
+    d_off, d_ln = dev(off), dev(ln)
+    for mis in (0, 2, 14, 126):
+        out = torch.empty(count, dtype=torch.int16, device="cuda")
+        ctx.batch_var_ex(tcpck.OP_CHECKSUM, buf.data_ptr() + mis, d_off, d_ln, count, out,
+                         tcpck.KERNEL_RVSTREAM, variant, packed=True)
+        exp = oracle_c.batch(arena_np[mis:], off, ln, threads=8)
+        np.testing.assert_array_equal(host(out).view(np.uint16), exp)
+
+
+@pytest.mark.parametrize("variant", RVSTREAM)
+def test_rvstream_not_packed_falls_back(ctx, oracle_c, variant):
+    """Gaps and a non-zero first offset: waves whose length walk disagrees
+    with the offsets recompute per image -- results stay exact."""
+    import tcpck
+    import synth_np
+    rng = np.random.default_rng(variant)
+    count = 30000
+    off, ln, _ = synth_np.mixed_layout(count, seed=3)
+    off = off.copy()
+    for k in rng.integers(1, count, 25):
+        off[k:] += 10
+    off += np.uint64(4096)
+    total = int(off[-1] + ln[-1]) + 64
+    arena_np = rng.integers(0, 256, total, dtype=np.uint8)
+    out = torch.empty(count, dtype=torch.int16, device="cuda")
+    ctx.batch_var_ex(tcpck.OP_CHECKSUM, dev(arena_np), dev(off), dev(ln), count, out,
+                     tcpck.KERNEL_RVSTREAM, variant, packed=True)
+    np.testing.assert_array_equal(host(out).view(np.uint16), oracle_c.batch(arena_np, off, ln, threads=8))
+
+
+@pytest.mark.parametrize("variant", RVSTREAM)
+@pytest.mark.parametrize("payloads", [(64, 576, 1460), (0, 2, 30, 1460), (65504,)])
+def test_rvstream_fill_verify(ctx, variant, payloads):
+    import tcpck
+    from oracle import ref16 as R
+    count = 6000 if max(payloads) < 10000 else 300
+    off, ln, total = packed_layout(count, 11 + variant, payloads)
+    rng = np.random.default_rng(variant + len(payloads))
+    arena_np = rng.integers(0, 256, total, dtype=np.uint8)
+    arena = dev(arena_np)
+    out = torch.empty(count, dtype=torch.int16, device="cuda")
+    ctx.batch_var_ex(tcpck.OP_FILL, arena, dev(off), dev(ln), count, out, tcpck.KERNEL_RVSTREAM, variant,
+                     packed=True)
+    exp_arena = arena_np.copy()
+    exp = np.array([R.fill_np(exp_arena[int(off[k]):int(off[k]) + int(ln[k])]) for k in range(count)], np.uint16)
+    np.testing.assert_array_equal(host(out).view(np.uint16), exp)
+    got = host(arena)
+    np.testing.assert_array_equal(got, exp_arena)
+    bad = rng.choice(count, 40, replace=False)
+    for k in bad:
+        got[int(off[k]) + int(rng.integers(0, int(ln[k])))] ^= 0x42
+    ok = torch.empty(count, dtype=torch.uint8, device="cuda")
+    ctx.batch_var_ex(tcpck.OP_VERIFY, dev(got), dev(off), dev(ln), count, ok, tcpck.KERNEL_RVSTREAM, variant,
+                     packed=True)
+    np.testing.assert_array_equal(np.nonzero(host(ok) == 0)[0], np.sort(bad))
