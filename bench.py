@@ -65,15 +65,50 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    p.add_argument("--config", default="c2", choices=sorted(CONFIGS) + ["c1"])
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline time budget")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-e2e", action="store_true")
     return p.parse_args()
 
 
+def bench_c1(args):
+    """C1: one 1460-B segment at a time over UDP loopback, CPU only (plumbing).
+
+    tcp-stack_amd/bin/loopback_c1 is the same program compiled against the
+    drop-in header (this library) and, as oracle/_ref/loopback_c1_ref, against
+    the reference's own tcp-header.h; both run here on the host."""
+    import subprocess
+    n = max(1000, args.steps * 1000)
+
+    def run(exe):
+        r = subprocess.run([exe, str(n), "1460"], capture_output=True, text=True, timeout=300)
+        if r.returncode != 0:
+            raise SystemExit(f"{exe} failed rc={r.returncode}: {r.stderr}")
+        return json.loads(r.stdout.strip().splitlines()[-1])
+
+    ours = run(os.path.join(ROOT, "tcp-stack_amd", "bin", "loopback_c1"))
+    rec = {"metric": "C1 loopback send+fill+recv+verify latency per 1492-B segment (CPU, no GPU)",
+           "value": round(ours["us_per_segment"], 3), "unit": "us/segment", "n_gpus": 0, "steps": n,
+           "warmup": 0, "ms_per_step": round(ours["us_per_segment"] / 1e3, 6), "higher_is_better": False,
+           "scaling": "weak", "vs_baseline": None, "dtype": "u16", "data": "synthetic (fixed payload pattern)",
+           "config": {"workload": "C1: single 1460-B segments over UDP 127.0.0.1, drop-in tcp_stack/tcp-header.h",
+                      "segments": n, "verified": ours["verified"], "send_checksum_ns": ours["send_checksum_ns"],
+                      "recv_checksum_ns": ours["recv_checksum_ns"]}}
+    ref = os.path.join(ROOT, "oracle", "_ref", "loopback_c1_ref")
+    if os.path.exists(ref):
+        r = run(ref)
+        rec["cpu_baseline"] = {"value": round(r["us_per_segment"], 3), "unit": "us/segment", "cores": 1,
+                               "kind": "reference", "sample": f"{n} segments, same program built on the "
+                               "reference's include/tcp-header.h (-O2)",
+                               "send_checksum_ns": r["send_checksum_ns"], "recv_checksum_ns": r["recv_checksum_ns"]}
+    print(json.dumps(rec), flush=True)
+
+
 def main():
     args = parse()
+    if args.config == "c1":
+        return bench_c1(args)
     import torch
     import torch.distributed as dist
     import tcpck

@@ -90,3 +90,16 @@ def test_packet_batch_gpu(built_lib):
     lines = run(exe, "batch", 20000, 7)
     assert lines[-1].endswith("mismatches=0"), lines
     assert "gpu_images=0" not in lines[-1]
+
+
+def test_loopback_c1(built_lib):
+    """Config C1: segments over UDP loopback, filled and verified through the drop-in."""
+    import json
+    exe = os.path.join(LIBDIR, "bin", "loopback_c1")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-s", "-C", LIBDIR], check=True)
+    r = subprocess.run([exe, "3000", "1460"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    d = json.loads(r.stdout)
+    assert d["received"] == d["verified"] == 3000
+    assert d["image_bytes"] == 1492
