@@ -32,7 +32,9 @@ extern "C" {
                                   per-wave time stamps, checksum only; 4/6/8:
                                   4/8/2 loads with slot-graded s_setprio, 5: 4
                                   with s_setprio 1 for slots >= 4, 7: 3 + graded
-                                  priority) | (blocks per CU cap << 8)          */
+                                  priority, 9: 4 with v_dot2 sums, 10/12/13:
+                                  4/2/8 with v_dot2 sums and buffer loads, 11:
+                                  4 with buffer loads) | (blocks per CU cap << 8) */
 #define TCPCK_KERNEL_RVSTREAM 6 /* packed variable layouts, MODE_REF: byte-balanced
                                    run per wave, scalar walk over the lengths;
                                    param = variant (0: 4 loads in flight, 1: 2,

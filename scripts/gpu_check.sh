@@ -22,7 +22,8 @@ for s in ${STEPS:-tests smoke bench prof}; do
     bench_c3) step bench_c3 600 python bench.py --config c3 --no-cpu-baseline ;;
     sweep) step sweep 900 python scripts/sweep.py ;;
     sweep_c3) step sweep_c3 600 python scripts/sweep.py --configs c3 ;;
-    rv) step rv 900 python -m pytest tests/test_gpu_kernels.py -x -q -k rvstream ;;
+    rv) step rv 900 python -m pytest tests/test_gpu_kernels.py -x -q -k "rvstream or rstream" ;;
+    sweep_c2) step sweep_c2 600 python scripts/sweep.py --configs c2 ;;
     bench_c4) step bench_c4 600 python bench.py --config c4 --no-cpu-baseline ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-e2e ;;
     pmc_c2|pmc_c3|pmc_c4)  # separate FETCH_SIZE / WRITE_SIZE passes (TCC slots), kernel trace only

@@ -53,7 +53,7 @@ def variants(w):
     if not (w["fixed"] and w["L"] > 16384):
         v += [(f"stream {n}", tcpck.KERNEL_STREAM, p) for p, n in tcpck.STREAM_VARIANTS.items()]
     if w["fixed"] and w["L"] <= 16384:
-        v += [(f"rstream v{p}", tcpck.KERNEL_RSTREAM, p) for p in (0, 1, 2)]
+        v += [(f"rstream v{p}", tcpck.KERNEL_RSTREAM, p) for p in (0, 1, 2, 9, 10, 11, 12, 13)]
     if not w["fixed"]:
         v += [(f"rvstream v{p}", tcpck.KERNEL_RVSTREAM, p) for p in (0, 1, 2)]
     return v

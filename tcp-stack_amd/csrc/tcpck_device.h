@@ -75,6 +75,28 @@ __device__ __forceinline__ uint32_t ref_chunk_sum(u32x4 w) {
   return ref_add(ref_add(ref_add(w.x + (w.x >> 16), w.y), w.z), w.w);
 }
 
+// Same sum with v_dot2_u32_u16 (both u16 halves times 1, plus the
+// accumulator): 4 VALU per chunk instead of 8.
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t ref_chunk_sum_dot(u32x4 w) {
+  const u16x2 one = {1, 1};
+  uint32_t a = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, w.x), one, 0u, false);
+  a = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, w.y), one, a, false);
+  a = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, w.z), one, a, false);
+  return __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, w.w), one, a, false);
+}
+
+// Raw buffer (SRSRC) loads: 32-bit lane offset + SGPR step offset, hardware
+// range check (bytes past `bytes` read as 0, no fault), nontemporal (aux 2).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), 0, static_cast<int>(bytes), 0x00020000);
+}
+__device__ __forceinline__ u32x4 load16_buf_nt(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  typedef unsigned v4u __attribute__((ext_vector_type(4)));
+  const v4u v = __builtin_amdgcn_raw_buffer_load_b128(r, static_cast<int>(voff), static_cast<int>(soff), 2);
+  return u32x4{v.x, v.y, v.z, v.w};
+}
+
 // RFC 1071: 32-bit one's-complement add (2^32 == 1 mod 0xFFFF).
 __device__ __forceinline__ uint32_t rfc_add(uint32_t acc, uint32_t w) {
   const uint32_t s = acc + w;

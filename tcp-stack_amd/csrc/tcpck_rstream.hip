@@ -40,7 +40,9 @@ using dev::u32x4;
 // for slots >= 4 -- the SIMD issues by priority, then age, so younger waves
 // (higher slots) otherwise starve: identical runs took 105 us in slot 0 and
 // 224 us in slot 7 of a C2 launch (scripts/stamps.py).
-template <int U, int OP, bool STAMP, int PRIO = 0>
+// FLAV bit 0: chunk sums with v_dot2_u32_u16; bit 1: buffer (SRSRC) loads with
+// the step offset in an SGPR instead of per-lane 64-bit clamped addresses.
+template <int U, int OP, bool STAMP, int PRIO = 0, int FLAV = 0>
 __global__ void __launch_bounds__(kBlock) rstream_kernel(FixedStreamArgs a) {
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t W = static_cast<uint64_t>(gridDim.x) * kWavesPerBlock;
@@ -80,9 +82,15 @@ __global__ void __launch_bounds__(kBlock) rstream_kernel(FixedStreamArgs a) {
   const uint32_t last_chunk = (span - 1) >> 4;
   const uint8_t *base = a.arena + A0;
 
+  // buffer flavour: records cover whole chunks of the run; steps past it read 0
+  const auto rsrc = dev::make_rsrc(base, (last_chunk + 1) << 4);
   auto load_step = [&](uint32_t st) -> u32x4 {
-    const uint32_t ci = min((st << 6) + lane, last_chunk);  // clamp: always a legal address
-    return dev::load16_nt(base + 16 * static_cast<uint64_t>(ci));
+    if constexpr (FLAV & 2) {
+      return dev::load16_buf_nt(rsrc, lane << 4, st << 10);
+    } else {
+      const uint32_t ci = min((st << 6) + lane, last_chunk);  // clamp: always a legal address
+      return dev::load16_nt(base + 16 * static_cast<uint64_t>(ci));
+    }
   };
 
   // wave-uniform boundary walk, all in 32-bit run-relative terms (SGPRs):
@@ -149,7 +157,7 @@ __global__ void __launch_bounds__(kBlock) rstream_kernel(FixedStreamArgs a) {
           nf += S;
         }
       }
-      const uint32_t tot = dev::ref_chunk_sum(w);
+      const uint32_t tot = (FLAV & 1) ? dev::ref_chunk_sum_dot(w) : dev::ref_chunk_sum(w);
       const uint32_t incl = dev::wave_inclusive_scan(tot);
       while (nb < sb + 1024 && jn < nimg) {  // scalar: boundaries in this step
         const uint32_t rel = nb - sb;
@@ -182,25 +190,25 @@ __global__ void __launch_bounds__(kBlock) rstream_kernel(FixedStreamArgs a) {
   }
 }
 
-template <int U, int OP, bool STAMP, int PRIO = 0>
+template <int U, int OP, bool STAMP, int PRIO = 0, int FLAV = 0>
 hipError_t launch_one(const FixedStreamArgs &a, uint32_t num_cus, hipStream_t stream) {
-  static const uint32_t per_cu = dev::resident_blocks_per_cu(rstream_kernel<U, OP, STAMP, PRIO>);
+  static const uint32_t per_cu = dev::resident_blocks_per_cu(rstream_kernel<U, OP, STAMP, PRIO, FLAV>);
   const uint32_t cap = (a.blocks_per_cu && a.blocks_per_cu < per_cu) ? a.blocks_per_cu : per_cu;
   uint64_t blocks = static_cast<uint64_t>(cap) * num_cus;
   const uint64_t need = (a.count + kWavesPerBlock - 1) / kWavesPerBlock;  // >= 1 image per wave
   if (blocks > need) blocks = need;
   if (blocks == 0) return hipSuccess;
-  hipLaunchKernelGGL((rstream_kernel<U, OP, STAMP, PRIO>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0,
+  hipLaunchKernelGGL((rstream_kernel<U, OP, STAMP, PRIO, FLAV>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0,
                      stream, a);
   return hipGetLastError();
 }
 
-template <int U, bool STAMP, int PRIO = 0>
+template <int U, bool STAMP, int PRIO = 0, int FLAV = 0>
 hipError_t dispatch(int op, const FixedStreamArgs &a, uint32_t num_cus, hipStream_t s) {
   switch (op) {
-    case kChecksum: return launch_one<U, kChecksum, STAMP, PRIO>(a, num_cus, s);
-    case kFill: return launch_one<U, kFill, STAMP, PRIO>(a, num_cus, s);
-    case kVerify: return launch_one<U, kVerify, STAMP, PRIO>(a, num_cus, s);
+    case kChecksum: return launch_one<U, kChecksum, STAMP, PRIO, FLAV>(a, num_cus, s);
+    case kFill: return launch_one<U, kFill, STAMP, PRIO, FLAV>(a, num_cus, s);
+    case kVerify: return launch_one<U, kVerify, STAMP, PRIO, FLAV>(a, num_cus, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -222,6 +230,11 @@ hipError_t launch_rstream(int op, int variant, const FixedStreamArgs &a, uint32_
     case 6: return dispatch<8, false, 1>(op, a, num_cus, stream);
     case 7: return op == kChecksum ? launch_one<4, kChecksum, true, 1>(a, num_cus, stream) : hipErrorInvalidValue;
     case 8: return dispatch<2, false, 1>(op, a, num_cus, stream);
+    case 9: return dispatch<4, false, 0, 1>(op, a, num_cus, stream);
+    case 10: return dispatch<4, false, 0, 3>(op, a, num_cus, stream);
+    case 11: return dispatch<4, false, 0, 2>(op, a, num_cus, stream);
+    case 12: return dispatch<2, false, 0, 3>(op, a, num_cus, stream);
+    case 13: return dispatch<8, false, 0, 3>(op, a, num_cus, stream);
     default: return hipErrorInvalidValue;
   }
 }

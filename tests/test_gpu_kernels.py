@@ -264,7 +264,7 @@ def test_fstream_rejects(ctx):
 
 
 # ---- run-stream kernel (KERNEL_RSTREAM = 5: fixed stride == len, scalar boundary walk) ----
-RSTREAM = [0, 1, 2]
+RSTREAM = [0, 1, 2, 9, 10, 11, 12, 13]  # 9-13: v_dot2 sums and/or buffer loads
 
 
 @pytest.mark.parametrize("variant", RSTREAM)
