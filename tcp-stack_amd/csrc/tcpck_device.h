@@ -77,13 +77,15 @@ __device__ __forceinline__ uint32_t ref_chunk_sum(u32x4 w) {
 
 // Same sum with v_dot2_u32_u16 (both u16 halves times 1, plus the
 // accumulator): 4 VALU per chunk instead of 8.
-typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+// (inline asm: hipcc 7.2 miscompiles the builtin on halves of a <4 x i32>
+// load -- every dot read the first dword)
+__device__ __forceinline__ uint32_t dot2_u16(uint32_t w, uint32_t acc) {
+  uint32_t r;
+  asm("v_dot2_u32_u16 %0, %1, %2, %3" : "=v"(r) : "v"(w), "s"(0x00010001u), "v"(acc));
+  return r;
+}
 __device__ __forceinline__ uint32_t ref_chunk_sum_dot(u32x4 w) {
-  const u16x2 one = {1, 1};
-  uint32_t a = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, w.x), one, 0u, false);
-  a = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, w.y), one, a, false);
-  a = __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, w.z), one, a, false);
-  return __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, w.w), one, a, false);
+  return dot2_u16(w.w, dot2_u16(w.z, dot2_u16(w.y, dot2_u16(w.x, 0u))));
 }
 
 // Raw buffer (SRSRC) loads: 32-bit lane offset + SGPR step offset, hardware

@@ -78,7 +78,9 @@ __device__ __forceinline__ void find_two(const uint64_t *offsets, uint64_t base,
   r1 = lo[1] + __popcll(__ballot(b1));
 }
 
-template <int U, int OP>
+// SPLIT 0: byte-balanced runs (two 64-ary searches over the offsets);
+// SPLIT 1: equal image counts (no search; balance only statistical) -- tuning.
+template <int U, int OP, int SPLIT = 0>
 __global__ void __launch_bounds__(kBlock)
     rvstream_kernel(uint8_t *__restrict__ arena, const uint64_t *__restrict__ offsets,
                     const uint32_t *__restrict__ lengths, uint64_t base, uint64_t count, void *__restrict__ out) {
@@ -94,7 +96,12 @@ __global__ void __launch_bounds__(kBlock)
   const uint64_t t0 = first + q * wid + rm * wid / W;
   const uint64_t t1 = first + q * (wid + 1) + rm * (wid + 1) / W;
   uint64_t kb, ke;
-  find_two(offsets, base, N, t0, t1, kb, ke);
+  if (SPLIT == 1) {
+    kb = wid * N / W;
+    ke = (wid + 1) * N / W;
+  } else {
+    find_two(offsets, base, N, t0, t1, kb, ke);
+  }
   if (wid == 0) kb = 0;
   if (wid + 1 == W) ke = N;
   if (kb >= ke) return;
@@ -240,25 +247,25 @@ __global__ void __launch_bounds__(kBlock)
   }
 }
 
-template <int U, int OP>
+template <int U, int OP, int SPLIT>
 hipError_t launch_one(const SpanArgs &a, uint32_t num_cus, uint32_t blocks_per_cu, hipStream_t stream) {
-  static const uint32_t per_cu = dev::resident_blocks_per_cu(rvstream_kernel<U, OP>);
+  static const uint32_t per_cu = dev::resident_blocks_per_cu(rvstream_kernel<U, OP, SPLIT>);
   const uint32_t cap = (blocks_per_cu && blocks_per_cu < per_cu) ? blocks_per_cu : per_cu;
   uint64_t blocks = static_cast<uint64_t>(cap) * num_cus;
   const uint64_t need = (a.count + kWavesPerBlock - 1) / kWavesPerBlock;
   if (blocks > need) blocks = need;
   if (blocks == 0) return hipSuccess;
-  hipLaunchKernelGGL((rvstream_kernel<U, OP>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0, stream, a.arena,
+  hipLaunchKernelGGL((rvstream_kernel<U, OP, SPLIT>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0, stream, a.arena,
                      a.offsets, a.lengths, a.base, a.count, a.out);
   return hipGetLastError();
 }
 
-template <int U>
+template <int U, int SPLIT = 0>
 hipError_t dispatch(int op, const SpanArgs &a, uint32_t num_cus, uint32_t cap, hipStream_t s) {
   switch (op) {
-    case kChecksum: return launch_one<U, kChecksum>(a, num_cus, cap, s);
-    case kFill: return launch_one<U, kFill>(a, num_cus, cap, s);
-    case kVerify: return launch_one<U, kVerify>(a, num_cus, cap, s);
+    case kChecksum: return launch_one<U, kChecksum, SPLIT>(a, num_cus, cap, s);
+    case kFill: return launch_one<U, kFill, SPLIT>(a, num_cus, cap, s);
+    case kVerify: return launch_one<U, kVerify, SPLIT>(a, num_cus, cap, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -272,6 +279,7 @@ hipError_t launch_rvstream(int op, int variant, const SpanArgs &a, uint32_t num_
     case 0: return dispatch<4>(op, a, num_cus, cap, stream);
     case 1: return dispatch<2>(op, a, num_cus, cap, stream);
     case 2: return dispatch<8>(op, a, num_cus, cap, stream);
+    case 3: return dispatch<4, 1>(op, a, num_cus, cap, stream);
     default: return hipErrorInvalidValue;
   }
 }
