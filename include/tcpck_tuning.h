@@ -35,6 +35,10 @@ extern "C" {
                                   priority, 9: 4 with v_dot2 sums, 10/12/13:
                                   4/2/8 with v_dot2 sums and buffer loads, 11:
                                   4 with buffer loads) | (blocks per CU cap << 8) */
+#define TCPCK_KERNEL_VSTREAM 7 /* fixed stride == len >= 16, MODE_REF: run per
+                                  wave, all boundaries of a step resolved by the
+                                  lanes in parallel (small images); param =
+                                  variant (0: 4 loads in flight, 1: 2, 2: 8)    */
 #define TCPCK_KERNEL_RVSTREAM 6 /* packed variable layouts, MODE_REF: byte-balanced
                                    run per wave, scalar walk over the lengths;
                                    param = variant (0: 4 loads in flight, 1: 2,

@@ -26,6 +26,8 @@ for s in ${STEPS:-tests smoke bench prof}; do
     sweep_c2) step sweep_c2 600 python scripts/sweep.py --configs c2 ;;
     rvprobe) step rvprobe 600 python scripts/rv_probe.py ;;
     policy) step policy 900 python scripts/policy_sweep.py ;;
+    policy_fixed) step policy_fixed 900 python scripts/policy_sweep.py --no-mixes ;;
+    vs) step vs 900 python -m pytest tests/test_gpu_kernels.py -x -q -k vstream ;;
     bench_c4) step bench_c4 600 python bench.py --config c4 --no-cpu-baseline ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-e2e ;;
     pmc_c2|pmc_c3|pmc_c4)  # separate FETCH_SIZE / WRITE_SIZE passes (TCC slots), kernel trace only

@@ -42,6 +42,7 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("--bytes", type=int, default=1564475392)
     p.add_argument("--reps", type=int, default=6)
+    p.add_argument("--no-mixes", action="store_true")
     args = p.parse_args()
     ctx = tcpck.Context(0)
     s = torch.cuda.current_stream()
@@ -61,6 +62,11 @@ def main():
                 ("stream", lambda: ctx.batch_fixed_ex(K.OP_CHECKSUM, a, L, L, n, out, K.KERNEL_STREAM, 0, stream=s)),
                 ("fstream", lambda: ctx.batch_fixed_ex(K.OP_CHECKSUM, a, L, L, n, out, K.KERNEL_FSTREAM, 0, stream=s)),
                 ("rstream", lambda: ctx.batch_fixed_ex(K.OP_CHECKSUM, a, L, L, n, out, K.KERNEL_RSTREAM, 0, stream=s)),
+                ("vstream", lambda: ctx.batch_fixed_ex(K.OP_CHECKSUM, a, L, L, n, out, K.KERNEL_VSTREAM, 0, stream=s)),
+                ("vstream U2", lambda: ctx.batch_fixed_ex(K.OP_CHECKSUM, a, L, L, n, out, K.KERNEL_VSTREAM, 1,
+                                                          stream=s)),
+                ("vstream U8", lambda: ctx.batch_fixed_ex(K.OP_CHECKSUM, a, L, L, n, out, K.KERNEL_VSTREAM, 2,
+                                                          stream=s)),
                 ("rstream U2", lambda: ctx.batch_fixed_ex(K.OP_CHECKSUM, a, L, L, n, out, K.KERNEL_RSTREAM, 1,
                                                           stream=s)),
                 ("var rvstream", lambda: ctx.batch_var_ex(K.OP_CHECKSUM, a, off, ln, n, out, K.KERNEL_RVSTREAM, 0,
@@ -86,7 +92,7 @@ def main():
             print(f"fixed L={L:5d} {label:14s} {ms:8.4f} ms {gbs:7.1f} GB/s ({gbs / 80:5.1f}%)", flush=True)
         del a, ref, out, off, ln
         torch.cuda.empty_cache()
-    for name, payloads in MIXES.items():
+    for name, payloads in ({} if args.no_mixes else MIXES).items():
         rng = np.random.default_rng(1)
         mean = np.mean(payloads) + 32
         n = int(args.bytes / mean)

@@ -160,10 +160,22 @@ constexpr uint64_t kSpanMaxLen = 16384;
 hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t stride, uint32_t len,
                      uint64_t count, void *out, int kernel, int param, hipStream_t s) {
   const bool span_ok = mode == TCPCK_MODE_REF && stride == len && len >= 16 && len <= (1u << 24);
-  // packed fixed stride, reference mode: the run-stream kernel (82.6% of the
-  // HBM roof on C2, scripts/prio.py); jumbo images stay on seg (G64/U4), which
-  // streams whole 16-B-aligned images per wave at the same rate
-  if (kernel == TCPCK_KERNEL_AUTO) kernel = (span_ok && len <= kSpanMaxLen) ? TCPCK_KERNEL_RSTREAM : TCPCK_KERNEL_SEG;
+  // packed fixed stride, reference mode, by image length (scripts/policy_sweep.py,
+  // profiles/r01/policy_sweep.log): below 64 B boundaries are so dense that the
+  // per-lane arithmetic boundaries of fstream win; up to 768 B the span tiles;
+  // from 768 B the run-stream kernel's scalar boundary walk (82.6% of the HBM
+  // roof on C2); jumbo images stay on seg (G64/U4), which streams whole images
+  // per wave at the same rate
+  if (kernel == TCPCK_KERNEL_AUTO) {
+    if (!span_ok || len > kSpanMaxLen)
+      kernel = TCPCK_KERNEL_SEG;
+    else if (len < 64)
+      kernel = TCPCK_KERNEL_FSTREAM;
+    else if (len < 768)
+      kernel = TCPCK_KERNEL_SPAN;
+    else
+      kernel = TCPCK_KERNEL_RSTREAM;
+  }
   if (kernel == TCPCK_KERNEL_SPAN) {
     if (!span_ok) return hipErrorInvalidValue;
     tcpck::SpanArgs a{};
@@ -205,6 +217,15 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
     a.dbg = static_cast<uint64_t *>(ctx->dbg);
     a.blocks_per_cu = static_cast<uint32_t>(param >> 8) & 0xFFu;
     return tcpck::launch_rstream(op, param & 0xFF, a, static_cast<uint32_t>(ctx->num_cus), s);
+  }
+  if (kernel == TCPCK_KERNEL_VSTREAM) {
+    if (!span_ok) return hipErrorInvalidValue;
+    tcpck::FixedStreamArgs a{};
+    a.arena = arena;
+    a.stride = stride;
+    a.count = count;
+    a.out = out;
+    return tcpck::launch_vstream(op, param & 0xFF, a, static_cast<uint32_t>(ctx->num_cus), s);
   }
   if (kernel != TCPCK_KERNEL_SEG) return hipErrorInvalidValue;
   SegArgs a{};

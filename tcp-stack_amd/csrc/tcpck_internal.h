@@ -73,6 +73,9 @@ struct FixedStreamArgs {
 // ---- run-stream kernel (fixed stride == len): one run per wave, scalar boundaries
 // variant: 0 = 4 loads in flight, 1 = 2, 2 = 8, 3 = 4 with per-wave time stamps
 hipError_t launch_rstream(int op, int variant, const FixedStreamArgs &a, uint32_t num_cus, hipStream_t stream);
+// ---- vector-boundary run stream (fixed stride == len, small images), MODE_REF:
+// variant = loads in flight (0: 4, 1: 2, 2: 8)
+hipError_t launch_vstream(int op, int variant, const FixedStreamArgs &a, uint32_t num_cus, hipStream_t stream);
 // ---- run-stream kernel for packed variable layouts (tcpck_rvstream.hip), MODE_REF:
 // variant = loads in flight (0: 4, 1: 2, 2: 8) | blocks-per-CU cap << 8
 hipError_t launch_rvstream(int op, int variant, const SpanArgs &a, uint32_t num_cus, hipStream_t stream);

@@ -406,3 +406,50 @@ def test_rvstream_fill_verify(ctx, variant, payloads):
     ctx.batch_var_ex(tcpck.OP_VERIFY, dev(got), dev(off), dev(ln), count, ok, tcpck.KERNEL_RVSTREAM, variant,
                      packed=True)
     np.testing.assert_array_equal(np.nonzero(host(ok) == 0)[0], np.sort(bad))
+
+
+# ---- vector-boundary run stream (KERNEL_VSTREAM = 7: fixed stride == len, small images) ----
+VSTREAM = [0, 1, 2]
+
+
+@pytest.mark.parametrize("variant", VSTREAM)
+@pytest.mark.parametrize("length", [16, 18, 30, 32, 34, 64, 96, 126, 128, 606, 1024, 1026, 1492, 4096])
+@pytest.mark.parametrize("count", [1, 2, 7, 64, 65, 3001, 70001])
+def test_vstream_fixed_vs_oracle(ctx, oracle_c, variant, length, count):
+    import tcpck
+    if count * length > (64 << 20):
+        count = (64 << 20) // length
+    rng = np.random.default_rng(length * 11 + count + variant)
+    arena_np = rng.integers(0, 256, count * length + 128, dtype=np.uint8)
+    arena_np[:length] = 0xFF
+    buf = dev(arena_np)
+    for mis in (0, 2, 14, 126):
+        out = torch.empty(count, dtype=torch.int16, device="cuda")
+        ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, buf.data_ptr() + mis, length, length, count, out,
+                           tcpck.KERNEL_VSTREAM, variant)
+        exp = oracle_c.batch(arena_np[mis:], stride=length, length=length, count=count, threads=8)
+        np.testing.assert_array_equal(host(out).view(np.uint16), exp)
+
+
+@pytest.mark.parametrize("variant", VSTREAM)
+@pytest.mark.parametrize("length", [30, 32, 34, 96, 1024, 1492])
+def test_vstream_fill_verify(ctx, variant, length):
+    import tcpck
+    from oracle import ref16 as R
+    rng = np.random.default_rng(length + 20 * variant)
+    count = 9000
+    arena_np = rng.integers(0, 256, count * length, dtype=np.uint8)
+    arena = dev(arena_np)
+    out = torch.empty(count, dtype=torch.int16, device="cuda")
+    ctx.batch_fixed_ex(tcpck.OP_FILL, arena, length, length, count, out, tcpck.KERNEL_VSTREAM, variant)
+    exp_arena = arena_np.copy()
+    exp = np.array([R.fill_np(exp_arena[k * length:(k + 1) * length]) for k in range(count)], np.uint16)
+    np.testing.assert_array_equal(host(out).view(np.uint16), exp)
+    got = host(arena)
+    np.testing.assert_array_equal(got, exp_arena)
+    bad = rng.choice(count, 64, replace=False)
+    for k in bad:
+        got[k * length + int(rng.integers(0, length))] ^= 0x18
+    ok = torch.empty(count, dtype=torch.uint8, device="cuda")
+    ctx.batch_fixed_ex(tcpck.OP_VERIFY, dev(got), length, length, count, ok, tcpck.KERNEL_VSTREAM, variant)
+    np.testing.assert_array_equal(np.nonzero(host(ok) == 0)[0], np.sort(bad))
