@@ -161,20 +161,20 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
                      uint64_t count, void *out, int kernel, int param, hipStream_t s) {
   const bool span_ok = mode == TCPCK_MODE_REF && stride == len && len >= 16 && len <= (1u << 24);
   // packed fixed stride, reference mode, by image length (scripts/policy_sweep.py,
-  // profiles/r01/policy_sweep.log): below 64 B boundaries are so dense that the
-  // per-lane arithmetic boundaries of fstream win; up to 768 B the span tiles;
-  // from 768 B the run-stream kernel's scalar boundary walk (82.6% of the HBM
-  // roof on C2); jumbo images stay on seg (G64/U4), which streams whole images
-  // per wave at the same rate
+  // profiles/r01/policy_fixed.log): below 768 B boundaries are dense enough that
+  // resolving all of a step's boundaries in parallel (vstream, 8 loads in
+  // flight) wins; from 768 B the run-stream kernel's scalar boundary walk
+  // (82.6% of the HBM roof on C2); jumbo images stay on seg (G64/U4), which
+  // streams whole images per wave at the same rate
   if (kernel == TCPCK_KERNEL_AUTO) {
-    if (!span_ok || len > kSpanMaxLen)
+    if (!span_ok || len > kSpanMaxLen) {
       kernel = TCPCK_KERNEL_SEG;
-    else if (len < 64)
-      kernel = TCPCK_KERNEL_FSTREAM;
-    else if (len < 768)
-      kernel = TCPCK_KERNEL_SPAN;
-    else
+    } else if (len < 768) {
+      kernel = TCPCK_KERNEL_VSTREAM;
+      param = 2;
+    } else {
       kernel = TCPCK_KERNEL_RSTREAM;
+    }
   }
   if (kernel == TCPCK_KERNEL_SPAN) {
     if (!span_ok) return hipErrorInvalidValue;
