@@ -13,7 +13,8 @@ import torch  # noqa: E402
 import tcpck  # noqa: E402
 
 NAMES = {0: "1x16B U4 scan", 1: "1x16B U4 noscan", 2: "2x16B U2 scan", 3: "2x16B U2 noscan",
-         4: "4x16B U1 scan", 5: "2x16B U4 scan", 6: "4x16B U2 scan", 7: "1x16B U2 scan"}
+         4: "4x16B U1 scan", 5: "2x16B U4 scan", 6: "4x16B U2 scan", 7: "1x16B U2 scan",
+         8: "dyn U4 16K units", 9: "dyn U4 32K units", 10: "dyn U4 8K units", 11: "dyn U8 32K units"}
 
 
 def main():
@@ -21,7 +22,7 @@ def main():
     stream = torch.cuda.current_stream()
     buf = torch.empty(17 << 30, dtype=torch.uint8, device="cuda")
     tcpck.synth_fixed(buf, 65536, 65536, (17 << 30) // 65536, seed=1)
-    out = torch.empty(1 << 16, dtype=torch.int32, device="cuda")
+    out = torch.empty(1 << 20, dtype=torch.int32, device="cuda")
     for nbytes in (1566572544, 17 << 30):
         times = {v: [] for v in NAMES}
         for _ in range(4):

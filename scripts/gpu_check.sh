@@ -25,6 +25,7 @@ for s in ${STEPS:-tests smoke bench prof}; do
     rv) step rv 900 python -m pytest tests/test_gpu_kernels.py -x -q -k "rvstream or rstream" ;;
     sweep_c2) step sweep_c2 600 python scripts/sweep.py --configs c2 ;;
     rvprobe) step rvprobe 600 python scripts/rv_probe.py ;;
+    diagstream) step diagstream 600 python scripts/diag_stream.py ;;
     policy) step policy 900 python scripts/policy_sweep.py ;;
     policy_fixed) step policy_fixed 900 python scripts/policy_sweep.py --no-mixes ;;
     vs) step vs 900 python -m pytest tests/test_gpu_kernels.py -x -q -k vstream ;;

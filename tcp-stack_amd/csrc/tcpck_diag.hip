@@ -57,6 +57,81 @@ __global__ void __launch_bounds__(kBlock) diag_stream_kernel(const uint8_t *buf,
   if (lane == 0) out[wid] = carry;
 }
 
+// Block-shared dynamic units: a 1024-thread block (16 waves, 4 per SIMD, of
+// different ages) owns an equal static byte range, cut into units of UNIT KiB
+// that its waves take from an LDS counter (ds_add_rtn: lgkmcnt, no interplay
+// with the load ring's vmcnt).  The ring rolls from one unit into the next
+// (the next unit is taken one unit ahead), so waves the SIMD favours simply
+// take more units and all waves of the block finish together.
+template <int U, int UNIT>
+__global__ void __launch_bounds__(1024) diag_dyn_kernel(const uint8_t *buf, uint64_t bytes, uint32_t *out) {
+  __shared__ uint32_t s_next;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t lines = bytes >> 7;
+  const uint64_t b0 = (static_cast<uint64_t>(blockIdx.x) * lines / gridDim.x) << 7;
+  const uint64_t b1 = (static_cast<uint64_t>(blockIdx.x + 1) * lines / gridDim.x) << 7;
+  constexpr uint32_t kUnit = UNIT * 1024u;
+  const uint32_t range = static_cast<uint32_t>(b1 - b0);
+  const uint32_t nunits = (range + kUnit - 1) / kUnit;
+  if (threadIdx.x == 0) s_next = 0;
+  __syncthreads();
+  const uint8_t *base = buf + b0;
+  auto grab = [&]() -> uint32_t {
+    uint32_t t = 0;
+    if (lane == 0) t = atomicAdd(&s_next, 1u);
+    return static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(t)));
+  };
+  uint32_t cur = grab();
+  if (cur >= nunits) return;
+  uint32_t nxt = grab();
+  const uint32_t last_chunk = (range >> 4) - 1;
+  // virtual step v of the wave: steps of unit cur are v in [vcur, vcur + kSteps)
+  constexpr uint32_t kSteps = UNIT;
+  uint32_t vcur = 0;
+  auto addr_of = [&](uint32_t v) -> uint32_t {  // chunk index of lane for virtual step v
+    const uint32_t t = v - vcur;
+    const uint32_t u = t < kSteps ? cur : nxt;  // units are >= U steps: at most one ahead
+    const uint32_t tt = t < kSteps ? t : t - kSteps;
+    const uint32_t ci = u * (kUnit >> 4) + (tt << 6) + lane;
+    return min(ci, last_chunk);  // invalid next unit / range end: clamp (masked below)
+  };
+  u32x4 ring[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) ring[u] = dev::load16_nt(base + 16 * static_cast<uint64_t>(addr_of(u)));
+  uint32_t carry = 0;
+  uint32_t v = 0;
+  while (true) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t cbyte = (cur * (kUnit >> 4) + ((v + u - vcur) << 6) + lane) << 4;
+      u32x4 w = ring[u];
+      if (cbyte >= range) w = u32x4{0, 0, 0, 0};
+      const uint32_t t = dev::ref_chunk_sum(w);
+      const uint32_t incl = dev::wave_inclusive_scan(t);
+      carry += dev::read_lane(incl, 63);
+      ring[u] = dev::load16_nt(base + 16 * static_cast<uint64_t>(addr_of(v + u + U)));
+    }
+    v += U;
+    if (v - vcur >= kSteps) {  // unit done (kSteps multiple of U)
+      if (nxt >= nunits) break;
+      cur = nxt;
+      vcur += kSteps;
+      nxt = grab();
+    }
+  }
+  if (lane == 0) out[blockIdx.x * 16 + (threadIdx.x >> 6)] = carry;
+}
+
+template <int U, int UNIT>
+hipError_t launch_dyn(const uint8_t *buf, uint64_t bytes, uint32_t *out, uint32_t num_cus, hipStream_t s) {
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, diag_dyn_kernel<U, UNIT>, 1024, 0) != hipSuccess || nb < 1)
+    nb = 1;
+  hipLaunchKernelGGL((diag_dyn_kernel<U, UNIT>), dim3(static_cast<uint32_t>(nb) * num_cus), dim3(1024), 0, s, buf,
+                     bytes, out);
+  return hipGetLastError();
+}
+
 template <int LPB, int U, bool SCAN>
 hipError_t launch_one(const uint8_t *buf, uint64_t bytes, uint32_t *out, uint32_t num_cus, hipStream_t s) {
   static const uint32_t per_cu = dev::resident_blocks_per_cu(diag_stream_kernel<LPB, U, SCAN>);
@@ -67,7 +142,9 @@ hipError_t launch_one(const uint8_t *buf, uint64_t bytes, uint32_t *out, uint32_
 }  // namespace
 
 // variant: LPB x U x scan: 0 = 1x4 scan, 1 = 1x4 no scan, 2 = 2x2 scan, 3 = 2x2 no scan,
-// 4 = 4x1 scan, 5 = 2x4 scan, 6 = 4x2 scan, 7 = 1x2 scan
+// 4 = 4x1 scan, 5 = 2x4 scan, 6 = 4x2 scan, 7 = 1x2 scan;
+// block-shared dynamic units (1x16 B, scan): 8 = U4 16 KiB units, 9 = U4 32 KiB,
+// 10 = U4 8 KiB, 11 = U8 32 KiB
 hipError_t launch_diag_stream(int variant, const uint8_t *buf, uint64_t bytes, uint32_t *out, uint32_t num_cus,
                               hipStream_t s) {
   switch (variant) {
@@ -79,6 +156,10 @@ hipError_t launch_diag_stream(int variant, const uint8_t *buf, uint64_t bytes, u
     case 5: return launch_one<2, 4, true>(buf, bytes, out, num_cus, s);
     case 6: return launch_one<4, 2, true>(buf, bytes, out, num_cus, s);
     case 7: return launch_one<1, 2, true>(buf, bytes, out, num_cus, s);
+    case 8: return launch_dyn<4, 16>(buf, bytes, out, num_cus, s);
+    case 9: return launch_dyn<4, 32>(buf, bytes, out, num_cus, s);
+    case 10: return launch_dyn<4, 8>(buf, bytes, out, num_cus, s);
+    case 11: return launch_dyn<8, 32>(buf, bytes, out, num_cus, s);
     default: return hipErrorInvalidValue;
   }
 }
