@@ -39,6 +39,12 @@ extern "C" {
                                   wave, all boundaries of a step resolved by the
                                   lanes in parallel (small images); param =
                                   variant (0: 4 loads in flight, 1: 2, 2: 8)    */
+#define TCPCK_KERNEL_VVSTREAM 8 /* packed variable layouts, MODE_REF, CHECKSUM /
+                                   VERIFY: run per wave, a step's boundaries
+                                   resolved in parallel from an LDS ring of
+                                   image ends; param = variant (0: 4 loads in
+                                   flight, 1: 8; 2/3: same with equal-count
+                                   instead of byte-balanced runs)               */
 #define TCPCK_KERNEL_RVSTREAM 6 /* packed variable layouts, MODE_REF: byte-balanced
                                    run per wave, scalar walk over the lengths;
                                    param = variant (0: 4 loads in flight, 1: 2,

@@ -28,6 +28,8 @@ for s in ${STEPS:-tests smoke bench prof}; do
     diagstream) step diagstream 600 python scripts/diag_stream.py ;;
     policy) step policy 900 python scripts/policy_sweep.py ;;
     policy_fixed) step policy_fixed 900 python scripts/policy_sweep.py --no-mixes ;;
+    policy_mix) step policy_mix 900 python scripts/policy_sweep.py --no-fixed ;;
+    vv) step vv 900 python -m pytest tests/test_gpu_kernels.py -x -q -k vvstream ;;
     vs) step vs 900 python -m pytest tests/test_gpu_kernels.py -x -q -k vstream ;;
     bench_c4) step bench_c4 600 python bench.py --config c4 --no-cpu-baseline ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-e2e ;;

@@ -43,11 +43,12 @@ def main():
     p.add_argument("--bytes", type=int, default=1564475392)
     p.add_argument("--reps", type=int, default=6)
     p.add_argument("--no-mixes", action="store_true")
+    p.add_argument("--no-fixed", action="store_true")
     args = p.parse_args()
     ctx = tcpck.Context(0)
     s = torch.cuda.current_stream()
     K = tcpck
-    for L in FIXED_L:
+    for L in ([] if args.no_fixed else FIXED_L):
         n = args.bytes // L
         a = torch.empty(n * L, dtype=torch.uint8, device="cuda")
         K.synth_fixed(a, L, L, n, seed=42)
@@ -115,6 +116,12 @@ def main():
                                                     **lay)),
                 ("rvstream", lambda: ctx.batch_var_ex(K.OP_CHECKSUM, a, off, ln, n, out, K.KERNEL_RVSTREAM, 0,
                                                       stream=s, **lay)),
+                ("vvstream", lambda: ctx.batch_var_ex(K.OP_CHECKSUM, a, off, ln, n, out, K.KERNEL_VVSTREAM, 0,
+                                                      stream=s, **lay)),
+                ("vvstream U8", lambda: ctx.batch_var_ex(K.OP_CHECKSUM, a, off, ln, n, out, K.KERNEL_VVSTREAM, 1,
+                                                         stream=s, **lay)),
+                ("vvstream cnt", lambda: ctx.batch_var_ex(K.OP_CHECKSUM, a, off, ln, n, out, K.KERNEL_VVSTREAM, 2,
+                                                          stream=s, **lay)),
                 ("rvstream cnt", lambda: ctx.batch_var_ex(K.OP_CHECKSUM, a, off, ln, n, out, K.KERNEL_RVSTREAM, 3,
                                                           stream=s, **lay))]
         runs = []

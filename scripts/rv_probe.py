@@ -47,7 +47,8 @@ def main():
         tcpck.synth_var(a, d_off, d_ln, int(ln.max()), n, seed=42)
         ref = torch.empty(n, dtype=torch.int16, device="cuda")
         ctx.batch_var_ex(tcpck.OP_CHECKSUM, a, d_off, d_ln, n, ref, tcpck.KERNEL_SEG, 0)
-        runs = [(f"rvstream v{v}", "var", tcpck.KERNEL_RVSTREAM, v) for v in (0, 1, 2, 3)]
+        runs = [(f"rvstream v{v}", "var", tcpck.KERNEL_RVSTREAM, v) for v in (0, 3)]
+        runs += [(f"vvstream v{v}", "var", tcpck.KERNEL_VVSTREAM, v) for v in (0, 1, 2, 3)]
         runs += [("span T16", "var", tcpck.KERNEL_SPAN, 16), ("stream U4", "var", tcpck.KERNEL_STREAM, 0)]
         if name != "c3":
             L = int(ln[0])

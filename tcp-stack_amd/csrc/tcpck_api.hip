@@ -259,6 +259,17 @@ hipError_t run_var(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const uint6
     a.tile = param > 0 ? static_cast<uint32_t>(param) : tcpck::span_tile_for_len(typical);
     return tcpck::launch_span(op, false, a, static_cast<uint32_t>(ctx->num_cus), s);
   }
+  if (kernel == TCPCK_KERNEL_VVSTREAM) {
+    if (mode != TCPCK_MODE_REF) return hipErrorInvalidValue;
+    tcpck::SpanArgs a{};
+    a.arena = arena;
+    a.offsets = off;
+    a.lengths = len;
+    a.base = base;
+    a.count = count;
+    a.out = out;
+    return tcpck::launch_vvstream(op, param, a, static_cast<uint32_t>(ctx->num_cus), s);
+  }
   if (kernel == TCPCK_KERNEL_RVSTREAM) {
     // offsets ascending and packed (the layout hint); a wave whose length walk
     // disagrees with the offsets recomputes its images one by one

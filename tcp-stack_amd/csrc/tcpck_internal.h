@@ -79,6 +79,9 @@ hipError_t launch_vstream(int op, int variant, const FixedStreamArgs &a, uint32_
 // ---- run-stream kernel for packed variable layouts (tcpck_rvstream.hip), MODE_REF:
 // variant = loads in flight (0: 4, 1: 2, 2: 8) | blocks-per-CU cap << 8
 hipError_t launch_rvstream(int op, int variant, const SpanArgs &a, uint32_t num_cus, hipStream_t stream);
+// ---- vector-boundary run stream for packed variable layouts (tcpck_vvstream.hip),
+// MODE_REF, kChecksum / kVerify: variant 0 U4 byte split, 1 U8, 2 U4 count split, 3 U8
+hipError_t launch_vvstream(int op, int variant, const SpanArgs &a, uint32_t num_cus, hipStream_t stream);
 // timing-only streaming micro-kernels (tcpck_diag.hip)
 hipError_t launch_diag_stream(int variant, const uint8_t *buf, uint64_t bytes, uint32_t *out, uint32_t num_cus,
                               hipStream_t s);

@@ -1,0 +1,264 @@
+// tcpck_vvstream.hip -- packed variable-length batches (C3): one contiguous
+// run of whole images per wave, the boundaries of each 1 KiB step resolved by
+// the lanes in parallel from a per-wave LDS ring of image end positions.
+//
+// Reference semantics: CalculateChecksum, include/tcp-header.h:252-263:
+// ~(sum of the image's LE u16 words mod 2^16).  Packed images make the run one
+// flat byte stream and sum(k) = P(end_k) - P(end_{k-1}) (mod 2^16), with P(x)
+// the word sum of the run before byte x.
+//
+//   * run split as rvstream (byte-balanced, two lockstep 64-ary searches);
+//   * image end positions: 256 lengths at a time are read with one vector
+//     load per lane (4 lengths each, prefetched a round ahead, so the load
+//     ring drains once per 256 images), prefix-summed across the wave and
+//     written to a 512-entry LDS ring per wave;
+//   * per step: lane j reads end e(jn + j) from LDS; the lanes whose end falls
+//     in the step (a ballot, <= 64 since images are >= 16 B, at most one end
+//     per chunk) post the end's byte offset into the LDS slot of the lane
+//     holding that chunk; that lane forms P = carry + exclusive scan + its
+//     words before the end (partial sums of its own v_dot2 chain) and clears
+//     its slot; the boundary lane takes P back (ds_bpermute); sum(jn + j) =
+//     P(j) - P(j - 1), P(-1) = the last P of the step before (one SGPR);
+//   * results leave from lanes 0..cnt-1 as one contiguous store per step.
+// A wave whose lengths are shorter than 16 B or disagree with the offsets
+// (layout hint wrong) recomputes its images one by one.  kFill is served by
+// the span kernel (the host routes it); kChecksum and kVerify here.
+#include "tcpck_device.h"
+#include "tcpck_internal.h"
+
+namespace tcpck {
+
+namespace {
+
+using dev::kBlock;
+using dev::kWavesPerBlock;
+using dev::u32x4;
+
+constexpr uint32_t kRound = 256;   // ends loaded per round (4 per lane)
+constexpr uint32_t kRing = 512;    // LDS ring entries per wave (two rounds)
+
+__device__ __forceinline__ void find_two(const uint64_t *offsets, uint64_t base, uint64_t count, uint64_t t0,
+                                         uint64_t t1, uint64_t &r0, uint64_t &r1) {
+  const uint32_t lane = threadIdx.x & 63;
+  uint64_t lo[2] = {0, 0}, hi[2] = {count, count};
+  const uint64_t t[2] = {t0, t1};
+  while (hi[0] - lo[0] > 64 || hi[1] - lo[1] > 64) {
+    uint64_t step[2], idx[2], v[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      step[i] = hi[i] - lo[i] > 64 ? (hi[i] - lo[i] + 63) / 64 : 1;
+      idx[i] = lo[i] + lane * step[i];
+      v[i] = idx[i] < hi[i] ? offsets[idx[i]] : 0;
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      if (hi[i] - lo[i] <= 64) continue;
+      const bool below = idx[i] < hi[i] && v[i] - base < t[i];
+      const uint32_t c = __popcll(__ballot(below));
+      const uint64_t nlo = c ? lo[i] + (c - 1) * step[i] + 1 : lo[i];
+      hi[i] = min(hi[i], lo[i] + c * step[i]);
+      lo[i] = nlo;
+    }
+  }
+  uint64_t v[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const uint64_t idx = lo[i] + lane;
+    v[i] = idx < hi[i] ? offsets[idx] : 0;
+  }
+  const bool b0 = lo[0] + lane < hi[0] && v[0] - base < t0;
+  const bool b1 = lo[1] + lane < hi[1] && v[1] - base < t1;
+  r0 = lo[0] + __popcll(__ballot(b0));
+  r1 = lo[1] + __popcll(__ballot(b1));
+}
+
+__device__ __forceinline__ uint32_t lane_bpermute(uint32_t v, uint32_t src_lane) {
+  return static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(static_cast<int>(src_lane << 2), static_cast<int>(v)));
+}
+
+template <int U, int OP, int SPLIT>
+__global__ void __launch_bounds__(kBlock)
+    vvstream_kernel(uint8_t *__restrict__ arena, const uint64_t *__restrict__ offsets,
+                    const uint32_t *__restrict__ lengths, uint64_t base, uint64_t count, void *__restrict__ out) {
+  __shared__ uint32_t s_end[kWavesPerBlock][kRing];
+  __shared__ uint32_t s_slot[kWavesPerBlock][64];  // end offset in chunk + 1, posted to the chunk's lane
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wv = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6)));
+  const uint64_t W = static_cast<uint64_t>(gridDim.x) * kWavesPerBlock;
+  const uint64_t wid = static_cast<uint64_t>(blockIdx.x) * kWavesPerBlock + wv;
+  const uint64_t N = count;
+  uint64_t kb, ke;
+  if (SPLIT == 1) {
+    kb = wid * N / W;
+    ke = (wid + 1) * N / W;
+  } else {
+    const uint64_t first = offsets[0] - base;
+    const uint64_t total = offsets[N - 1] - base + lengths[N - 1] - first;
+    const uint64_t q = total / W, rm = total % W;
+    find_two(offsets, base, N, first + q * wid + rm * wid / W, first + q * (wid + 1) + rm * (wid + 1) / W, kb, ke);
+    if (wid == 0) kb = 0;
+    if (wid + 1 == W) ke = N;
+  }
+  if (kb >= ke) return;
+
+  const uint64_t s0 = offsets[kb] - base;
+  const uint64_t s1 = offsets[ke - 1] - base + lengths[ke - 1];
+  const uint64_t A0 = dev::align128_rel(arena, s0);
+  const uint32_t nimg = static_cast<uint32_t>(ke - kb);
+  bool bad = !(s1 >= s0 && s1 - A0 < (uint64_t{1} << 31));
+
+  auto store = [&](uint64_t k, uint32_t sum) {
+    const uint16_t c = static_cast<uint16_t>(~sum);  // tcp-header.h:262
+    if constexpr (OP == kVerify)
+      static_cast<uint8_t *>(out)[k] = (c == 0) ? 1 : 0;
+    else
+      static_cast<uint16_t *>(out)[k] = c;
+  };
+
+  if (!bad) {
+    const uint32_t lead = static_cast<uint32_t>(s0 - A0);
+    const uint32_t span = static_cast<uint32_t>(s1 - A0);
+    const uint32_t nsteps = (span + 1023) >> 10;
+    const uint32_t last_chunk = span > 0 ? (span - 1) >> 4 : 0;
+    const auto rsrc = dev::make_rsrc(arena + A0, (last_chunk + 1) << 4);
+    auto load_step = [&](uint32_t st) -> u32x4 { return dev::load16_buf_nt(rsrc, lane << 4, st << 10); };
+    uint32_t *ring_end = s_end[wv];
+    uint32_t *slot = s_slot[wv];
+    slot[lane] = 0;
+
+    // descriptor rounds: lengths of run images [256 r, 256 r + 256), 4 per lane
+    const uint32_t *lens = lengths + kb;
+    auto load_round = [&](uint32_t r, uint32_t (&d)[4]) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t j = r * kRound + 4 * lane + i;
+        d[i] = j < nimg ? lens[j] : 0u;
+      }
+    };
+    uint32_t dnext[4];
+    load_round(0, dnext);
+    uint32_t loaded = 0;     // ends written to the ring (run-relative image count)
+    uint32_t pos = lead;     // end of the last written image
+    bool short_img = false;  // an image < 16 B: more than one end per chunk possible
+    auto fill_round = [&]() {  // write round (loaded / 256) from dnext, prefetch the next
+      uint32_t d[4] = {dnext[0], dnext[1], dnext[2], dnext[3]};
+      const uint32_t r = loaded / kRound;
+      load_round(r + 1, dnext);
+      uint32_t e1 = d[0], e2 = e1 + d[1], e3 = e2 + d[2], e4 = e3 + d[3];
+      const uint32_t incl = dev::wave_inclusive_scan(e4);
+      const uint32_t ex = pos + incl - e4;
+      const uint32_t jb = r * kRound + 4 * lane;
+      bool sh = false;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sh |= (jb + i < nimg) && d[i] < 16;
+      short_img |= __ballot(sh) != 0;
+      const uint32_t si = (r * kRound) % kRing + 4 * lane;
+      ring_end[si] = ex + e1;
+      ring_end[si + 1] = ex + e2;
+      ring_end[si + 2] = ex + e3;
+      ring_end[si + 3] = ex + e4;
+      pos = pos + dev::read_lane(incl, 63);
+      loaded += kRound;
+    };
+    fill_round();
+
+    uint32_t carry = 0, p_last = 0, jn = 0;
+    u32x4 ring[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) ring[u] = load_step(static_cast<uint32_t>(u));
+
+    for (uint32_t g = 0; g < nsteps && !short_img; g += U) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t st = g + u;
+        const uint32_t sb = st << 10;
+        const uint32_t c = sb + (lane << 4);
+        u32x4 w = ring[u];
+        if (sb == 0 || sb + 1024 > span) {
+          const int32_t lo = min(max(static_cast<int32_t>(lead) - static_cast<int32_t>(c), 0), 16);
+          const int32_t hi = min(max(static_cast<int32_t>(span) - static_cast<int32_t>(c), 0), 16);
+          w = dev::apply_mask(w, dev::word_mask(lo, hi));
+        }
+        const uint32_t q1 = dev::dot2_u16(w.x, 0u);
+        const uint32_t q2 = dev::dot2_u16(w.y, q1);
+        const uint32_t q3 = dev::dot2_u16(w.z, q2);
+        const uint32_t tot = dev::dot2_u16(w.w, q3);
+        const uint32_t incl = dev::wave_inclusive_scan(tot);
+        if (jn + 64 > loaded && loaded < nimg) fill_round();  // keep >= 64 ends ahead
+        const uint32_t j = jn + lane;
+        const uint32_t e = j < nimg ? ring_end[j % kRing] : ~0u;
+        const bool inb = e < sb + 1024;
+        const uint64_t bal = __ballot(inb);
+        if (bal) {
+          const uint32_t cnt = static_cast<uint32_t>(__popcll(bal));  // lanes 0..cnt-1 (ends ascend)
+          const uint32_t rel = e - sb;
+          const uint32_t cl = rel >> 4;
+          if (inb) slot[cl] = (rel & 15u) + 1u;  // tell the chunk's lane where the end lies
+          const uint32_t rr = slot[lane];
+          if (rr) slot[lane] = 0u;
+          const uint32_t r = rr ? rr - 1 : 0u;
+          const uint32_t di = r >> 2;
+          const uint32_t qd = di == 0 ? 0u : (di == 1 ? q1 : (di == 2 ? q2 : q3));
+          const uint32_t dw = di == 0 ? w.x : (di == 1 ? w.y : (di == 2 ? w.z : w.w));
+          const uint32_t pb = carry + incl - tot + qd + ((r & 2u) ? (dw & 0xFFFFu) : 0u);
+          const uint32_t pj = lane_bpermute(pb, inb ? cl : 0u);
+          const uint32_t pl = lane_bpermute(pj, lane ? lane - 1 : 0u);
+          const uint32_t pprev = lane == 0 ? p_last : pl;
+          if (inb) store(kb + j, pj - pprev);
+          p_last = dev::read_lane(pj, cnt - 1);
+          jn += cnt;
+        }
+        carry += dev::read_lane(incl, 63);
+        ring[u] = load_step(st + U);
+      }
+    }
+    bad = short_img || pos != span || loaded < nimg;
+    if (!bad && jn < nimg) {  // the last end sits exactly at the last step's end
+      if (lane == 0) store(kb + jn, carry - p_last);
+      jn += 1;
+    }
+    bad = bad || jn != nimg;
+  }
+  if (bad) {  // wave-uniform: the layout is not what the walk assumed -> exact per-image pass
+    for (uint64_t k = kb; k < ke; ++k) {
+      const uint32_t sum = dev::wave_image_sum<2, kRef>(arena, offsets[k] - base, lengths[k], false);
+      if (lane == 0) store(k, sum);
+    }
+  }
+}
+
+template <int U, int OP, int SPLIT>
+hipError_t launch_one(const SpanArgs &a, uint32_t num_cus, hipStream_t stream) {
+  static const uint32_t per_cu = dev::resident_blocks_per_cu(vvstream_kernel<U, OP, SPLIT>);
+  uint64_t blocks = static_cast<uint64_t>(per_cu) * num_cus;
+  const uint64_t need = (a.count + kWavesPerBlock - 1) / kWavesPerBlock;
+  if (blocks > need) blocks = need;
+  if (blocks == 0) return hipSuccess;
+  hipLaunchKernelGGL((vvstream_kernel<U, OP, SPLIT>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0, stream,
+                     a.arena, a.offsets, a.lengths, a.base, a.count, a.out);
+  return hipGetLastError();
+}
+
+template <int U, int SPLIT>
+hipError_t dispatch(int op, const SpanArgs &a, uint32_t num_cus, hipStream_t s) {
+  switch (op) {
+    case kChecksum: return launch_one<U, kChecksum, SPLIT>(a, num_cus, s);
+    case kVerify: return launch_one<U, kVerify, SPLIT>(a, num_cus, s);
+    default: return hipErrorInvalidValue;  // kFill: span kernel
+  }
+}
+
+}  // namespace
+
+hipError_t launch_vvstream(int op, int variant, const SpanArgs &a, uint32_t num_cus, hipStream_t stream) {
+  if (a.count == 0) return hipSuccess;
+  switch (variant) {
+    case 0: return dispatch<4, 0>(op, a, num_cus, stream);
+    case 1: return dispatch<8, 0>(op, a, num_cus, stream);
+    case 2: return dispatch<4, 1>(op, a, num_cus, stream);
+    case 3: return dispatch<8, 1>(op, a, num_cus, stream);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace tcpck

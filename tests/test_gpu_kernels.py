@@ -453,3 +453,62 @@ def test_vstream_fill_verify(ctx, variant, length):
     ok = torch.empty(count, dtype=torch.uint8, device="cuda")
     ctx.batch_fixed_ex(tcpck.OP_VERIFY, dev(got), length, length, count, ok, tcpck.KERNEL_VSTREAM, variant)
     np.testing.assert_array_equal(np.nonzero(host(ok) == 0)[0], np.sort(bad))
+
+
+# ---- vector-boundary run stream for packed variable layouts (KERNEL_VVSTREAM = 8) ----
+VVSTREAM = [0, 1, 2, 3]
+
+
+@pytest.mark.parametrize("variant", VVSTREAM)
+@pytest.mark.parametrize("payloads", [(64, 576, 1460), (-16, 0, 1460), (-16,), (0, 9000, 65504), (-32, 64, 1460)])
+@pytest.mark.parametrize("count", [1, 2, 63, 64, 65, 255, 256, 257, 1000, 70001])
+def test_vvstream_var_vs_oracle(ctx, oracle_c, variant, payloads, count):
+    """Includes 16-B images (one end per chunk at most) and, with payload -32,
+    empty images: waves holding one fall back to per-image sums."""
+    import tcpck
+    off, ln, total = packed_layout(count, count * 5 + len(payloads), payloads)
+    if total > (96 << 20):
+        return
+    rng = np.random.default_rng(count + 3 * variant)
+    arena_np = rng.integers(0, 256, total + 128, dtype=np.uint8)
+    buf = dev(arena_np)
+    d_off, d_ln = dev(off), dev(ln)
+    for mis in (0, 2, 126):
+        out = torch.empty(count, dtype=torch.int16, device="cuda")
+        ctx.batch_var_ex(tcpck.OP_CHECKSUM, buf.data_ptr() + mis, d_off, d_ln, count, out,
+                         tcpck.KERNEL_VVSTREAM, variant, packed=True)
+        np.testing.assert_array_equal(host(out).view(np.uint16), oracle_c.batch(arena_np[mis:], off, ln, threads=8))
+
+
+@pytest.mark.parametrize("variant", VVSTREAM)
+def test_vvstream_not_packed_and_verify(ctx, oracle_c, variant):
+    import tcpck
+    import synth_np
+    from oracle import ref16 as R
+    rng = np.random.default_rng(40 + variant)
+    count = 30000
+    off, ln, _ = synth_np.mixed_layout(count, seed=9)
+    off = off.copy()
+    for k in rng.integers(1, count, 25):
+        off[k:] += 10
+    total = int(off[-1] + ln[-1]) + 64
+    arena_np = rng.integers(0, 256, total, dtype=np.uint8)
+    out = torch.empty(count, dtype=torch.int16, device="cuda")
+    ctx.batch_var_ex(tcpck.OP_CHECKSUM, dev(arena_np), dev(off), dev(ln), count, out,
+                     tcpck.KERNEL_VVSTREAM, variant, packed=True)
+    np.testing.assert_array_equal(host(out).view(np.uint16), oracle_c.batch(arena_np, off, ln, threads=8))
+    # verify on a packed, filled batch with corruptions
+    off, ln, total = packed_layout(count, 77, (64, 576, 1460))
+    arena_np = rng.integers(0, 256, total, dtype=np.uint8)
+    for k in range(count):
+        R.fill_np(arena_np[int(off[k]):int(off[k]) + int(ln[k])])
+    bad = rng.choice(count, 60, replace=False)
+    for k in bad:
+        arena_np[int(off[k]) + int(rng.integers(0, int(ln[k])))] ^= 0x81
+    ok = torch.empty(count, dtype=torch.uint8, device="cuda")
+    ctx.batch_var_ex(tcpck.OP_VERIFY, dev(arena_np), dev(off), dev(ln), count, ok, tcpck.KERNEL_VVSTREAM, variant,
+                     packed=True)
+    np.testing.assert_array_equal(np.nonzero(host(ok) == 0)[0], np.sort(bad))
+    with pytest.raises(tcpck.TcpckError):
+        ctx.batch_var_ex(tcpck.OP_FILL, dev(arena_np), dev(off), dev(ln), count, ok, tcpck.KERNEL_VVSTREAM, variant,
+                         packed=True)
