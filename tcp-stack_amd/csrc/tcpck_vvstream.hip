@@ -37,41 +37,6 @@ using dev::u32x4;
 constexpr uint32_t kRound = 256;   // ends loaded per round (4 per lane)
 constexpr uint32_t kRing = 512;    // LDS ring entries per wave (two rounds)
 
-__device__ __forceinline__ void find_two(const uint64_t *offsets, uint64_t base, uint64_t count, uint64_t t0,
-                                         uint64_t t1, uint64_t &r0, uint64_t &r1) {
-  const uint32_t lane = threadIdx.x & 63;
-  uint64_t lo[2] = {0, 0}, hi[2] = {count, count};
-  const uint64_t t[2] = {t0, t1};
-  while (hi[0] - lo[0] > 64 || hi[1] - lo[1] > 64) {
-    uint64_t step[2], idx[2], v[2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      step[i] = hi[i] - lo[i] > 64 ? (hi[i] - lo[i] + 63) / 64 : 1;
-      idx[i] = lo[i] + lane * step[i];
-      v[i] = idx[i] < hi[i] ? offsets[idx[i]] : 0;
-    }
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      if (hi[i] - lo[i] <= 64) continue;
-      const bool below = idx[i] < hi[i] && v[i] - base < t[i];
-      const uint32_t c = __popcll(__ballot(below));
-      const uint64_t nlo = c ? lo[i] + (c - 1) * step[i] + 1 : lo[i];
-      hi[i] = min(hi[i], lo[i] + c * step[i]);
-      lo[i] = nlo;
-    }
-  }
-  uint64_t v[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const uint64_t idx = lo[i] + lane;
-    v[i] = idx < hi[i] ? offsets[idx] : 0;
-  }
-  const bool b0 = lo[0] + lane < hi[0] && v[0] - base < t0;
-  const bool b1 = lo[1] + lane < hi[1] && v[1] - base < t1;
-  r0 = lo[0] + __popcll(__ballot(b0));
-  r1 = lo[1] + __popcll(__ballot(b1));
-}
-
 __device__ __forceinline__ uint32_t lane_bpermute(uint32_t v, uint32_t src_lane) {
   return static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(static_cast<int>(src_lane << 2), static_cast<int>(v)));
 }
@@ -95,7 +60,7 @@ __global__ void __launch_bounds__(kBlock)
     const uint64_t first = offsets[0] - base;
     const uint64_t total = offsets[N - 1] - base + lengths[N - 1] - first;
     const uint64_t q = total / W, rm = total % W;
-    find_two(offsets, base, N, first + q * wid + rm * wid / W, first + q * (wid + 1) + rm * (wid + 1) / W, kb, ke);
+    dev::find_two(offsets, base, N, first + q * wid + rm * wid / W, first + q * (wid + 1) + rm * (wid + 1) / W, kb, ke);
     if (wid == 0) kb = 0;
     if (wid + 1 == W) ke = N;
   }
