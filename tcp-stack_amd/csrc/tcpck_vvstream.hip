@@ -90,6 +90,7 @@ __global__ void __launch_bounds__(kBlock)
     uint32_t *ring_end = s_end[wv];
     uint32_t *slot = s_slot[wv];
     slot[lane] = 0;
+    __builtin_amdgcn_wave_barrier();
 
     // descriptor rounds: lengths of run images [256 r, 256 r + 256), 4 per lane
     const uint32_t *lens = lengths + kb;
@@ -124,6 +125,7 @@ __global__ void __launch_bounds__(kBlock)
       ring_end[si + 3] = ex + e4;
       pos = pos + dev::read_lane(incl, 63);
       loaded += kRound;
+      __builtin_amdgcn_wave_barrier();  // ends are read by other lanes
     };
     fill_round();
 
@@ -159,8 +161,10 @@ __global__ void __launch_bounds__(kBlock)
           const uint32_t rel = e - sb;
           const uint32_t cl = rel >> 4;
           if (inb) slot[cl] = (rel & 15u) + 1u;  // tell the chunk's lane where the end lies
+          __builtin_amdgcn_wave_barrier();        // cross-lane LDS hand-off: no per-lane forwarding
           const uint32_t rr = slot[lane];
           if (rr) slot[lane] = 0u;
+          __builtin_amdgcn_wave_barrier();
           const uint32_t r = rr ? rr - 1 : 0u;
           const uint32_t di = r >> 2;
           const uint32_t qd = di == 0 ? 0u : (di == 1 ? q1 : (di == 2 ? q2 : q3));
