@@ -244,7 +244,16 @@ hipError_t run_var(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const uint6
   const uint64_t typical = (layout && layout->total_bytes) ? layout->total_bytes / count : 1500;
   const bool span_ok = mode == TCPCK_MODE_REF && layout && (layout->flags & TCPCK_LAYOUT_PACKED) &&
                        (layout->min_len == 0 || layout->min_len >= 16);
-  if (kernel == TCPCK_KERNEL_AUTO) kernel = (span_ok && typical <= kSpanMaxLen) ? TCPCK_KERNEL_SPAN : TCPCK_KERNEL_SEG;
+  // packed, reference mode: checksum / verify on vvstream (C3 78.5%, 96-B images
+  // 74% vs span's 37%: profiles/r01/rv_probe.log, policy_mix.log); fill on span
+  if (kernel == TCPCK_KERNEL_AUTO) {
+    if (!span_ok || typical > kSpanMaxLen)
+      kernel = TCPCK_KERNEL_SEG;
+    else if (op == TCPCK_OP_FILL)
+      kernel = TCPCK_KERNEL_SPAN;
+    else
+      kernel = TCPCK_KERNEL_VVSTREAM;
+  }
   if (kernel == TCPCK_KERNEL_SPAN) {
     // the kernel re-checks packing and lengths per tile, so a wrong hint
     // costs speed, never correctness
