@@ -118,9 +118,18 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
-    torch.cuda.set_device(local)
+    # rehearsal knobs (not used by the driver): several ranks on one GPU with
+    # gloo collectives, to exercise the N>1 path on a one-GPU box
+    backend = os.environ.get("TCPCK_BENCH_BACKEND", "nccl")
+    dev_index = int(os.environ.get("TCPCK_BENCH_DEVICE", local))
+    coll_dev = "cuda" if backend == "nccl" else "cpu"
+    torch.cuda.set_device(dev_index)
+    local = dev_index
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
 
     from tcpck.shard import max_over_ranks, shard_range
     desc, kind, count, L = CONFIGS[args.config]
@@ -173,8 +182,8 @@ def main():
     elapsed = time.perf_counter() - t0
     launch_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts, ends)]))
 
-    tmax = max_over_ranks(elapsed, device="cuda")
-    shard_bytes = torch.tensor([img_bytes], dtype=torch.int64, device="cuda")
+    tmax = max_over_ranks(elapsed, device=coll_dev)
+    shard_bytes = torch.tensor([img_bytes], dtype=torch.int64, device=coll_dev)
     if world > 1:
         dist.all_reduce(shard_bytes)  # bytes all ranks processed per step (shards may differ by one image)
     total_bytes = int(shard_bytes.item()) * args.steps
