@@ -34,11 +34,13 @@ extern "C" {
                                   with s_setprio 1 for slots >= 4, 7: 3 + graded
                                   priority, 9: 4 with v_dot2 sums, 10/12/13:
                                   4/2/8 with v_dot2 sums and buffer loads, 11:
-                                  4 with buffer loads) | (blocks per CU cap << 8) */
+                                  4 with buffer loads) | (blocks per CU cap << 8)
+                                  | (grid oversubscription factor << 16)        */
 #define TCPCK_KERNEL_VSTREAM 7 /* fixed stride == len >= 16, MODE_REF: run per
                                   wave, all boundaries of a step resolved by the
                                   lanes in parallel (small images); param =
-                                  variant (0: 4 loads in flight, 1: 2, 2: 8)    */
+                                  variant (0: 4 loads in flight, 1: 2, 2: 8)
+                                  | (grid oversubscription factor << 16)        */
 #define TCPCK_KERNEL_VVSTREAM 8 /* packed variable layouts, MODE_REF, CHECKSUM /
                                    VERIFY: run per wave, a step's boundaries
                                    resolved in parallel from an LDS ring of

@@ -34,6 +34,7 @@ for s in ${STEPS:-tests smoke bench prof}; do
     bench_c4) step bench_c4 600 python bench.py --config c4 --no-cpu-baseline ;;
     mrank) step mrank 600 env TCPCK_BENCH_BACKEND=gloo TCPCK_BENCH_DEVICE=0 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29561 bench.py --gpus 2 --steps 5 --warmup 2 &&
       step mrank_c5 600 env TCPCK_BENCH_BACKEND=gloo TCPCK_BENCH_DEVICE=0 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29562 bench.py --gpus 2 --config c5 --steps 5 --warmup 2 ;;
+    oversub) step oversub 600 python scripts/oversub.py ;;
     prof_c3) step prof_c3 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c3 -o run --output-format csv -- python3 bench.py --config c3 --steps 10 --warmup 2 --no-cpu-baseline --no-e2e ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-e2e ;;
     pmc_c2|pmc_c3|pmc_c4)  # separate FETCH_SIZE / WRITE_SIZE passes (TCC slots), kernel trace only

@@ -216,6 +216,7 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
     a.out = out;
     a.dbg = static_cast<uint64_t *>(ctx->dbg);
     a.blocks_per_cu = static_cast<uint32_t>(param >> 8) & 0xFFu;
+    a.oversub = static_cast<uint32_t>(param >> 16) & 0xFu;
     return tcpck::launch_rstream(op, param & 0xFF, a, static_cast<uint32_t>(ctx->num_cus), s);
   }
   if (kernel == TCPCK_KERNEL_VSTREAM) {
@@ -225,6 +226,7 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
     a.stride = stride;
     a.count = count;
     a.out = out;
+    a.oversub = static_cast<uint32_t>(param >> 16) & 0xFu;
     return tcpck::launch_vstream(op, param & 0xFF, a, static_cast<uint32_t>(ctx->num_cus), s);
   }
   if (kernel != TCPCK_KERNEL_SEG) return hipErrorInvalidValue;

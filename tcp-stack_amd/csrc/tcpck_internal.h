@@ -69,6 +69,7 @@ struct FixedStreamArgs {
   uint32_t tile;    // images per tile (>= fstream_min_tile)
   uint64_t *dbg;    // optional per-wave {start, end} s_memrealtime stamps (timing builds)
   uint32_t blocks_per_cu;  // optional occupancy cap (0 = as many as fit)
+  uint32_t oversub;        // grid = resident blocks x this (0/1: one wave per resident slot)
 };
 // ---- run-stream kernel (fixed stride == len): one run per wave, scalar boundaries
 // variant: 0 = 4 loads in flight, 1 = 2, 2 = 8, 3 = 4 with per-wave time stamps
