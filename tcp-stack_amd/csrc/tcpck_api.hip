@@ -216,7 +216,7 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
     a.out = out;
     a.dbg = static_cast<uint64_t *>(ctx->dbg);
     a.blocks_per_cu = static_cast<uint32_t>(param >> 8) & 0xFFu;
-    a.oversub = static_cast<uint32_t>(param >> 16) & 0xFu;
+    a.oversub = static_cast<uint32_t>(param >> 16) & 0xFFu;
     return tcpck::launch_rstream(op, param & 0xFF, a, static_cast<uint32_t>(ctx->num_cus), s);
   }
   if (kernel == TCPCK_KERNEL_VSTREAM) {
@@ -226,7 +226,7 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
     a.stride = stride;
     a.count = count;
     a.out = out;
-    a.oversub = static_cast<uint32_t>(param >> 16) & 0xFu;
+    a.oversub = static_cast<uint32_t>(param >> 16) & 0xFFu;
     return tcpck::launch_vstream(op, param & 0xFF, a, static_cast<uint32_t>(ctx->num_cus), s);
   }
   if (kernel != TCPCK_KERNEL_SEG) return hipErrorInvalidValue;
@@ -236,7 +236,8 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
   a.len = len;
   a.count = count;
   a.out = out;
-  const auto shape = param > 0 ? static_cast<tcpck::SegShape>(param - 1) : tcpck::shape_for_len(len);
+  a.oversub = static_cast<uint32_t>(param >> 16) & 0xFFu;
+  const auto shape = (param & 0xFF) > 0 ? static_cast<tcpck::SegShape>((param & 0xFF) - 1) : tcpck::shape_for_len(len);
   return tcpck::launch_seg(op, mode, true, shape, a, static_cast<uint32_t>(ctx->num_cus), s);
 }
 
@@ -279,7 +280,8 @@ hipError_t run_var(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const uint6
     a.base = base;
     a.count = count;
     a.out = out;
-    return tcpck::launch_vvstream(op, param, a, static_cast<uint32_t>(ctx->num_cus), s);
+    a.oversub = static_cast<uint32_t>(param >> 16) & 0xFFu;
+    return tcpck::launch_vvstream(op, param & 0xFF, a, static_cast<uint32_t>(ctx->num_cus), s);
   }
   if (kernel == TCPCK_KERNEL_RVSTREAM) {
     // offsets ascending and packed (the layout hint); a wave whose length walk
@@ -315,7 +317,8 @@ hipError_t run_var(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const uint6
   a.base = base;
   a.count = count;
   a.out = out;
-  const auto shape = param > 0 ? static_cast<tcpck::SegShape>(param - 1) : tcpck::shape_for_len(typical);
+  a.oversub = static_cast<uint32_t>(param >> 16) & 0xFFu;
+  const auto shape = (param & 0xFF) > 0 ? static_cast<tcpck::SegShape>((param & 0xFF) - 1) : tcpck::shape_for_len(typical);
   return tcpck::launch_seg(op, mode, false, shape, a, static_cast<uint32_t>(ctx->num_cus), s);
 }
 

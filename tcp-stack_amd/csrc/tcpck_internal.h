@@ -30,6 +30,7 @@ struct SegArgs {
   uint64_t count;            // images
   void *out;                 // u16[count] or u8[count] (verify); may be null for fill
   uint32_t len;              // fixed layout: image length
+  uint32_t oversub;          // grid = resident blocks x this (0/1: one block per resident slot)
 };
 
 SegShape shape_for_len(uint64_t typical_len);
@@ -46,6 +47,7 @@ struct SpanArgs {
   uint64_t count;
   void *out;
   uint32_t tile;             // images per wave tile, 1..63
+  uint32_t oversub;          // grid = resident blocks x this (run-stream kernels; 0/1: none)
 };
 
 uint32_t span_tile_for_len(uint64_t typical_len);

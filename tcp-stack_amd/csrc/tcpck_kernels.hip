@@ -98,7 +98,7 @@ hipError_t launch_one(const SegArgs &a, uint32_t num_cus, hipStream_t stream) {
   uint64_t blocks = (a.count + groups_per_block - 1) / groups_per_block;
   // grid-stride kernel: launch exactly the resident blocks, never a second wave of them
   static const uint32_t per_cu = dev::resident_blocks_per_cu(seg_kernel<G, U, MODE, OP, FIXED>);
-  const uint64_t max_blocks = static_cast<uint64_t>(per_cu) * num_cus;
+  const uint64_t max_blocks = static_cast<uint64_t>(per_cu) * num_cus * (a.oversub > 1 ? a.oversub : 1u);
   if (blocks > max_blocks) blocks = max_blocks;
   if (blocks == 0) return hipSuccess;
   hipLaunchKernelGGL((seg_kernel<G, U, MODE, OP, FIXED>), dim3(static_cast<uint32_t>(blocks)),

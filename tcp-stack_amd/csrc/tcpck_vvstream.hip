@@ -199,7 +199,7 @@ __global__ void __launch_bounds__(kBlock)
 template <int U, int OP, int SPLIT>
 hipError_t launch_one(const SpanArgs &a, uint32_t num_cus, hipStream_t stream) {
   static const uint32_t per_cu = dev::resident_blocks_per_cu(vvstream_kernel<U, OP, SPLIT>);
-  uint64_t blocks = static_cast<uint64_t>(per_cu) * num_cus;
+  uint64_t blocks = static_cast<uint64_t>(per_cu) * num_cus * (a.oversub > 1 ? a.oversub : 1u);
   const uint64_t need = (a.count + kWavesPerBlock - 1) / kWavesPerBlock;
   if (blocks > need) blocks = need;
   if (blocks == 0) return hipSuccess;
