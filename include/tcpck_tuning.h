@@ -35,18 +35,22 @@ extern "C" {
                                   priority, 9: 4 with v_dot2 sums, 10/12/13:
                                   4/2/8 with v_dot2 sums and buffer loads, 11:
                                   4 with buffer loads) | (blocks per CU cap << 8)
-                                  | (grid oversubscription factor << 16)        */
+                                  | (grid oversubscription << 16: 0 = by batch
+                                  size, 1 = none, M = M x the resident grid)    */
 #define TCPCK_KERNEL_VSTREAM 7 /* fixed stride == len >= 16, MODE_REF: run per
                                   wave, all boundaries of a step resolved by the
                                   lanes in parallel (small images); param =
                                   variant (0: 4 loads in flight, 1: 2, 2: 8)
-                                  | (grid oversubscription factor << 16)        */
+                                  | (grid oversubscription << 16: 0 = by batch
+                                  size, 1 = none, M = M x the resident grid)    */
 #define TCPCK_KERNEL_VVSTREAM 8 /* packed variable layouts, MODE_REF, CHECKSUM /
                                    VERIFY: run per wave, a step's boundaries
                                    resolved in parallel from an LDS ring of
                                    image ends; param = variant (0: 4 loads in
                                    flight, 1: 8; 2/3: same with equal-count
-                                   instead of byte-balanced runs)               */
+                                   instead of byte-balanced runs; 4: policy)
+                                   | (grid oversubscription << 16: 0 = by batch
+                                  size, 1 = none, M = M x the resident grid)    */
 #define TCPCK_KERNEL_RVSTREAM 6 /* packed variable layouts, MODE_REF: byte-balanced
                                    run per wave, scalar walk over the lengths;
                                    param = variant (0: 4 loads in flight, 1: 2,

@@ -254,8 +254,10 @@ hipError_t run_var(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const uint6
       kernel = TCPCK_KERNEL_SEG;
     else if (op == TCPCK_OP_FILL)
       kernel = TCPCK_KERNEL_SPAN;
-    else
+    else {
       kernel = TCPCK_KERNEL_VVSTREAM;
+      param = 4;
+    }
   }
   if (kernel == TCPCK_KERNEL_SPAN) {
     // the kernel re-checks packing and lengths per tile, so a wrong hint
@@ -281,6 +283,7 @@ hipError_t run_var(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const uint6
     a.count = count;
     a.out = out;
     a.oversub = static_cast<uint32_t>(param >> 16) & 0xFFu;
+    a.total_bytes = layout ? layout->total_bytes : 0;
     return tcpck::launch_vvstream(op, param & 0xFF, a, static_cast<uint32_t>(ctx->num_cus), s);
   }
   if (kernel == TCPCK_KERNEL_RVSTREAM) {

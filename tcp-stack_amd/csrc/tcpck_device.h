@@ -24,6 +24,18 @@ inline uint32_t resident_blocks_per_cu(Kernel kernel) {
   return static_cast<uint32_t>(nb);
 }
 
+// Grid oversubscription for the run-per-wave kernels.  With one run per
+// resident wave, the SIMD's age-ordered issue arbitration finishes the oldest
+// slot ~2x before the youngest and the last runs stream alone; launching M x
+// the resident grid lets the dispatcher refill freed slots with fresh, smaller
+// runs (C2: 82% -> 85% of the HBM roof at M = 8, profiles/r01/oversub.log).
+// requested: 0 = by size (runs of >= ~24 KiB, at most max_m), else explicit.
+inline uint32_t oversub_for(uint32_t requested, uint64_t bytes, uint64_t resident_waves, uint32_t max_m) {
+  if (requested) return requested;
+  const uint64_t m = bytes / (resident_waves * (24u << 10) + 1);
+  return static_cast<uint32_t>(m < 1 ? 1 : (m > max_m ? max_m : m));
+}
+
 // Offset (relative to `arena`, wrapping) of the 16-byte-aligned ADDRESS at or
 // below arena + off: loads stay naturally aligned even when the caller's arena
 // pointer is not (the few bytes read before an image are masked, and they lie

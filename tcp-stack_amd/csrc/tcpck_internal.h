@@ -47,7 +47,8 @@ struct SpanArgs {
   uint64_t count;
   void *out;
   uint32_t tile;             // images per wave tile, 1..63
-  uint32_t oversub;          // grid = resident blocks x this (run-stream kernels; 0/1: none)
+  uint32_t oversub;          // grid = resident blocks x this (run-stream kernels; 0 = by size)
+  uint64_t total_bytes;      // batch byte span hint (0 = unknown)
 };
 
 uint32_t span_tile_for_len(uint64_t typical_len);
@@ -71,7 +72,7 @@ struct FixedStreamArgs {
   uint32_t tile;    // images per tile (>= fstream_min_tile)
   uint64_t *dbg;    // optional per-wave {start, end} s_memrealtime stamps (timing builds)
   uint32_t blocks_per_cu;  // optional occupancy cap (0 = as many as fit)
-  uint32_t oversub;        // grid = resident blocks x this (0/1: one wave per resident slot)
+  uint32_t oversub;        // grid = resident blocks x this (0 = by size, 1 = none)
 };
 // ---- run-stream kernel (fixed stride == len): one run per wave, scalar boundaries
 // variant: 0 = 4 loads in flight, 1 = 2, 2 = 8, 3 = 4 with per-wave time stamps
@@ -83,7 +84,8 @@ hipError_t launch_vstream(int op, int variant, const FixedStreamArgs &a, uint32_
 // variant = loads in flight (0: 4, 1: 2, 2: 8) | blocks-per-CU cap << 8
 hipError_t launch_rvstream(int op, int variant, const SpanArgs &a, uint32_t num_cus, hipStream_t stream);
 // ---- vector-boundary run stream for packed variable layouts (tcpck_vvstream.hip),
-// MODE_REF, kChecksum / kVerify: variant 0 U4 byte split, 1 U8, 2 U4 count split, 3 U8
+// MODE_REF, kChecksum / kVerify: variant 0 U4 byte split, 1 U8, 2 U4 count split, 3 U8,
+// 4 = policy (oversubscription and split by size)
 hipError_t launch_vvstream(int op, int variant, const SpanArgs &a, uint32_t num_cus, hipStream_t stream);
 // timing-only streaming micro-kernels (tcpck_diag.hip)
 hipError_t launch_diag_stream(int variant, const uint8_t *buf, uint64_t bytes, uint32_t *out, uint32_t num_cus,

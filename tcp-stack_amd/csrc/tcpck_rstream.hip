@@ -194,7 +194,8 @@ template <int U, int OP, bool STAMP, int PRIO = 0, int FLAV = 0>
 hipError_t launch_one(const FixedStreamArgs &a, uint32_t num_cus, hipStream_t stream) {
   static const uint32_t per_cu = dev::resident_blocks_per_cu(rstream_kernel<U, OP, STAMP, PRIO, FLAV>);
   const uint32_t cap = (a.blocks_per_cu && a.blocks_per_cu < per_cu) ? a.blocks_per_cu : per_cu;
-  uint64_t blocks = static_cast<uint64_t>(cap) * num_cus * (a.oversub > 1 ? a.oversub : 1u);
+  const uint64_t resident = static_cast<uint64_t>(cap) * num_cus;
+  uint64_t blocks = resident * dev::oversub_for(a.oversub, a.count * a.stride, resident * kWavesPerBlock, 8);
   const uint64_t need = (a.count + kWavesPerBlock - 1) / kWavesPerBlock;  // >= 1 image per wave
   if (blocks > need) blocks = need;
   if (blocks == 0) return hipSuccess;

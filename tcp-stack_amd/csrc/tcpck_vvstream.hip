@@ -199,7 +199,8 @@ __global__ void __launch_bounds__(kBlock)
 template <int U, int OP, int SPLIT>
 hipError_t launch_one(const SpanArgs &a, uint32_t num_cus, hipStream_t stream) {
   static const uint32_t per_cu = dev::resident_blocks_per_cu(vvstream_kernel<U, OP, SPLIT>);
-  uint64_t blocks = static_cast<uint64_t>(per_cu) * num_cus * (a.oversub > 1 ? a.oversub : 1u);
+  const uint64_t resident = static_cast<uint64_t>(per_cu) * num_cus;
+  uint64_t blocks = resident * dev::oversub_for(a.oversub, a.total_bytes, resident * kWavesPerBlock, 16);
   const uint64_t need = (a.count + kWavesPerBlock - 1) / kWavesPerBlock;
   if (blocks > need) blocks = need;
   if (blocks == 0) return hipSuccess;
@@ -221,6 +222,14 @@ hipError_t dispatch(int op, const SpanArgs &a, uint32_t num_cus, hipStream_t s) 
 
 hipError_t launch_vvstream(int op, int variant, const SpanArgs &a, uint32_t num_cus, hipStream_t stream) {
   if (a.count == 0) return hipSuccess;
+  if (variant == 4) {
+    // library policy: oversubscribe by size; once the grid is >= 4x the resident
+    // waves the dispatcher balances the runs, and equal-count runs (no offset
+    // searches) win (C3: 80.0% vs 75.5%, profiles/r01/oversub.log)
+    SpanArgs b = a;
+    b.oversub = dev::oversub_for(a.oversub, a.total_bytes, static_cast<uint64_t>(num_cus) * 32, 16);
+    return b.oversub >= 4 ? dispatch<4, 1>(op, b, num_cus, stream) : dispatch<4, 0>(op, b, num_cus, stream);
+  }
   switch (variant) {
     case 0: return dispatch<4, 0>(op, a, num_cus, stream);
     case 1: return dispatch<8, 0>(op, a, num_cus, stream);

@@ -512,3 +512,35 @@ def test_vvstream_not_packed_and_verify(ctx, oracle_c, variant):
     with pytest.raises(tcpck.TcpckError):
         ctx.batch_var_ex(tcpck.OP_FILL, dev(arena_np), dev(off), dev(ln), count, ok, tcpck.KERNEL_VVSTREAM, variant,
                          packed=True)
+
+
+# ---- grid oversubscription (param bits 16..23): more, shorter runs per launch ----
+@pytest.mark.parametrize("kernel,variant,length", [(5, 0, 1492), (5, 10, 1024), (7, 2, 96), (7, 0, 256), (7, 2, 34)])
+@pytest.mark.parametrize("oversub", [2, 8, 32])
+def test_oversubscribed_fixed(ctx, oracle_c, kernel, variant, length, oversub):
+    import tcpck
+    count = (48 << 20) // length
+    rng = np.random.default_rng(length + oversub)
+    arena_np = rng.integers(0, 256, count * length + 128, dtype=np.uint8)
+    buf = dev(arena_np)
+    for mis in (0, 6):
+        out = torch.empty(count, dtype=torch.int16, device="cuda")
+        ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, buf.data_ptr() + mis, length, length, count, out, kernel,
+                           variant | (oversub << 16))
+        exp = oracle_c.batch(arena_np[mis:], stride=length, length=length, count=count, threads=8)
+        np.testing.assert_array_equal(host(out).view(np.uint16), exp)
+
+
+@pytest.mark.parametrize("variant", [0, 2, 4])
+@pytest.mark.parametrize("oversub", [0, 2, 8, 16])
+def test_oversubscribed_vvstream(ctx, oracle_c, variant, oversub):
+    import tcpck
+    import synth_np
+    count = 60000
+    off, ln, total = synth_np.mixed_layout(count, seed=oversub + variant)
+    rng = np.random.default_rng(variant)
+    arena_np = rng.integers(0, 256, total, dtype=np.uint8)
+    out = torch.empty(count, dtype=torch.int16, device="cuda")
+    ctx.batch_var_ex(tcpck.OP_CHECKSUM, dev(arena_np), dev(off), dev(ln), count, out, tcpck.KERNEL_VVSTREAM,
+                     variant | (oversub << 16), packed=True, total_bytes=total)
+    np.testing.assert_array_equal(host(out).view(np.uint16), oracle_c.batch(arena_np, off, ln, threads=8))
