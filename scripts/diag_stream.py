@@ -14,7 +14,9 @@ import tcpck  # noqa: E402
 
 NAMES = {0: "1x16B U4 scan", 1: "1x16B U4 noscan", 2: "2x16B U2 scan", 3: "2x16B U2 noscan",
          4: "4x16B U1 scan", 5: "2x16B U4 scan", 6: "4x16B U2 scan", 7: "1x16B U2 scan",
-         8: "dyn U4 16K units", 9: "dyn U4 32K units", 10: "dyn U4 8K units", 11: "dyn U8 32K units"}
+         8: "dyn U4 16K units", 9: "dyn U4 32K units", 10: "dyn U4 8K units", 11: "dyn U8 32K units",
+         4 << 8: "1x16B U4 scan x4", 8 << 8: "1x16B U4 scan x8", 16 << 8: "1x16B U4 scan x16",
+         32 << 8: "1x16B U4 scan x32"}
 
 
 def main():

@@ -133,9 +133,11 @@ hipError_t launch_dyn(const uint8_t *buf, uint64_t bytes, uint32_t *out, uint32_
 }
 
 template <int LPB, int U, bool SCAN>
-hipError_t launch_one(const uint8_t *buf, uint64_t bytes, uint32_t *out, uint32_t num_cus, hipStream_t s) {
+hipError_t launch_one(const uint8_t *buf, uint64_t bytes, uint32_t *out, uint32_t num_cus, hipStream_t s,
+                      uint32_t oversub = 1) {
   static const uint32_t per_cu = dev::resident_blocks_per_cu(diag_stream_kernel<LPB, U, SCAN>);
-  hipLaunchKernelGGL((diag_stream_kernel<LPB, U, SCAN>), dim3(per_cu * num_cus), dim3(kBlock), 0, s, buf, bytes, out);
+  hipLaunchKernelGGL((diag_stream_kernel<LPB, U, SCAN>), dim3(per_cu * num_cus * (oversub ? oversub : 1)),
+                     dim3(kBlock), 0, s, buf, bytes, out);
   return hipGetLastError();
 }
 
@@ -147,6 +149,8 @@ hipError_t launch_one(const uint8_t *buf, uint64_t bytes, uint32_t *out, uint32_
 // 10 = U4 8 KiB, 11 = U8 32 KiB
 hipError_t launch_diag_stream(int variant, const uint8_t *buf, uint64_t bytes, uint32_t *out, uint32_t num_cus,
                               hipStream_t s) {
+  if (variant >> 8)  // 1x16 B, U4, scan, grid = (variant >> 8) x resident
+    return launch_one<1, 4, true>(buf, bytes, out, num_cus, s, static_cast<uint32_t>(variant >> 8) & 0xFFu);
   switch (variant) {
     case 0: return launch_one<1, 4, true>(buf, bytes, out, num_cus, s);
     case 1: return launch_one<1, 4, false>(buf, bytes, out, num_cus, s);
