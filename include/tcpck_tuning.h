@@ -48,7 +48,9 @@ extern "C" {
                                    resolved in parallel from an LDS ring of
                                    image ends; param = variant (0: 4 loads in
                                    flight, 1: 8; 2/3: same with equal-count
-                                   instead of byte-balanced runs; 4: policy)
+                                   instead of byte-balanced runs; 5-8: 0-3
+                                   with the prefix-table resolution, any
+                                   image lengths; 4/9: policy)
                                    | (grid oversubscription << 16: 0 = by batch
                                   size, 1 = none, M = M x the resident grid)    */
 #define TCPCK_KERNEL_RVSTREAM 6 /* packed variable layouts, MODE_REF: byte-balanced

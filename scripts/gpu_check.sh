@@ -34,12 +34,21 @@ for s in ${STEPS:-tests smoke bench prof}; do
     bench_c4) step bench_c4 600 python bench.py --config c4 --no-cpu-baseline ;;
     mrank) step mrank 600 env TCPCK_BENCH_BACKEND=gloo TCPCK_BENCH_DEVICE=0 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29561 bench.py --gpus 2 --steps 5 --warmup 2 &&
       step mrank_c5 600 env TCPCK_BENCH_BACKEND=gloo TCPCK_BENCH_DEVICE=0 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29562 bench.py --gpus 2 --config c5 --steps 5 --warmup 2 ;;
+    vvprobe) step vvprobe 600 python scripts/vv_probe.py ;;
+    vvtests) step vvtests 600 python -u -m pytest tests/test_gpu_kernels.py -x -q --timeout 120 --timeout-method thread -k vvstream ;;
+    b2b_c3) step b2b_c3 600 python scripts/b2b_probe.py --what c3 ;;
+    b2b_c2) step b2b_c2 600 python scripts/b2b_probe.py --what c2 ;;
+    tr_c3) step tr_c3 300 python scripts/transient.py --what c3 ;;
+    tr_c2) step tr_c2 300 python scripts/transient.py --what c2 --n 800 ;;
     oversub) step oversub 600 python scripts/oversub.py ;;
+    os_c2) step os_c2 600 python scripts/oversub.py --what c2 --variants 0,9,10 --ms 8,16,24,32,40,48 ;;
+    os_c3) step os_c3 600 python scripts/oversub.py --what c3 --variants 2,7,8 --ms 16,24,28,32,40 ;;
     prof_c3) step prof_c3 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c3 -o run --output-format csv -- python3 bench.py --config c3 --steps 10 --warmup 2 --no-cpu-baseline --no-e2e ;;
+    prof_c4) step prof_c4 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c4 -o run --output-format csv -- python3 bench.py --config c4 --steps 10 --warmup 2 --no-cpu-baseline --no-e2e ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-e2e ;;
     pmc_c2|pmc_c3|pmc_c4)  # separate FETCH_SIZE / WRITE_SIZE passes (TCC slots), kernel trace only
       c=${s#pmc_}
-      step ${s}_fetch 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d gpurun_out/pmc_${c}_fetch -o run --output-format csv -- python3 bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline --no-e2e
-      step ${s}_write 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d gpurun_out/pmc_${c}_write -o run --output-format csv -- python3 bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline --no-e2e ;;
+      step ${s}_fetch 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d gpurun_out/pmc_${c}_fetch -o run --output-format csv -- python3 bench.py --config $c --steps 3 --warmup 1 --settle-ms 0 --no-cpu-baseline --no-e2e
+      step ${s}_write 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d gpurun_out/pmc_${c}_write -o run --output-format csv -- python3 bench.py --config $c --steps 3 --warmup 1 --settle-ms 0 --no-cpu-baseline --no-e2e ;;
   esac
 done

@@ -164,7 +164,7 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
   // profiles/r01/policy_fixed.log): below 768 B boundaries are dense enough that
   // resolving all of a step's boundaries in parallel (vstream, 8 loads in
   // flight) wins; from 768 B the run-stream kernel's scalar boundary walk
-  // (82.6% of the HBM roof on C2); jumbo images stay on seg (G64/U4), which
+  // (~88% of the HBM roof on C2 at 32x oversubscription); jumbo images stay on seg (G64/U4), which
   // streams whole images per wave at the same rate
   if (kernel == TCPCK_KERNEL_AUTO) {
     if (!span_ok || len > kSpanMaxLen) {
@@ -174,6 +174,7 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
       param = 2;
     } else {
       kernel = TCPCK_KERNEL_RSTREAM;
+      param = 10;  // v_dot2 chunk sums, buffer loads (C2 +0.5%, profiles/r01/b2b_c2c3.log)
     }
   }
   if (kernel == TCPCK_KERNEL_SPAN) {
@@ -245,15 +246,15 @@ hipError_t run_var(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const uint6
                    uint64_t base, uint64_t count, void *out, const tcpck_layout *layout, int kernel, int param,
                    hipStream_t s) {
   const uint64_t typical = (layout && layout->total_bytes) ? layout->total_bytes / count : 1500;
-  const bool span_ok = mode == TCPCK_MODE_REF && layout && (layout->flags & TCPCK_LAYOUT_PACKED) &&
-                       (layout->min_len == 0 || layout->min_len >= 16);
-  // packed, reference mode: checksum / verify on vvstream (C3 78.5%, 96-B images
-  // 74% vs span's 37%: profiles/r01/rv_probe.log, policy_mix.log); fill on span
+  const bool packed = mode == TCPCK_MODE_REF && layout && (layout->flags & TCPCK_LAYOUT_PACKED);
+  // packed, reference mode: checksum / verify on vvstream (any image lengths;
+  // C3 85% at 32x oversubscription, profiles/r01/oversub_c2c3.log); fill on
+  // span, whose one-end-per-chunk hand-off needs images >= 16 B
   if (kernel == TCPCK_KERNEL_AUTO) {
-    if (!span_ok || typical > kSpanMaxLen)
+    if (!packed || typical > kSpanMaxLen)
       kernel = TCPCK_KERNEL_SEG;
     else if (op == TCPCK_OP_FILL)
-      kernel = TCPCK_KERNEL_SPAN;
+      kernel = (layout->min_len == 0 || layout->min_len >= 16) ? TCPCK_KERNEL_SPAN : TCPCK_KERNEL_SEG;
     else {
       kernel = TCPCK_KERNEL_VVSTREAM;
       param = 4;

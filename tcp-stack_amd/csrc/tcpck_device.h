@@ -28,12 +28,17 @@ inline uint32_t resident_blocks_per_cu(Kernel kernel) {
 // resident wave, the SIMD's age-ordered issue arbitration finishes the oldest
 // slot ~2x before the youngest and the last runs stream alone; launching M x
 // the resident grid lets the dispatcher refill freed slots with fresh, smaller
-// runs (C2: 82% -> 85% of the HBM roof at M = 8, profiles/r01/oversub.log).
-// requested: 0 = by size (runs of >= ~24 KiB, at most max_m), else explicit.
-inline uint32_t oversub_for(uint32_t requested, uint64_t bytes, uint64_t resident_waves, uint32_t max_m) {
+// runs.  requested: 0 = by size -- the largest power of two <= max_m that keeps
+// runs >= min_run bytes (M = 12/16/24/40 measured 1-4% below M = 8/32 on the
+// run kernels; C2 rstream 82.8% at M = 7, 87.9% at M = 32 back to back,
+// profiles/r01/oversub_c2c3.log, b2b_c2c3.log) -- else explicit.
+inline uint32_t oversub_for(uint32_t requested, uint64_t bytes, uint64_t resident_waves, uint32_t max_m,
+                            uint32_t min_run = 4u << 10) {
   if (requested) return requested;
-  const uint64_t m = bytes / (resident_waves * (24u << 10) + 1);
-  return static_cast<uint32_t>(m < 1 ? 1 : (m > max_m ? max_m : m));
+  const uint64_t q = bytes / (resident_waves * min_run + 1);
+  uint32_t m = 1;
+  while (2 * m <= max_m && 2 * m <= q) m *= 2;
+  return m;
 }
 
 // Offset (relative to `arena`, wrapping) of the 16-byte-aligned ADDRESS at or
@@ -291,6 +296,13 @@ __device__ __forceinline__ void find_two(const uint64_t *offsets, uint64_t base,
   const bool b1 = lo[1] + lane < hi[1] && v[1] - base < t1;
   r0 = lo[0] + __popcll(__ballot(b0));
   r1 = lo[1] + __popcll(__ballot(b1));
+}
+
+// Equal-count run split without a device division: count = q * waves + r,
+// wave w owns [w q + min(w, r), +q + (w < r)); q and r come from the launcher.
+__device__ __forceinline__ void count_split(uint64_t wid, uint64_t q, uint64_t r, uint64_t &kb, uint64_t &ke) {
+  kb = wid * q + (wid < r ? wid : r);
+  ke = kb + q + (wid < r ? 1u : 0u);
 }
 
 // SPLIT 0: byte-balanced runs (two 64-ary searches over the offsets);

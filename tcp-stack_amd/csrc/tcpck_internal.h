@@ -73,6 +73,8 @@ struct FixedStreamArgs {
   uint64_t *dbg;    // optional per-wave {start, end} s_memrealtime stamps (timing builds)
   uint32_t blocks_per_cu;  // optional occupancy cap (0 = as many as fit)
   uint32_t oversub;        // grid = resident blocks x this (0 = by size, 1 = none)
+  uint64_t per_wave;       // run split, set by the launcher: count = per_wave * waves + rem,
+  uint64_t rem;            // wave w owns per_wave + (w < rem) images (no 64-bit division on device)
 };
 // ---- run-stream kernel (fixed stride == len): one run per wave, scalar boundaries
 // variant: 0 = 4 loads in flight, 1 = 2, 2 = 8, 3 = 4 with per-wave time stamps
@@ -85,7 +87,8 @@ hipError_t launch_vstream(int op, int variant, const FixedStreamArgs &a, uint32_
 hipError_t launch_rvstream(int op, int variant, const SpanArgs &a, uint32_t num_cus, hipStream_t stream);
 // ---- vector-boundary run stream for packed variable layouts (tcpck_vvstream.hip),
 // MODE_REF, kChecksum / kVerify: variant 0 U4 byte split, 1 U8, 2 U4 count split, 3 U8,
-// 4 = policy (oversubscription and split by size)
+// 5-8 = 0-3 with prefix-table boundary resolution, 4 (= 9) = policy (oversubscription,
+// split and loads in flight by size; prefix table)
 hipError_t launch_vvstream(int op, int variant, const SpanArgs &a, uint32_t num_cus, hipStream_t stream);
 // timing-only streaming micro-kernels (tcpck_diag.hip)
 hipError_t launch_diag_stream(int variant, const uint8_t *buf, uint64_t bytes, uint32_t *out, uint32_t num_cus,

@@ -7,7 +7,8 @@
 // fixed stride S, so sum(k) = P((k+1)S) - P(kS) (mod 2^16) where P(x) is the
 // word sum of the wave's run before byte x: the run is read as one flat stream.
 //
-//   * wave w owns images [w N / W, (w+1) N / W): one contiguous run per wave
+//   * wave w owns an equal share of the images (dev::count_split; the split is
+//     computed by the launcher, no device division): one contiguous run per wave
 //     (measured faster than interleaved tiles on this part), its start rounded
 //     down to a 128-B line so that every 1 KiB step covers exactly eight whole
 //     lines;
@@ -45,7 +46,6 @@ using dev::u32x4;
 template <int U, int OP, bool STAMP, int PRIO = 0, int FLAV = 0>
 __global__ void __launch_bounds__(kBlock) rstream_kernel(FixedStreamArgs a) {
   const uint32_t lane = threadIdx.x & 63;
-  const uint64_t W = static_cast<uint64_t>(gridDim.x) * kWavesPerBlock;
   // readfirstlane: the wave index is uniform, but hipcc cannot prove anything
   // derived from threadIdx is; without it every boundary variable below lives
   // in VGPRs and each uniform test becomes an exec-masked region
@@ -69,9 +69,8 @@ __global__ void __launch_bounds__(kBlock) rstream_kernel(FixedStreamArgs a) {
       __builtin_amdgcn_s_setprio(1);
     }
   }
-  const uint64_t N = a.count;
-  const uint64_t kb = wid * N / W;
-  const uint64_t ke = (wid + 1) * N / W;
+  uint64_t kb, ke;
+  dev::count_split(wid, a.per_wave, a.rem, kb, ke);
   if (kb >= ke) return;
   const uint32_t S = static_cast<uint32_t>(a.stride);
   const uint64_t s0 = kb * S;
@@ -195,12 +194,15 @@ hipError_t launch_one(const FixedStreamArgs &a, uint32_t num_cus, hipStream_t st
   static const uint32_t per_cu = dev::resident_blocks_per_cu(rstream_kernel<U, OP, STAMP, PRIO, FLAV>);
   const uint32_t cap = (a.blocks_per_cu && a.blocks_per_cu < per_cu) ? a.blocks_per_cu : per_cu;
   const uint64_t resident = static_cast<uint64_t>(cap) * num_cus;
-  uint64_t blocks = resident * dev::oversub_for(a.oversub, a.count * a.stride, resident * kWavesPerBlock, 8);
+  uint64_t blocks = resident * dev::oversub_for(a.oversub, a.count * a.stride, resident * kWavesPerBlock, 32);
   const uint64_t need = (a.count + kWavesPerBlock - 1) / kWavesPerBlock;  // >= 1 image per wave
   if (blocks > need) blocks = need;
   if (blocks == 0) return hipSuccess;
+  FixedStreamArgs b = a;
+  b.per_wave = a.count / (blocks * kWavesPerBlock);
+  b.rem = a.count % (blocks * kWavesPerBlock);
   hipLaunchKernelGGL((rstream_kernel<U, OP, STAMP, PRIO, FLAV>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0,
-                     stream, a);
+                     stream, b);
   return hipGetLastError();
 }
 

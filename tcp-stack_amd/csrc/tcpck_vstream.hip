@@ -43,12 +43,10 @@ __device__ __forceinline__ uint32_t lane_bpermute(uint32_t v, uint32_t src_lane)
 template <int U, int OP>
 __global__ void __launch_bounds__(kBlock) vstream_kernel(FixedStreamArgs a) {
   const uint32_t lane = threadIdx.x & 63;
-  const uint64_t W = static_cast<uint64_t>(gridDim.x) * kWavesPerBlock;
   const uint64_t wid = static_cast<uint64_t>(blockIdx.x) * kWavesPerBlock +
                        static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6)));
-  const uint64_t N = a.count;
-  const uint64_t kb = wid * N / W;
-  const uint64_t ke = (wid + 1) * N / W;
+  uint64_t kb, ke;
+  dev::count_split(wid, a.per_wave, a.rem, kb, ke);
   if (kb >= ke) return;
   const uint32_t S = static_cast<uint32_t>(a.stride);
   const uint64_t s0 = kb * S;
@@ -164,11 +162,14 @@ hipError_t launch_one(const FixedStreamArgs &a, uint32_t num_cus, hipStream_t st
   static const uint32_t per_cu = dev::resident_blocks_per_cu(vstream_kernel<U, OP>);
   const uint32_t cap = (a.blocks_per_cu && a.blocks_per_cu < per_cu) ? a.blocks_per_cu : per_cu;
   const uint64_t resident = static_cast<uint64_t>(cap) * num_cus;
-  uint64_t blocks = resident * dev::oversub_for(a.oversub, a.count * a.stride, resident * kWavesPerBlock, 8);
+  uint64_t blocks = resident * dev::oversub_for(a.oversub, a.count * a.stride, resident * kWavesPerBlock, 32);
   const uint64_t need = (a.count + kWavesPerBlock - 1) / kWavesPerBlock;
   if (blocks > need) blocks = need;
   if (blocks == 0) return hipSuccess;
-  hipLaunchKernelGGL((vstream_kernel<U, OP>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0, stream, a);
+  FixedStreamArgs b = a;
+  b.per_wave = a.count / (blocks * kWavesPerBlock);
+  b.rem = a.count % (blocks * kWavesPerBlock);
+  hipLaunchKernelGGL((vstream_kernel<U, OP>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0, stream, b);
   return hipGetLastError();
 }
 

@@ -41,12 +41,25 @@ __device__ __forceinline__ uint32_t lane_bpermute(uint32_t v, uint32_t src_lane)
   return static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(static_cast<int>(src_lane << 2), static_cast<int>(v)));
 }
 
-template <int U, int OP, int SPLIT>
+// RES: how a step's boundaries are resolved.
+//   0: slot hand-off -- the lane holding an end posts it to the LDS slot of the
+//      chunk's lane, which forms P from its own v_dot2 partial sums; the
+//      boundary lane pulls P back (ds_bpermute).  One end per chunk at most:
+//      images < 16 B fall back to per-image sums.
+//   1: prefix table -- every lane writes the run prefix P at each of its
+//      chunk's 8 word positions as packed u16s (one ds_write_b128: P matters
+//      mod 2^16 only), the boundary lane reads the u16 at its end's byte offset
+//      in the step (the table is laid out like the step).  Any number of ends
+//      per chunk (a step with more than 64 ends loops), 3 LDS ops per step
+//      instead of 7, no cross-lane selects.
+template <int U, int OP, int SPLIT, int RES = 0>
 __global__ void __launch_bounds__(kBlock)
     vvstream_kernel(uint8_t *__restrict__ arena, const uint64_t *__restrict__ offsets,
-                    const uint32_t *__restrict__ lengths, uint64_t base, uint64_t count, void *__restrict__ out) {
+                    const uint32_t *__restrict__ lengths, uint64_t base, uint64_t count, void *__restrict__ out,
+                    uint64_t per_wave, uint64_t rem) {
   __shared__ uint32_t s_end[kWavesPerBlock][kRing];
-  __shared__ uint32_t s_slot[kWavesPerBlock][64];  // end offset in chunk + 1, posted to the chunk's lane
+  __shared__ uint32_t s_slot[kWavesPerBlock][RES == 0 ? 64 : 1];  // end offset in chunk + 1, posted to the chunk's lane
+  __shared__ __attribute__((aligned(16))) uint32_t s_pre[kWavesPerBlock][RES == 1 ? 256 : 1];  // packed u16 prefixes
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wv = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6)));
   const uint64_t W = static_cast<uint64_t>(gridDim.x) * kWavesPerBlock;
@@ -54,8 +67,7 @@ __global__ void __launch_bounds__(kBlock)
   const uint64_t N = count;
   uint64_t kb, ke;
   if (SPLIT == 1) {
-    kb = wid * N / W;
-    ke = (wid + 1) * N / W;
+    dev::count_split(wid, per_wave, rem, kb, ke);
   } else {
     const uint64_t first = offsets[0] - base;
     const uint64_t total = offsets[N - 1] - base + lengths[N - 1] - first;
@@ -89,8 +101,12 @@ __global__ void __launch_bounds__(kBlock)
     auto load_step = [&](uint32_t st) -> u32x4 { return dev::load16_buf_nt(rsrc, lane << 4, st << 10); };
     uint32_t *ring_end = s_end[wv];
     uint32_t *slot = s_slot[wv];
-    slot[lane] = 0;
-    __builtin_amdgcn_wave_barrier();
+    if constexpr (RES == 0) {
+      slot[lane] = 0;
+      __builtin_amdgcn_wave_barrier();
+    }
+    u32x4 *pre4 = reinterpret_cast<u32x4 *>(s_pre[wv]);
+    const uint16_t *pre16 = reinterpret_cast<const uint16_t *>(s_pre[wv]);
 
     // descriptor rounds: lengths of run images [256 r, 256 r + 256), 4 per lane
     const uint32_t *lens = lengths + kb;
@@ -117,7 +133,7 @@ __global__ void __launch_bounds__(kBlock)
       bool sh = false;
 #pragma unroll
       for (int i = 0; i < 4; ++i) sh |= (jb + i < nimg) && d[i] < 16;
-      short_img |= __ballot(sh) != 0;
+      if (RES == 0) short_img |= __ballot(sh) != 0;
       const uint32_t si = (r * kRound) % kRing + 4 * lane;
       ring_end[si] = ex + e1;
       ring_end[si + 1] = ex + e2;
@@ -127,12 +143,13 @@ __global__ void __launch_bounds__(kBlock)
       loaded += kRound;
       __builtin_amdgcn_wave_barrier();  // ends are read by other lanes
     };
-    fill_round();
-
     uint32_t carry = 0, p_last = 0, jn = 0;
     u32x4 ring[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) ring[u] = load_step(static_cast<uint32_t>(u));
+    // the first ends after the data loads: the lengths' latency overlaps the
+    // stream's instead of preceding it (straight-line code: vmcnt(U), no drain)
+    fill_round();
 
     for (uint32_t g = 0; g < nsteps && !short_img; g += U) {
 #pragma unroll
@@ -146,45 +163,87 @@ __global__ void __launch_bounds__(kBlock)
           const int32_t hi = min(max(static_cast<int32_t>(span) - static_cast<int32_t>(c), 0), 16);
           w = dev::apply_mask(w, dev::word_mask(lo, hi));
         }
+        uint32_t j = jn + lane;
+        uint32_t e = ~0u;
+        if constexpr (RES == 1) {  // the step's first ends, read before the sums (LDS latency overlaps)
+          if (jn + 64 > loaded && loaded < nimg) fill_round();  // keep >= 64 ends ahead
+          j = jn + lane;
+          e = j < nimg ? ring_end[j % kRing] : ~0u;
+        }
         const uint32_t q1 = dev::dot2_u16(w.x, 0u);
         const uint32_t q2 = dev::dot2_u16(w.y, q1);
         const uint32_t q3 = dev::dot2_u16(w.z, q2);
         const uint32_t tot = dev::dot2_u16(w.w, q3);
         const uint32_t incl = dev::wave_inclusive_scan(tot);
-        if (jn + 64 > loaded && loaded < nimg) fill_round();  // keep >= 64 ends ahead
-        const uint32_t j = jn + lane;
-        const uint32_t e = j < nimg ? ring_end[j % kRing] : ~0u;
-        const bool inb = e < sb + 1024;
-        const uint64_t bal = __ballot(inb);
-        if (bal) {
-          const uint32_t cnt = static_cast<uint32_t>(__popcll(bal));  // lanes 0..cnt-1 (ends ascend)
-          const uint32_t rel = e - sb;
-          const uint32_t cl = rel >> 4;
-          if (inb) slot[cl] = (rel & 15u) + 1u;  // tell the chunk's lane where the end lies
-          __builtin_amdgcn_wave_barrier();        // cross-lane LDS hand-off: no per-lane forwarding
-          const uint32_t rr = slot[lane];
-          if (rr) slot[lane] = 0u;
-          __builtin_amdgcn_wave_barrier();
-          const uint32_t r = rr ? rr - 1 : 0u;
-          const uint32_t di = r >> 2;
-          const uint32_t qd = di == 0 ? 0u : (di == 1 ? q1 : (di == 2 ? q2 : q3));
-          const uint32_t dw = di == 0 ? w.x : (di == 1 ? w.y : (di == 2 ? w.z : w.w));
-          const uint32_t pb = carry + incl - tot + qd + ((r & 2u) ? (dw & 0xFFFFu) : 0u);
-          const uint32_t pj = lane_bpermute(pb, inb ? cl : 0u);
-          const uint32_t pl = lane_bpermute(pj, lane ? lane - 1 : 0u);
-          const uint32_t pprev = lane == 0 ? p_last : pl;
-          if (inb) store(kb + j, pj - pprev);
-          p_last = dev::read_lane(pj, cnt - 1);
-          jn += cnt;
+        if constexpr (RES == 1) {
+          bool table = false;
+          for (;;) {  // once per step unless it holds more than 64 ends
+            const bool inb = e < sb + 1024;
+            const uint64_t bal = __ballot(inb);
+            if (!bal) break;
+            if (!table) {
+              // P at the chunk start, then at word positions 2i (P = a + q_i)
+              // and 2i + 1 (+ low word of dword i), packed low/high per dword
+              const uint32_t a = carry + incl - tot;
+              const uint32_t b1 = a + q1, b2 = a + q2, b3 = a + q3;
+              pre4[lane] = u32x4{__builtin_amdgcn_perm(a + w.x, a, 0x05040100u),
+                                 __builtin_amdgcn_perm(b1 + w.y, b1, 0x05040100u),
+                                 __builtin_amdgcn_perm(b2 + w.z, b2, 0x05040100u),
+                                 __builtin_amdgcn_perm(b3 + w.w, b3, 0x05040100u)};
+              __builtin_amdgcn_wave_barrier();  // cross-lane LDS reads below
+              table = true;
+            }
+            const uint32_t cnt = static_cast<uint32_t>(__popcll(bal));  // lanes 0..cnt-1 (ends ascend)
+            const uint32_t P = pre16[inb ? ((e - sb) >> 1) : 0u];     // the table is laid out like the step
+            const uint32_t pl = static_cast<uint32_t>(
+                __builtin_amdgcn_update_dpp(static_cast<int>(p_last), static_cast<int>(P), 0x138, 0xF, 0xF, false));
+            const uint32_t pprev = lane == 0 ? p_last : pl;  // wave_shr:1
+            if (inb) store(kb + j, P - pprev);
+            p_last = dev::read_lane(P, cnt - 1);
+            jn += cnt;
+            if (cnt < 64) break;
+            if (jn + 64 > loaded && loaded < nimg) fill_round();
+            j = jn + lane;
+            e = j < nimg ? ring_end[j % kRing] : ~0u;
+          }
+          __builtin_amdgcn_wave_barrier();  // the next step rewrites the table
+        } else {
+          if (jn + 64 > loaded && loaded < nimg) fill_round();  // keep >= 64 ends ahead
+          j = jn + lane;
+          e = j < nimg ? ring_end[j % kRing] : ~0u;
+          const bool inb = e < sb + 1024;
+          const uint64_t bal = __ballot(inb);
+          if (bal) {
+            const uint32_t cnt = static_cast<uint32_t>(__popcll(bal));  // lanes 0..cnt-1 (ends ascend)
+            const uint32_t rel = e - sb;
+            const uint32_t cl = rel >> 4;
+            if (inb) slot[cl] = (rel & 15u) + 1u;  // tell the chunk's lane where the end lies
+            __builtin_amdgcn_wave_barrier();        // cross-lane LDS hand-off: no per-lane forwarding
+            const uint32_t rr = slot[lane];
+            if (rr) slot[lane] = 0u;
+            __builtin_amdgcn_wave_barrier();
+            const uint32_t r = rr ? rr - 1 : 0u;
+            const uint32_t di = r >> 2;
+            const uint32_t qd = di == 0 ? 0u : (di == 1 ? q1 : (di == 2 ? q2 : q3));
+            const uint32_t dw = di == 0 ? w.x : (di == 1 ? w.y : (di == 2 ? w.z : w.w));
+            const uint32_t pb = carry + incl - tot + qd + ((r & 2u) ? (dw & 0xFFFFu) : 0u);
+            const uint32_t pj = lane_bpermute(pb, inb ? cl : 0u);
+            const uint32_t pl = lane_bpermute(pj, lane ? lane - 1 : 0u);
+            const uint32_t pprev = lane == 0 ? p_last : pl;
+            if (inb) store(kb + j, pj - pprev);
+            p_last = dev::read_lane(pj, cnt - 1);
+            jn += cnt;
+          }
         }
         carry += dev::read_lane(incl, 63);
         ring[u] = load_step(st + U);
       }
     }
     bad = short_img || pos != span || loaded < nimg;
-    if (!bad && jn < nimg) {  // the last end sits exactly at the last step's end
-      if (lane == 0) store(kb + jn, carry - p_last);
-      jn += 1;
+    if (!bad && jn < nimg) {  // ends exactly at the last step's end (= span): the first gets the rest
+      const uint32_t rem = nimg - jn;
+      for (uint32_t i = lane; i < rem; i += 64) store(kb + jn + i, i == 0 ? carry - p_last : 0u);
+      jn = nimg;
     }
     bad = bad || jn != nimg;
   }
@@ -196,24 +255,25 @@ __global__ void __launch_bounds__(kBlock)
   }
 }
 
-template <int U, int OP, int SPLIT>
+template <int U, int OP, int SPLIT, int RES>
 hipError_t launch_one(const SpanArgs &a, uint32_t num_cus, hipStream_t stream) {
-  static const uint32_t per_cu = dev::resident_blocks_per_cu(vvstream_kernel<U, OP, SPLIT>);
+  static const uint32_t per_cu = dev::resident_blocks_per_cu(vvstream_kernel<U, OP, SPLIT, RES>);
   const uint64_t resident = static_cast<uint64_t>(per_cu) * num_cus;
-  uint64_t blocks = resident * dev::oversub_for(a.oversub, a.total_bytes, resident * kWavesPerBlock, 16);
+  uint64_t blocks = resident * dev::oversub_for(a.oversub, a.total_bytes, resident * kWavesPerBlock, 32, 8u << 10);
   const uint64_t need = (a.count + kWavesPerBlock - 1) / kWavesPerBlock;
   if (blocks > need) blocks = need;
   if (blocks == 0) return hipSuccess;
-  hipLaunchKernelGGL((vvstream_kernel<U, OP, SPLIT>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0, stream,
-                     a.arena, a.offsets, a.lengths, a.base, a.count, a.out);
+  hipLaunchKernelGGL((vvstream_kernel<U, OP, SPLIT, RES>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0, stream,
+                     a.arena, a.offsets, a.lengths, a.base, a.count, a.out, a.count / (blocks * kWavesPerBlock),
+                     a.count % (blocks * kWavesPerBlock));
   return hipGetLastError();
 }
 
-template <int U, int SPLIT>
+template <int U, int SPLIT, int RES = 0>
 hipError_t dispatch(int op, const SpanArgs &a, uint32_t num_cus, hipStream_t s) {
   switch (op) {
-    case kChecksum: return launch_one<U, kChecksum, SPLIT>(a, num_cus, s);
-    case kVerify: return launch_one<U, kVerify, SPLIT>(a, num_cus, s);
+    case kChecksum: return launch_one<U, kChecksum, SPLIT, RES>(a, num_cus, s);
+    case kVerify: return launch_one<U, kVerify, SPLIT, RES>(a, num_cus, s);
     default: return hipErrorInvalidValue;  // kFill: span kernel
   }
 }
@@ -222,19 +282,33 @@ hipError_t dispatch(int op, const SpanArgs &a, uint32_t num_cus, hipStream_t s) 
 
 hipError_t launch_vvstream(int op, int variant, const SpanArgs &a, uint32_t num_cus, hipStream_t stream) {
   if (a.count == 0) return hipSuccess;
-  if (variant == 4) {
-    // library policy: oversubscribe by size; once the grid is >= 4x the resident
-    // waves the dispatcher balances the runs, and equal-count runs (no offset
-    // searches) win (C3: 80.0% vs 75.5%, profiles/r01/oversub.log)
+  if (variant == 4 || variant == 9) {
+    // library policy (prefix-table resolution): oversubscribe by size, runs of
+    // >= 8 KiB, M a power of two <= 32 (M = 16/24/40 measured 2-4% below 32 on
+    // both run kernels, profiles/r01/oversub_c2c3.log).  At M = 32, U8 (C3
+    // 85.0-86.3% vs U4 82.7-84.2%); once M >= 4 the dispatcher balances the runs
+    // and equal-count runs (no offset searches) win.
     SpanArgs b = a;
-    b.oversub = dev::oversub_for(a.oversub, a.total_bytes, static_cast<uint64_t>(num_cus) * 32, 16);
-    return b.oversub >= 4 ? dispatch<4, 1>(op, b, num_cus, stream) : dispatch<4, 0>(op, b, num_cus, stream);
+    uint32_t m = a.oversub;
+    if (m == 0) {
+      const uint64_t per = static_cast<uint64_t>(num_cus) * 32 * (8u << 10);
+      const uint64_t q = a.total_bytes / per;
+      m = 1;
+      while (m < 32 && 2 * m <= q) m *= 2;
+    }
+    b.oversub = m;
+    if (m >= 32) return dispatch<8, 1, 1>(op, b, num_cus, stream);
+    return m >= 4 ? dispatch<4, 1, 1>(op, b, num_cus, stream) : dispatch<4, 0, 1>(op, b, num_cus, stream);
   }
   switch (variant) {
     case 0: return dispatch<4, 0>(op, a, num_cus, stream);
     case 1: return dispatch<8, 0>(op, a, num_cus, stream);
     case 2: return dispatch<4, 1>(op, a, num_cus, stream);
     case 3: return dispatch<8, 1>(op, a, num_cus, stream);
+    case 5: return dispatch<4, 0, 1>(op, a, num_cus, stream);
+    case 6: return dispatch<8, 0, 1>(op, a, num_cus, stream);
+    case 7: return dispatch<4, 1, 1>(op, a, num_cus, stream);
+    case 8: return dispatch<8, 1, 1>(op, a, num_cus, stream);
     default: return hipErrorInvalidValue;
   }
 }

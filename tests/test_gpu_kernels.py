@@ -456,7 +456,7 @@ def test_vstream_fill_verify(ctx, variant, length):
 
 
 # ---- vector-boundary run stream for packed variable layouts (KERNEL_VVSTREAM = 8) ----
-VVSTREAM = [0, 1, 2, 3]
+VVSTREAM = [0, 1, 2, 3, 5, 6, 7, 8]  # 5..8: prefix-table resolution (any lengths, > 64 ends per step)
 
 
 @pytest.mark.parametrize("variant", VVSTREAM)
@@ -531,7 +531,36 @@ def test_oversubscribed_fixed(ctx, oracle_c, kernel, variant, length, oversub):
         np.testing.assert_array_equal(host(out).view(np.uint16), exp)
 
 
-@pytest.mark.parametrize("variant", [0, 2, 4])
+@pytest.mark.parametrize("variant", [5, 7])
+@pytest.mark.parametrize("payloads", [(-30, -28, -20), (-32, -30), (-32, -2, 1460), (-30, 64, 9000)])
+@pytest.mark.parametrize("count", [1, 65, 257, 5000, 70001])
+def test_vvstream_table_tiny_images(ctx, oracle_c, variant, payloads, count):
+    """Prefix-table variants: 0..14-B images (up to 512 ends per 1 KiB step),
+    several ends per 16-B chunk, zero-length runs at the batch end."""
+    import tcpck
+    off, ln, total = packed_layout(count, count * 7 + len(payloads), payloads)
+    rng = np.random.default_rng(count + variant)
+    arena_np = rng.integers(0, 256, total + 128, dtype=np.uint8)
+    buf = dev(arena_np)
+    d_off, d_ln = dev(off), dev(ln)
+    for mis in (0, 2, 126):
+        for oversub in (1, 8):
+            out = torch.empty(count, dtype=torch.int16, device="cuda")
+            ctx.batch_var_ex(tcpck.OP_CHECKSUM, buf.data_ptr() + mis, d_off, d_ln, count, out,
+                             tcpck.KERNEL_VVSTREAM, variant | (oversub << 16), packed=True)
+            np.testing.assert_array_equal(host(out).view(np.uint16), oracle_c.batch(arena_np[mis:], off, ln, threads=8))
+    # trailing empty images end exactly at the run end
+    ln2 = ln.copy()
+    ln2[-3:] = 0
+    off2 = np.zeros(count, np.uint64)
+    if count > 1:
+        off2[1:] = np.cumsum(ln2[:-1].astype(np.uint64))
+    out = torch.empty(count, dtype=torch.int16, device="cuda")
+    ctx.batch_var_ex(tcpck.OP_CHECKSUM, buf, dev(off2), dev(ln2), count, out, tcpck.KERNEL_VVSTREAM, variant, packed=True)
+    np.testing.assert_array_equal(host(out).view(np.uint16), oracle_c.batch(arena_np, off2, ln2, threads=8))
+
+
+@pytest.mark.parametrize("variant", [0, 2, 4, 5, 7, 9])
 @pytest.mark.parametrize("oversub", [0, 2, 8, 16])
 def test_oversubscribed_vvstream(ctx, oracle_c, variant, oversub):
     import tcpck
