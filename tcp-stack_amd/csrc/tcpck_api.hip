@@ -559,10 +559,7 @@ int tcpck_host_batch_var(tcpck_ctx *ctx, int op, int mode, void *h_arena, const 
   auto *arena = static_cast<uint8_t *>(h_arena);
   auto *out_bytes = h_out ? static_cast<uint8_t *>(h_out) : reinterpret_cast<uint8_t *>(fill_res.data());
   const size_t es = out_elem(op);
-  uint64_t total_bytes = 0;
-  for (uint64_t k = 0; k < count; ++k) total_bytes += h_lengths[k];
   tcpck_layout lay{};
-  lay.total_bytes = total_bytes;
   lay.min_len = static_cast<uint32_t>(std::min<uint64_t>(min_len, UINT32_MAX));
   lay.max_len = static_cast<uint32_t>(std::min<uint64_t>(max_len, UINT32_MAX));
   lay.flags = packed ? TCPCK_LAYOUT_PACKED : 0u;
@@ -571,15 +568,17 @@ int tcpck_host_batch_var(tcpck_ctx *ctx, int op, int mode, void *h_arena, const 
   for (uint64_t k0 = 0; k0 < count && e == hipSuccess; ++c) {
     // greedy chunk: extend while the hull [lo, hi) of the chunk fits the stage
     uint64_t lo = h_offsets[k0] & ~uint64_t{15}, hi = h_offsets[k0] + h_lengths[k0];
-    uint64_t k1 = k0 + 1;
+    uint64_t k1 = k0 + 1, chunk_bytes = h_lengths[k0];
     while (k1 < count && k1 - k0 < max_imgs) {
       const uint64_t nlo = std::min(lo, h_offsets[k1] & ~uint64_t{15});
       const uint64_t nhi = std::max(hi, h_offsets[k1] + h_lengths[k1]);
       if (nhi - nlo > cap) break;
       lo = nlo;
       hi = nhi;
+      chunk_bytes += h_lengths[k1];
       ++k1;
     }
+    lay.total_bytes = chunk_bytes;  // the kernel policy sizes its grid by this launch's bytes
     const uint64_t n = k1 - k0;
     const int slot = static_cast<int>(c & 1);
     hipStream_t s = ctx->s[slot];

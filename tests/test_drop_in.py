@@ -103,3 +103,37 @@ def test_loopback_c1(built_lib):
     d = json.loads(r.stdout)
     assert d["received"] == d["verified"] == 3000
     assert d["image_bytes"] == 1492
+
+
+def _recv_burst(args, gpu):
+    import json
+    exe = os.path.join(LIBDIR, "bin", "recv_burst")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-s", "-C", LIBDIR], check=True)
+    r = subprocess.run([exe] + [str(a) for a in args] + ([] if gpu else ["--cpu-only"]),
+                       capture_output=True, text=True, timeout=120)
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert r.returncode == 0, (r.stderr, d)
+    assert d["lost"] == 0 and d["truncated"] == 0 and d["mismatches"] == 0 and d["flagged_wrong"] == 0
+    assert d["flagged"] == d["expected_flagged"]
+    return d
+
+
+@pytest.mark.parametrize("segments,payload,batch,every", [(20000, 1460, 4096, 97), (3000, 14, 700, 5),
+                                                           (2000, 1461, 512, 11), (1000, 576, 1000, 0)])
+def test_recv_burst_cpu(built_lib, segments, payload, batch, every):
+    """SURVEY §8f rank 2 plumbing on CPU: recvmmsg bursts into an arena, verdicts
+    per packet through the drop-in CalculateChecksum, corrupted segments flagged."""
+    d = _recv_burst([segments, payload, batch, every], gpu=False)
+    assert d["batches"] == -(-segments // batch)
+    assert d["odd"] == (segments if payload % 2 else 0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("segments,payload,batch,every", [(100000, 1460, 32768, 97), (20000, 64, 8192, 3),
+                                                           (4000, 1461, 1024, 13)])
+def test_recv_burst_gpu(built_lib, segments, payload, batch, every):
+    """One tcpck_host_batch_var(VERIFY) per batch of received datagrams; every GPU
+    verdict equals CalculateChecksum on the same bytes (odd lengths stay on the CPU)."""
+    d = _recv_burst([segments, payload, batch, every], gpu=True)
+    assert d["gpu"] is True and d["batches"] == -(-segments // batch)
