@@ -32,7 +32,7 @@ def main():
         kern = tcpck.KERNEL_VVSTREAM
         lmin, lmax = int(ln.min()), int(ln.max())
         params = [int(p, 0) for p in args.params.split(",")] if args.params else \
-            [4, 8 | (32 << 16), 7 | (32 << 16), 2 | (16 << 16), 2 | (8 << 16), 6 | (1 << 16)]
+            [4, 3 | (32 << 16), 2 | (32 << 16), 2 | (16 << 16), 2 | (8 << 16), 1 | (1 << 16)]
 
         def run(p):
             if p < 0:

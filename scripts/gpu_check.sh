@@ -28,6 +28,7 @@ for s in ${STEPS:-tests smoke bench prof}; do
     diagstream) step diagstream 600 python scripts/diag_stream.py ;;
     policy) step policy 900 python scripts/policy_sweep.py ;;
     policy_fixed) step policy_fixed 900 python scripts/policy_sweep.py --no-mixes ;;
+    policy_small) step policy_small 900 python scripts/policy_sweep.py --no-mixes --lengths 32,64,96,192,256,512,768,1024 --reps 4 ;;
     policy_mix) step policy_mix 900 python scripts/policy_sweep.py --no-fixed ;;
     vv) step vv 900 python -m pytest tests/test_gpu_kernels.py -x -q -k vvstream ;;
     vs) step vs 900 python -m pytest tests/test_gpu_kernels.py -x -q -k vstream ;;
@@ -40,9 +41,11 @@ for s in ${STEPS:-tests smoke bench prof}; do
     b2b_c2) step b2b_c2 600 python scripts/b2b_probe.py --what c2 ;;
     tr_c3) step tr_c3 300 python scripts/transient.py --what c3 ;;
     tr_c2) step tr_c2 300 python scripts/transient.py --what c2 --n 800 ;;
+    fillprobe) step fillprobe 600 python scripts/fill_probe.py ;;
+    vvall) step vvall 900 python -u -m pytest tests/test_gpu_kernels.py -x -q --timeout 300 --timeout-method thread -k vvstream ;;
     oversub) step oversub 600 python scripts/oversub.py ;;
     os_c2) step os_c2 600 python scripts/oversub.py --what c2 --variants 0,9,10 --ms 8,16,24,32,40,48 ;;
-    os_c3) step os_c3 600 python scripts/oversub.py --what c3 --variants 2,7,8 --ms 16,24,28,32,40 ;;
+    os_c3) step os_c3 600 python scripts/oversub.py --what c3 --variants 2,3 --ms 8,16,32 ;;
     prof_c3) step prof_c3 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c3 -o run --output-format csv -- python3 bench.py --config c3 --steps 10 --warmup 2 --no-cpu-baseline --no-e2e ;;
     prof_c4) step prof_c4 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c4 -o run --output-format csv -- python3 bench.py --config c4 --steps 10 --warmup 2 --no-cpu-baseline --no-e2e ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-e2e ;;

@@ -71,7 +71,7 @@ def main():
             label = f"L={L:5d} n={n:9d} kernel {kern}"
         elif what == "c3":
             from synth_np import mixed_layout
-            variants = [int(v) for v in args.variants.split(",")] if args.variants else (2, 8)
+            variants = [int(v) for v in args.variants.split(",")] if args.variants else (2, 3)
             off, ln, total = mixed_layout(4 << 20, seed=42)
             n = ln.size
             a = torch.empty(total, dtype=torch.uint8, device="cuda")

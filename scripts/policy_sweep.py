@@ -44,11 +44,13 @@ def main():
     p.add_argument("--reps", type=int, default=6)
     p.add_argument("--no-mixes", action="store_true")
     p.add_argument("--no-fixed", action="store_true")
+    p.add_argument("--lengths", default="", help="comma list of fixed image lengths (default: all)")
     args = p.parse_args()
     ctx = tcpck.Context(0)
     s = torch.cuda.current_stream()
     K = tcpck
-    for L in ([] if args.no_fixed else FIXED_L):
+    fixed_l = [int(x) for x in args.lengths.split(",")] if args.lengths else FIXED_L
+    for L in ([] if args.no_fixed else fixed_l):
         n = args.bytes // L
         a = torch.empty(n * L, dtype=torch.uint8, device="cuda")
         K.synth_fixed(a, L, L, n, seed=42)
@@ -68,6 +70,8 @@ def main():
                                                           stream=s)),
                 ("vstream U8", lambda: ctx.batch_fixed_ex(K.OP_CHECKSUM, a, L, L, n, out, K.KERNEL_VSTREAM, 2,
                                                           stream=s)),
+                ("vvstream fix", lambda: ctx.batch_fixed_ex(K.OP_CHECKSUM, a, L, L, n, out, K.KERNEL_VVSTREAM, 4,
+                                                            stream=s)),
                 ("rstream U2", lambda: ctx.batch_fixed_ex(K.OP_CHECKSUM, a, L, L, n, out, K.KERNEL_RSTREAM, 1,
                                                           stream=s)),
                 ("var rvstream", lambda: ctx.batch_var_ex(K.OP_CHECKSUM, a, off, ln, n, out, K.KERNEL_RVSTREAM, 0,
@@ -75,7 +79,9 @@ def main():
                 ("var stream", lambda: ctx.batch_var_ex(K.OP_CHECKSUM, a, off, ln, n, out, K.KERNEL_STREAM, 0,
                                                         packed=True, stream=s)),
                 ("var span", lambda: ctx.batch_var_ex(K.OP_CHECKSUM, a, off, ln, n, out, K.KERNEL_SPAN, 0,
-                                                      packed=True, stream=s))]
+                                                      packed=True, stream=s)),
+                ("var vvstream", lambda: ctx.batch_var_ex(K.OP_CHECKSUM, a, off, ln, n, out, K.KERNEL_VVSTREAM, 4,
+                                                          packed=True, total_bytes=n * L, stream=s))]
         runs = []
         for label, fn in cand:
             try:
@@ -120,6 +126,8 @@ def main():
                                                       stream=s, **lay)),
                 ("vvstream U8", lambda: ctx.batch_var_ex(K.OP_CHECKSUM, a, off, ln, n, out, K.KERNEL_VVSTREAM, 1,
                                                          stream=s, **lay)),
+                ("vvstream pol", lambda: ctx.batch_var_ex(K.OP_CHECKSUM, a, off, ln, n, out, K.KERNEL_VVSTREAM, 4,
+                                                          stream=s, **lay)),
                 ("vvstream cnt", lambda: ctx.batch_var_ex(K.OP_CHECKSUM, a, off, ln, n, out, K.KERNEL_VVSTREAM, 2,
                                                           stream=s, **lay)),
                 ("rvstream cnt", lambda: ctx.batch_var_ex(K.OP_CHECKSUM, a, off, ln, n, out, K.KERNEL_RVSTREAM, 3,

@@ -161,17 +161,18 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
                      uint64_t count, void *out, int kernel, int param, hipStream_t s) {
   const bool span_ok = mode == TCPCK_MODE_REF && stride == len && len >= 16 && len <= (1u << 24);
   // packed fixed stride, reference mode, by image length (scripts/policy_sweep.py,
-  // profiles/r01/policy_fixed.log): below 768 B boundaries are dense enough that
-  // resolving all of a step's boundaries in parallel (vstream, 8 loads in
-  // flight) wins; from 768 B the run-stream kernel's scalar boundary walk
-  // (~88% of the HBM roof on C2 at 32x oversubscription); jumbo images stay on seg (G64/U4), which
-  // streams whole images per wave at the same rate
+  // profiles/r01/policy_small.log): below 512 B boundaries are dense enough
+  // that resolving all of a step's ends in parallel from the prefix table
+  // (vvstream, FIXED) wins (+3-4% over vstream U8 at 32-256 B); from 512 B the
+  // run-stream kernel's scalar boundary walk (~87% of the HBM roof on C2 at
+  // 32x oversubscription); jumbo images stay on seg (G64/U4), which streams
+  // whole images per wave at the same rate.  FILL below 30 B is not defined.
   if (kernel == TCPCK_KERNEL_AUTO) {
     if (!span_ok || len > kSpanMaxLen) {
       kernel = TCPCK_KERNEL_SEG;
-    } else if (len < 768) {
-      kernel = TCPCK_KERNEL_VSTREAM;
-      param = 2;
+    } else if (len < 512) {
+      kernel = (op == TCPCK_OP_FILL && len < 30) ? TCPCK_KERNEL_SEG : TCPCK_KERNEL_VVSTREAM;
+      param = 4;
     } else {
       kernel = TCPCK_KERNEL_RSTREAM;
       param = 10;  // v_dot2 chunk sums, buffer loads (C2 +0.5%, profiles/r01/b2b_c2c3.log)
@@ -219,6 +220,17 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
     a.blocks_per_cu = static_cast<uint32_t>(param >> 8) & 0xFFu;
     a.oversub = static_cast<uint32_t>(param >> 16) & 0xFFu;
     return tcpck::launch_rstream(op, param & 0xFF, a, static_cast<uint32_t>(ctx->num_cus), s);
+  }
+  if (kernel == TCPCK_KERNEL_VVSTREAM) {  // any even length: the prefix table takes any number of ends per step
+    if (mode != TCPCK_MODE_REF || stride != len || len == 0 || len > (1u << 24) || (op == TCPCK_OP_FILL && len < 30))
+      return hipErrorInvalidValue;
+    tcpck::SpanArgs a{};
+    a.arena = arena;
+    a.stride = stride;
+    a.count = count;
+    a.out = out;
+    a.oversub = static_cast<uint32_t>(param >> 16) & 0xFFu;
+    return tcpck::launch_vvstream(op, param & 0xFF, true, a, static_cast<uint32_t>(ctx->num_cus), s);
   }
   if (kernel == TCPCK_KERNEL_VSTREAM) {
     if (!span_ok) return hipErrorInvalidValue;
@@ -285,7 +297,7 @@ hipError_t run_var(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const uint6
     a.out = out;
     a.oversub = static_cast<uint32_t>(param >> 16) & 0xFFu;
     a.total_bytes = layout ? layout->total_bytes : 0;
-    return tcpck::launch_vvstream(op, param & 0xFF, a, static_cast<uint32_t>(ctx->num_cus), s);
+    return tcpck::launch_vvstream(op, param & 0xFF, false, a, static_cast<uint32_t>(ctx->num_cus), s);
   }
   if (kernel == TCPCK_KERNEL_RVSTREAM) {
     // offsets ascending and packed (the layout hint); a wave whose length walk

@@ -85,11 +85,11 @@ hipError_t launch_vstream(int op, int variant, const FixedStreamArgs &a, uint32_
 // ---- run-stream kernel for packed variable layouts (tcpck_rvstream.hip), MODE_REF:
 // variant = loads in flight (0: 4, 1: 2, 2: 8) | blocks-per-CU cap << 8
 hipError_t launch_rvstream(int op, int variant, const SpanArgs &a, uint32_t num_cus, hipStream_t stream);
-// ---- vector-boundary run stream for packed variable layouts (tcpck_vvstream.hip),
-// MODE_REF, kChecksum / kVerify: variant 0 U4 byte split, 1 U8, 2 U4 count split, 3 U8,
-// 5-8 = 0-3 with prefix-table boundary resolution, 4 (= 9) = policy (oversubscription,
-// split and loads in flight by size; prefix table)
-hipError_t launch_vvstream(int op, int variant, const SpanArgs &a, uint32_t num_cus, hipStream_t stream);
+// ---- prefix-table run stream (tcpck_vvstream.hip), MODE_REF, all ops: packed
+// variable layouts (fixed = false) or fixed stride == len (fixed = true, a.stride).
+// variant 0 U4 byte split, 1 U8, 2 U4 count split, 3 U8 (fixed: 0/2 U4, 1/3 U8),
+// 4 = policy (oversubscription, split and loads in flight by size)
+hipError_t launch_vvstream(int op, int variant, bool fixed, const SpanArgs &a, uint32_t num_cus, hipStream_t stream);
 // timing-only streaming micro-kernels (tcpck_diag.hip)
 hipError_t launch_diag_stream(int variant, const uint8_t *buf, uint64_t bytes, uint32_t *out, uint32_t num_cus,
                               hipStream_t s);
