@@ -1,0 +1,46 @@
+#!/usr/bin/env python3
+"""Cost of FILL's in-place field write (tcpck_diag.hip diag_fill_kernel): the bare
+stream over 1.5 GB of 1492-B images plus one store per image of W bytes at the
+checksum field, W = 0 (none), 2, 4, 16, 32, 64, 128.  Median back-to-back."""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "tcp-stack_amd")]
+
+import torch  # noqa: E402
+import tcpck  # noqa: E402
+
+
+def main():
+    ctx = tcpck.Context(0)
+    s = torch.cuda.current_stream()
+    nbytes = 1492 << 20
+    buf = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    tcpck.synth_fixed(buf, 1492, 1492, 1 << 20, seed=1)
+    out = torch.empty(1 << 22, dtype=torch.int32, device="cuda")
+    names = {0: "no write", 1: "2 B", 2: "4 B", 3: "16 B", 4: "32 B", 5: "64 B", 6: "128 B", 7: "2 B, write-only pass", 8: "none, then a 2-B write-only pass"}
+    t = {v: [] for v in names}
+    for v in names:
+        for _ in range(20):
+            ctx.diag_stream(0x1000 | v, buf, nbytes, out, stream=s)
+    torch.cuda.synchronize()
+    for _ in range(5):
+        for v in names:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            for _ in range(10):
+                ctx.diag_stream(0x1000 | v, buf, nbytes, out, stream=s)
+            e1.record(s)
+            torch.cuda.synchronize()
+            t[v].append(e0.elapsed_time(e1) / 10)
+    for v, name in names.items():
+        ms = float(np.median(t[v]))
+        print(f"1492-B images, field write {name:8s} {ms:8.4f} ms  read rate {nbytes / ms / 1e6:7.1f} GB/s "
+              f"({nbytes / ms / 1e6 / 80:.1f}%)", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -132,6 +132,83 @@ hipError_t launch_dyn(const uint8_t *buf, uint64_t bytes, uint32_t *out, uint32_
   return hipGetLastError();
 }
 
+// In-place FILL write cost: the bare stream (1x16 B, U4, scan) over a buffer
+// of 1492-B images, plus one store per image at its checksum field (byte 28):
+// W bytes aligned down to W (W = 2, 4: the field's lane; W >= 16: every lane
+// whose 16-B chunk lies in the W-byte block, writing back the data it read).
+// Answers: is the cost of FILL the sub-line write itself, and does a wider,
+// aligned write-back of data already in registers avoid it?
+template <int W>
+__global__ void __launch_bounds__(kBlock) diag_fill_kernel(uint8_t *buf, uint64_t bytes, uint32_t *out) {
+  constexpr uint32_t kS = 1492;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t NW = static_cast<uint64_t>(gridDim.x) * kWavesPerBlock;
+  const uint64_t wid = static_cast<uint64_t>(blockIdx.x) * kWavesPerBlock +
+                       static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6)));
+  const uint64_t lines = bytes >> 7;
+  const uint64_t b0 = (wid * lines / NW) << 7;
+  const uint64_t b1 = ((wid + 1) * lines / NW) << 7;
+  if (b0 >= b1) return;
+  const uint32_t nsteps = static_cast<uint32_t>((b1 - b0 + 1023) >> 10);
+  const uint32_t last_chunk = static_cast<uint32_t>((b1 - b0) >> 4) - 1;
+  uint8_t *base = buf + b0;
+  auto ld = [&](uint32_t st) -> u32x4 {
+    return dev::load16_nt(base + 16 * static_cast<uint64_t>(min((st << 6) + lane, last_chunk)));
+  };
+  // first field at or after b0 (absolute), then every kS bytes
+  uint64_t nf = ((b0 + kS - 1 - 28) / kS) * kS + 28;
+  if (nf < b0) nf += kS;
+  u32x4 ring[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) ring[u] = ld(static_cast<uint32_t>(u));
+  uint32_t carry = 0;
+  for (uint32_t g = 0; g < nsteps; g += 4) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t st = g + u;
+      const uint64_t sb = b0 + (static_cast<uint64_t>(st) << 10);
+      const u32x4 w = ring[u];
+      const uint32_t t = dev::ref_chunk_sum(w);
+      const uint32_t incl = dev::wave_inclusive_scan(t);
+      carry += dev::read_lane(incl, 63);
+      if (W > 0) {
+        while (nf < sb + 1024 && nf < b1) {
+          const uint64_t c = sb + 16 * lane;  // this lane's chunk (absolute)
+          if constexpr (W < 16) {
+            const uint64_t blk = nf & ~static_cast<uint64_t>(W - 1);
+            if (c <= blk && blk < c + 16) {
+              if (W == 2) *reinterpret_cast<uint16_t *>(buf + blk) = static_cast<uint16_t>(t);
+              if (W == 4) *reinterpret_cast<uint32_t *>(buf + blk) = t;
+            }
+          } else {
+            const uint64_t blk = nf & ~static_cast<uint64_t>(W - 1);
+            if (c >= blk && c + 16 <= blk + W && c + 16 <= b1) *reinterpret_cast<u32x4 *>(buf + c) = w;
+          }
+          nf += kS;
+        }
+      }
+      ring[u] = ld(st + 4);
+    }
+  }
+  if (lane == 0) out[wid] = carry;
+}
+
+// The same field writes as a separate write-only pass: one thread per image.
+template <int W>
+__global__ void __launch_bounds__(kBlock) diag_scatter_kernel(uint8_t *buf, uint64_t n, uint32_t v) {
+  const uint64_t k = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (k >= n) return;
+  if (W == 2) *reinterpret_cast<uint16_t *>(buf + k * 1492 + 28) = static_cast<uint16_t>(v + k);
+  if (W == 4) *reinterpret_cast<uint32_t *>(buf + k * 1492 + 28) = static_cast<uint32_t>(v + k);
+}
+
+template <int W>
+hipError_t launch_fill(uint8_t *buf, uint64_t bytes, uint32_t *out, uint32_t num_cus, hipStream_t s) {
+  static const uint32_t per_cu = dev::resident_blocks_per_cu(diag_fill_kernel<W>);
+  hipLaunchKernelGGL((diag_fill_kernel<W>), dim3(per_cu * num_cus * 8), dim3(kBlock), 0, s, buf, bytes, out);
+  return hipGetLastError();
+}
+
 template <int LPB, int U, bool SCAN>
 hipError_t launch_one(const uint8_t *buf, uint64_t bytes, uint32_t *out, uint32_t num_cus, hipStream_t s,
                       uint32_t oversub = 1) {
@@ -146,9 +223,37 @@ hipError_t launch_one(const uint8_t *buf, uint64_t bytes, uint32_t *out, uint32_
 // variant: LPB x U x scan: 0 = 1x4 scan, 1 = 1x4 no scan, 2 = 2x2 scan, 3 = 2x2 no scan,
 // 4 = 4x1 scan, 5 = 2x4 scan, 6 = 4x2 scan, 7 = 1x2 scan;
 // block-shared dynamic units (1x16 B, scan): 8 = U4 16 KiB units, 9 = U4 32 KiB,
-// 10 = U4 8 KiB, 11 = U8 32 KiB
+// 10 = U4 8 KiB, 11 = U8 32 KiB; 0x1000 | w: in-place FILL write cost per 1492-B
+// image (w = 0 none, 1 2 B, 2 4 B, 3 16 B, 4 32 B, 5 64 B, 6 128 B)
 hipError_t launch_diag_stream(int variant, const uint8_t *buf, uint64_t bytes, uint32_t *out, uint32_t num_cus,
                               hipStream_t s) {
+  if (variant >= 0x1000) {  // in-place FILL write cost (timing only; writes into buf)
+    uint8_t *wb = const_cast<uint8_t *>(buf);
+    switch (variant & 0xFF) {
+      case 0: return launch_fill<0>(wb, bytes, out, num_cus, s);
+      case 1: return launch_fill<2>(wb, bytes, out, num_cus, s);
+      case 2: return launch_fill<4>(wb, bytes, out, num_cus, s);
+      case 3: return launch_fill<16>(wb, bytes, out, num_cus, s);
+      case 4: return launch_fill<32>(wb, bytes, out, num_cus, s);
+      case 5: return launch_fill<64>(wb, bytes, out, num_cus, s);
+      case 6: return launch_fill<128>(wb, bytes, out, num_cus, s);
+      case 7: {  // write-only pass, 2 B per image
+        const uint64_t n = bytes / 1492;
+        hipLaunchKernelGGL((diag_scatter_kernel<2>), dim3(static_cast<uint32_t>((n + kBlock - 1) / kBlock)), dim3(kBlock),
+                           0, s, wb, n, 7u);
+        return hipGetLastError();
+      }
+      case 8: {  // the stream without writes, then the write-only pass
+        hipError_t e = launch_fill<0>(wb, bytes, out, num_cus, s);
+        if (e != hipSuccess) return e;
+        const uint64_t n = bytes / 1492;
+        hipLaunchKernelGGL((diag_scatter_kernel<2>), dim3(static_cast<uint32_t>((n + kBlock - 1) / kBlock)), dim3(kBlock),
+                           0, s, wb, n, 7u);
+        return hipGetLastError();
+      }
+      default: return hipErrorInvalidValue;
+    }
+  }
   if (variant >> 8)  // 1x16 B, U4, scan, grid = (variant >> 8) x resident
     return launch_one<1, 4, true>(buf, bytes, out, num_cus, s, static_cast<uint32_t>(variant >> 8) & 0xFFu);
   switch (variant) {
