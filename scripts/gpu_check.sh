@@ -44,6 +44,8 @@ for s in ${STEPS:-tests smoke bench prof}; do
     fillprobe) step fillprobe 600 python scripts/fill_probe.py ;;
     vvall) step vvall 900 python -u -m pytest tests/test_gpu_kernels.py -x -q --timeout 300 --timeout-method thread -k vvstream ;;
     fillwrite) step fillwrite 300 python scripts/fill_write_probe.py ;;
+    cpol) step cpol 300 python scripts/cpol_probe.py ;;
+    os_c4) step os_c4 600 python scripts/oversub.py --what c4,c4r,c4v --ms 1,2,4,8,16,32 ;;
     oversub) step oversub 600 python scripts/oversub.py ;;
     os_c2) step os_c2 600 python scripts/oversub.py --what c2 --variants 0,9,10 --ms 8,16,24,32,40,48 ;;
     os_c3) step os_c3 600 python scripts/oversub.py --what c3 --variants 2,3 --ms 8,16,32 ;;

@@ -27,6 +27,8 @@ import tcpck  # noqa: E402
 FIXED = {"c2": (1492, 1 << 20, tcpck.KERNEL_RSTREAM, (0, 10)),
          "c5": (1492, 8 << 20, tcpck.KERNEL_RSTREAM, (0,)),
          "c4": (65536, 256 << 10, tcpck.KERNEL_SEG, (3,)),
+         "c4r": (65536, 256 << 10, tcpck.KERNEL_RSTREAM, (0, 10)),
+         "c4v": (65536, 256 << 10, tcpck.KERNEL_VVSTREAM, (0, 1)),
          "v256": (256, 6 << 20, tcpck.KERNEL_VSTREAM, (2,)),
          "v96": (96, 16 << 20, tcpck.KERNEL_VSTREAM, (2,))}
 

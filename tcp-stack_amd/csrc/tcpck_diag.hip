@@ -132,6 +132,49 @@ hipError_t launch_dyn(const uint8_t *buf, uint64_t bytes, uint32_t *out, uint32_
   return hipGetLastError();
 }
 
+// Cache-policy bits of the stream's loads: the bare stream (1x16 B, U4, scan,
+// one run per wave, grid oversubscribed 8x) with raw buffer loads whose aux
+// operand is AUX (bit 0 sc0, bit 1 nt, bit 4 sc1 on gfx950).
+template <int AUX>
+__global__ void __launch_bounds__(kBlock) diag_cpol_kernel(const uint8_t *buf, uint64_t bytes, uint32_t *out) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t NW = static_cast<uint64_t>(gridDim.x) * kWavesPerBlock;
+  const uint64_t wid = static_cast<uint64_t>(blockIdx.x) * kWavesPerBlock +
+                       static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6)));
+  const uint64_t lines = bytes >> 7;
+  const uint64_t b0 = (wid * lines / NW) << 7;
+  const uint64_t b1 = ((wid + 1) * lines / NW) << 7;
+  if (b0 >= b1) return;
+  const uint32_t nsteps = static_cast<uint32_t>((b1 - b0 + 1023) >> 10);
+  const auto rsrc = dev::make_rsrc(buf + b0, static_cast<uint32_t>(b1 - b0));
+  auto ld = [&](uint32_t st) -> u32x4 {
+    typedef unsigned v4u __attribute__((ext_vector_type(4)));
+    const v4u v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, static_cast<int>(lane << 4), static_cast<int>(st << 10), AUX);
+    return u32x4{v.x, v.y, v.z, v.w};
+  };
+  u32x4 ring[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) ring[u] = ld(static_cast<uint32_t>(u));
+  uint32_t carry = 0;
+  for (uint32_t g = 0; g < nsteps; g += 4) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t t = dev::ref_chunk_sum(ring[u]);
+      const uint32_t incl = dev::wave_inclusive_scan(t);
+      carry += dev::read_lane(incl, 63);
+      ring[u] = ld(g + u + 4);
+    }
+  }
+  if (lane == 0) out[wid] = carry;
+}
+
+template <int AUX>
+hipError_t launch_cpol(const uint8_t *buf, uint64_t bytes, uint32_t *out, uint32_t num_cus, hipStream_t s) {
+  static const uint32_t per_cu = dev::resident_blocks_per_cu(diag_cpol_kernel<AUX>);
+  hipLaunchKernelGGL((diag_cpol_kernel<AUX>), dim3(per_cu * num_cus * 8), dim3(kBlock), 0, s, buf, bytes, out);
+  return hipGetLastError();
+}
+
 // In-place FILL write cost: the bare stream (1x16 B, U4, scan) over a buffer
 // of 1492-B images, plus one store per image at its checksum field (byte 28):
 // W bytes aligned down to W (W = 2, 4: the field's lane; W >= 16: every lane
@@ -227,6 +270,19 @@ hipError_t launch_one(const uint8_t *buf, uint64_t bytes, uint32_t *out, uint32_
 // image (w = 0 none, 1 2 B, 2 4 B, 3 16 B, 4 32 B, 5 64 B, 6 128 B)
 hipError_t launch_diag_stream(int variant, const uint8_t *buf, uint64_t bytes, uint32_t *out, uint32_t num_cus,
                               hipStream_t s) {
+  if (variant >= 0x2000) {  // load cache-policy bits
+    switch (variant & 0xFF) {
+      case 0: return launch_cpol<0>(buf, bytes, out, num_cus, s);
+      case 1: return launch_cpol<1>(buf, bytes, out, num_cus, s);
+      case 2: return launch_cpol<2>(buf, bytes, out, num_cus, s);
+      case 3: return launch_cpol<3>(buf, bytes, out, num_cus, s);
+      case 16: return launch_cpol<16>(buf, bytes, out, num_cus, s);
+      case 17: return launch_cpol<17>(buf, bytes, out, num_cus, s);
+      case 18: return launch_cpol<18>(buf, bytes, out, num_cus, s);
+      case 19: return launch_cpol<19>(buf, bytes, out, num_cus, s);
+      default: return hipErrorInvalidValue;
+    }
+  }
   if (variant >= 0x1000) {  // in-place FILL write cost (timing only; writes into buf)
     uint8_t *wb = const_cast<uint8_t *>(buf);
     switch (variant & 0xFF) {
