@@ -46,6 +46,7 @@ for s in ${STEPS:-tests smoke bench prof}; do
     fillwrite) step fillwrite 300 python scripts/fill_write_probe.py ;;
     cpol) step cpol 300 python scripts/cpol_probe.py ;;
     os_c4) step os_c4 600 python scripts/oversub.py --what c4,c4r,c4v --ms 1,2,4,8,16,32 ;;
+    gap) step gap 600 python scripts/gap_probe.py ;;
     oversub) step oversub 600 python scripts/oversub.py ;;
     os_c2) step os_c2 600 python scripts/oversub.py --what c2 --variants 0,9,10 --ms 8,16,24,32,40,48 ;;
     os_c3) step os_c3 600 python scripts/oversub.py --what c3 --variants 2,3 --ms 8,16,32 ;;

@@ -167,6 +167,22 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
   // run-stream kernel's scalar boundary walk (~87% of the HBM roof on C2 at
   // 32x oversubscription); jumbo images stay on seg (G64/U4), which streams
   // whole images per wave at the same rate.  FILL below 30 B is not defined.
+  // gapped fixed strides (stride > len, e.g. MSS slots), reference mode
+  // (scripts/gap_probe.py, profiles/r01/gap_probe.log): streaming the gaps with
+  // the images (vvstream, virtual gap images) wins while they are small --
+  // 128/96 B 57% of the roof for image bytes vs seg's 39% -- else seg with
+  // 8 lanes per image (1536/1492 B 81% vs 77% for the length-based shape)
+  if (kernel == TCPCK_KERNEL_AUTO && mode == TCPCK_MODE_REF && stride > len && len >= 2 && len <= kSpanMaxLen) {
+    const uint64_t l = len;
+    const bool hull = len < 512 ? stride <= 2 * l : (len < 1024 ? 4 * stride <= 5 * l : 16 * stride <= 17 * l);
+    if (hull && stride <= (1u << 24) && (op != TCPCK_OP_FILL || len >= 30)) {
+      kernel = TCPCK_KERNEL_VVSTREAM;
+      param = 4;
+    } else {
+      kernel = TCPCK_KERNEL_SEG;
+      param = tcpck::kShapeSmall + 1;
+    }
+  }
   if (kernel == TCPCK_KERNEL_AUTO) {
     if (!span_ok || len > kSpanMaxLen) {
       kernel = TCPCK_KERNEL_SEG;
@@ -222,11 +238,12 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
     return tcpck::launch_rstream(op, param & 0xFF, a, static_cast<uint32_t>(ctx->num_cus), s);
   }
   if (kernel == TCPCK_KERNEL_VVSTREAM) {  // any even length: the prefix table takes any number of ends per step
-    if (mode != TCPCK_MODE_REF || stride != len || len == 0 || len > (1u << 24) || (op == TCPCK_OP_FILL && len < 30))
+    if (mode != TCPCK_MODE_REF || len == 0 || stride > (1u << 24) || (op == TCPCK_OP_FILL && len < 30))
       return hipErrorInvalidValue;
     tcpck::SpanArgs a{};
     a.arena = arena;
     a.stride = stride;
+    a.len = len;
     a.count = count;
     a.out = out;
     a.oversub = static_cast<uint32_t>(param >> 16) & 0xFFu;

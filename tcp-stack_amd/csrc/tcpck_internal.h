@@ -49,6 +49,7 @@ struct SpanArgs {
   uint32_t tile;             // images per wave tile, 1..63
   uint32_t oversub;          // grid = resident blocks x this (run-stream kernels; 0 = by size)
   uint64_t total_bytes;      // batch byte span hint (0 = unknown)
+  uint32_t len;              // fixed layouts: image length (vvstream: <= stride)
 };
 
 uint32_t span_tile_for_len(uint64_t typical_len);
@@ -86,7 +87,7 @@ hipError_t launch_vstream(int op, int variant, const FixedStreamArgs &a, uint32_
 // variant = loads in flight (0: 4, 1: 2, 2: 8) | blocks-per-CU cap << 8
 hipError_t launch_rvstream(int op, int variant, const SpanArgs &a, uint32_t num_cus, hipStream_t stream);
 // ---- prefix-table run stream (tcpck_vvstream.hip), MODE_REF, all ops: packed
-// variable layouts (fixed = false) or fixed stride == len (fixed = true, a.stride).
+// variable layouts (fixed = false) or fixed strides (fixed = true: a.stride >= a.len).
 // variant 0 U4 byte split, 1 U8, 2 U4 count split, 3 U8 (fixed: 0/2 U4, 1/3 U8),
 // 4 = policy (oversubscription, split and loads in flight by size)
 hipError_t launch_vvstream(int op, int variant, bool fixed, const SpanArgs &a, uint32_t num_cus, hipStream_t stream);

@@ -1,7 +1,8 @@
 // tcpck_vvstream.hip -- packed batches streamed as one contiguous run of whole
 // images per wave, every image end of a 1 KiB step resolved by the lanes in
 // parallel from a per-wave prefix table in LDS.  Packed variable layouts (C3)
-// and, with FIXED, fixed-stride small images; CHECKSUM, VERIFY and FILL.
+// and fixed strides (LAYOUT 1: packed, stride == length; LAYOUT 2: stride >
+// length, the gaps streamed with the images); CHECKSUM, VERIFY and FILL.
 //
 // Reference semantics: CalculateChecksum, include/tcp-header.h:252-263:
 // ~(sum of the image's LE u16 words mod 2^16).  Packed images make the run one
@@ -15,7 +16,10 @@
 //     descriptor latency overlaps the stream's;
 //   * image ends (variable layouts): 256 lengths at a time, one vector load
 //     per lane (4 lengths, prefetched a round ahead), prefix-summed across the
-//     wave into a 512-entry LDS ring per wave; FIXED: end j = lead + (j+1) S;
+//     wave into a 512-entry LDS ring per wave; fixed packed: end j = lead +
+//     (j+1) S; fixed gapped: the run is a packed sequence of 2n virtual
+//     images, gap i (ending where image i starts) and image i, end v = lead +
+//     (v >> 1) S + (v & 1) L, and only the odd (image) differences are stored;
 //   * per step: lane j holds end e(jn + j), read before the step's sums so the
 //     LDS latency overlaps them.  If any end falls in the step, every lane
 //     writes P at its chunk's 8 word positions as packed u16s (one
@@ -54,7 +58,8 @@ struct VVArgs {
   uint64_t count;
   void *out;                // u16 (CHECKSUM, FILL; may be null for FILL) or u8 (VERIFY)
   uint64_t per_wave, rem;   // equal-count split: count = per_wave * waves + rem
-  uint32_t stride;          // FIXED: image length == stride
+  uint32_t stride;          // fixed layouts: image k at k * stride
+  uint32_t len;             // fixed layouts: image length (<= stride)
 };
 
 // Word wi (0..7) of a 16-byte chunk set to zero.
@@ -68,8 +73,11 @@ __device__ __forceinline__ u32x4 zero_word(u32x4 w, uint32_t wi) {
   return w;
 }
 
-template <int U, int OP, int SPLIT, bool FIXED>
+// LAYOUT: 0 packed variable, 1 fixed packed (stride == len), 2 fixed gapped
+template <int U, int OP, int SPLIT, int LAYOUT>
 __global__ void __launch_bounds__(kBlock) vvstream_kernel(VVArgs a) {
+  constexpr bool FIXED = LAYOUT != 0;
+  constexpr bool GAP = LAYOUT == 2;
   __shared__ uint32_t s_end[kWavesPerBlock][FIXED ? 1 : kRing];
   __shared__ __attribute__((aligned(16))) uint32_t s_pre[kWavesPerBlock][256];  // packed u16 prefixes
   __shared__ uint32_t s_fld[kWavesPerBlock][OP == kFill ? 64 : 1];              // kFill: field word + 1 per chunk
@@ -79,6 +87,7 @@ __global__ void __launch_bounds__(kBlock) vvstream_kernel(VVArgs a) {
   const uint64_t wid = static_cast<uint64_t>(blockIdx.x) * kWavesPerBlock + wv;
   const uint64_t N = a.count;
   const uint32_t S = a.stride;
+  const uint32_t L = FIXED ? a.len : 0u;
   uint64_t kb, ke;
   if (FIXED || SPLIT == 1) {
     dev::count_split(wid, a.per_wave, a.rem, kb, ke);
@@ -96,7 +105,7 @@ __global__ void __launch_bounds__(kBlock) vvstream_kernel(VVArgs a) {
   uint64_t s0, s1;
   if constexpr (FIXED) {
     s0 = kb * S;
-    s1 = ke * S;
+    s1 = (ke - 1) * S + L;
   } else {
     s0 = a.offsets[kb] - a.base;
     s1 = a.offsets[ke - 1] - a.base + a.lengths[ke - 1];
@@ -104,6 +113,7 @@ __global__ void __launch_bounds__(kBlock) vvstream_kernel(VVArgs a) {
   uint8_t *const arena = a.arena;
   const uint64_t A0 = dev::align128_rel(arena, s0);
   const uint32_t nimg = static_cast<uint32_t>(ke - kb);
+  const uint32_t nv = GAP ? 2 * nimg : nimg;  // (virtual) images whose ends the stream resolves
   bool bad = !(s1 >= s0 && s1 - A0 < (uint64_t{1} << 31));
 
   // k = batch image index, start = its offset in the arena
@@ -150,7 +160,7 @@ __global__ void __launch_bounds__(kBlock) vvstream_kernel(VVArgs a) {
       }
     };
     uint32_t dnext[4] = {0, 0, 0, 0};
-    uint32_t loaded = FIXED ? nimg : 0;  // ends available (run-relative image count)
+    uint32_t loaded = FIXED ? nv : 0;  // ends available (run-relative image count)
     uint32_t pos = lead;                 // end of the last written image
     bool short_fill = false;             // kFill: an image < 30 B (two fields per chunk possible)
     auto fill_round = [&]() {            // write round (loaded / 256) from dnext, prefetch the next
@@ -197,10 +207,12 @@ __global__ void __launch_bounds__(kBlock) vvstream_kernel(VVArgs a) {
         }
       }
     } else {
-      if constexpr (OP == kFill) bad = S < 30;
+      if constexpr (OP == kFill) bad = L < 30;
     }
     auto end_of = [&](uint32_t j) -> uint32_t {  // run-relative end of run image j (j < nimg)
-      if constexpr (FIXED) {
+      if constexpr (GAP) {
+        return lead + (j >> 1) * S + (j & 1u) * L;
+      } else if constexpr (FIXED) {
         return lead + (j + 1) * S;
       } else {
         return ring_end[j % kRing];
@@ -222,10 +234,14 @@ __global__ void __launch_bounds__(kBlock) vvstream_kernel(VVArgs a) {
         // the step's first ends, read before the sums (the LDS latency overlaps them)
         if (!FIXED && jn + 66 > loaded && loaded < nimg) fill_round();  // >= 64 ends (+ 1 field) ahead
         uint32_t j = jn + lane;
-        uint32_t e = j < nimg ? end_of(j) : ~0u;
+        uint32_t e = j < nv ? end_of(j) : ~0u;
         if constexpr (OP == kFill) {  // zero the checksum fields that lie in this step
           const uint32_t i = fj + lane;
-          const uint32_t f = (i == 0 ? lead : (i < nimg ? end_of(i - 1) : span)) + 28;
+          uint32_t f;
+          if constexpr (FIXED)
+            f = lead + i * S + 28;
+          else
+            f = (i == 0 ? lead : (i < nimg ? end_of(i - 1) : span)) + 28;
           const bool inf = i < nimg && f < sb + 1024;
           const uint64_t bf = __ballot(inf);
           if (bf) {
@@ -271,9 +287,9 @@ __global__ void __launch_bounds__(kBlock) vvstream_kernel(VVArgs a) {
             const uint32_t el = static_cast<uint32_t>(
                 __builtin_amdgcn_update_dpp(static_cast<int>(e_last), static_cast<int>(e), 0x138, 0xF, 0xF, false));
             const uint32_t start = lane == 0 ? e_last : el;  // image jn + lane starts where jn + lane - 1 ends
-            if (inb) store(kb + j, P - pprev, A0 + start);
+            if (inb && (!GAP || (j & 1u))) store(kb + (GAP ? j >> 1 : j), P - pprev, A0 + start);
           } else {
-            if (inb) store(kb + j, P - pprev, 0);
+            if (inb && (!GAP || (j & 1u))) store(kb + (GAP ? j >> 1 : j), P - pprev, 0);
           }
           p_last = dev::read_lane(P, cnt - 1);
           e_last = dev::read_lane(e, cnt - 1);
@@ -281,7 +297,7 @@ __global__ void __launch_bounds__(kBlock) vvstream_kernel(VVArgs a) {
           if (cnt < 64) break;
           if (!FIXED && jn + 66 > loaded && loaded < nimg) fill_round();
           j = jn + lane;
-          e = j < nimg ? end_of(j) : ~0u;
+          e = j < nv ? end_of(j) : ~0u;
         }
         __builtin_amdgcn_wave_barrier();  // the next step rewrites the table
         carry += dev::read_lane(incl, 63);
@@ -289,18 +305,20 @@ __global__ void __launch_bounds__(kBlock) vvstream_kernel(VVArgs a) {
       }
     }
     if constexpr (!FIXED) bad = bad || pos != span || loaded < nimg;
-    if (!bad && jn < nimg) {  // ends exactly at the last step's end (= span): the first gets the rest
-      const uint32_t rem = nimg - jn;
-      for (uint32_t i = lane; i < rem; i += 64)
-        store(kb + jn + i, i == 0 ? carry - p_last : 0u, A0 + (i == 0 ? e_last : span));
-      jn = nimg;
+    if (!bad && jn < nv) {  // ends exactly at the last step's end (= span): the first gets the rest
+      const uint32_t rem = nv - jn;
+      for (uint32_t i = lane; i < rem; i += 64) {
+        const uint32_t v = jn + i;
+        if (!GAP || (v & 1u)) store(kb + (GAP ? v >> 1 : v), i == 0 ? carry - p_last : 0u, A0 + (i == 0 ? e_last : span));
+      }
+      jn = nv;
     }
-    bad = bad || jn != nimg;
+    bad = bad || jn != nv;
   }
   if (bad) {  // wave-uniform: the layout is not what the walk assumed -> exact per-image pass
     for (uint64_t k = kb; k < ke; ++k) {
       const uint64_t start = FIXED ? k * S : a.offsets[k] - a.base;
-      const uint32_t len = FIXED ? S : a.lengths[k];
+      const uint32_t len = FIXED ? L : a.lengths[k];
       if (OP == kFill && len < 30) continue;  // precondition of kFill (the C ABI rejects these)
       const uint32_t sum = dev::wave_image_sum<2, kRef>(arena, start, len, OP == kFill);
       if (lane == 0) store(k, sum, start);
@@ -308,9 +326,9 @@ __global__ void __launch_bounds__(kBlock) vvstream_kernel(VVArgs a) {
   }
 }
 
-template <int U, int OP, int SPLIT, bool FIXED>
+template <int U, int OP, int SPLIT, int LAYOUT>
 hipError_t launch_one(const SpanArgs &s, uint32_t oversub, uint32_t num_cus, hipStream_t stream) {
-  static const uint32_t per_cu = dev::resident_blocks_per_cu(vvstream_kernel<U, OP, SPLIT, FIXED>);
+  static const uint32_t per_cu = dev::resident_blocks_per_cu(vvstream_kernel<U, OP, SPLIT, LAYOUT>);
   const uint64_t resident = static_cast<uint64_t>(per_cu) * num_cus;
   uint64_t blocks = resident * (oversub ? oversub : 1);
   const uint64_t need = (s.count + kWavesPerBlock - 1) / kWavesPerBlock;
@@ -326,17 +344,18 @@ hipError_t launch_one(const SpanArgs &s, uint32_t oversub, uint32_t num_cus, hip
   a.per_wave = s.count / (blocks * kWavesPerBlock);
   a.rem = s.count % (blocks * kWavesPerBlock);
   a.stride = static_cast<uint32_t>(s.stride);
-  hipLaunchKernelGGL((vvstream_kernel<U, OP, SPLIT, FIXED>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0,
+  a.len = s.len;
+  hipLaunchKernelGGL((vvstream_kernel<U, OP, SPLIT, LAYOUT>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0,
                      stream, a);
   return hipGetLastError();
 }
 
-template <int U, int SPLIT, bool FIXED>
+template <int U, int SPLIT, int LAYOUT>
 hipError_t dispatch(int op, const SpanArgs &a, uint32_t oversub, uint32_t num_cus, hipStream_t s) {
   switch (op) {
-    case kChecksum: return launch_one<U, kChecksum, SPLIT, FIXED>(a, oversub, num_cus, s);
-    case kVerify: return launch_one<U, kVerify, SPLIT, FIXED>(a, oversub, num_cus, s);
-    case kFill: return launch_one<U, kFill, SPLIT, FIXED>(a, oversub, num_cus, s);
+    case kChecksum: return launch_one<U, kChecksum, SPLIT, LAYOUT>(a, oversub, num_cus, s);
+    case kVerify: return launch_one<U, kVerify, SPLIT, LAYOUT>(a, oversub, num_cus, s);
+    case kFill: return launch_one<U, kFill, SPLIT, LAYOUT>(a, oversub, num_cus, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -346,35 +365,28 @@ hipError_t dispatch(int op, const SpanArgs &a, uint32_t oversub, uint32_t num_cu
 hipError_t launch_vvstream(int op, int variant, bool fixed, const SpanArgs &a, uint32_t num_cus,
                            hipStream_t stream) {
   if (a.count == 0) return hipSuccess;
-  if (fixed && (a.stride == 0 || a.stride > (1u << 24))) return hipErrorInvalidValue;
+  if (fixed && (a.len == 0 || a.stride < a.len || a.stride > (1u << 24))) return hipErrorInvalidValue;
+  const bool gap = fixed && a.stride != a.len;
   const uint64_t bytes = fixed ? a.count * a.stride : a.total_bytes;
+  uint32_t m = a.oversub ? a.oversub : 1;
+  int u8 = (variant & 1);
+  int split = variant >= 2 ? 1 : 0;
   if (variant == 4) {
     // library policy: oversubscribe by size, runs of >= 8 KiB, M a power of two
     // <= 32 (M = 16/24/40 measured 2-4% below 32 on the run kernels,
     // profiles/r01/oversub_c2c3.log).  At M = 32, U8 (C3 85.0-86.3% vs U4
     // 82.7-84.2%); once M >= 4 the dispatcher balances the runs and
     // equal-count runs (no offset searches) win.
-    const uint32_t m = dev::oversub_for(a.oversub, bytes, static_cast<uint64_t>(num_cus) * 32, 32, 8u << 10);
-    if (fixed)
-      return m >= 32 ? dispatch<8, 1, true>(op, a, m, num_cus, stream) : dispatch<4, 1, true>(op, a, m, num_cus, stream);
-    if (m >= 32) return dispatch<8, 1, false>(op, a, m, num_cus, stream);
-    return m >= 4 ? dispatch<4, 1, false>(op, a, m, num_cus, stream) : dispatch<4, 0, false>(op, a, m, num_cus, stream);
+    m = dev::oversub_for(a.oversub, bytes, static_cast<uint64_t>(num_cus) * 32, 32, 8u << 10);
+    u8 = m >= 32;
+    split = m >= 4;
+  } else if (variant > 4 || variant < 0) {
+    return hipErrorInvalidValue;
   }
-  const uint32_t m = a.oversub ? a.oversub : 1;
-  if (fixed) {
-    switch (variant) {
-      case 0: case 2: return dispatch<4, 1, true>(op, a, m, num_cus, stream);
-      case 1: case 3: return dispatch<8, 1, true>(op, a, m, num_cus, stream);
-      default: return hipErrorInvalidValue;
-    }
-  }
-  switch (variant) {
-    case 0: return dispatch<4, 0, false>(op, a, m, num_cus, stream);
-    case 1: return dispatch<8, 0, false>(op, a, m, num_cus, stream);
-    case 2: return dispatch<4, 1, false>(op, a, m, num_cus, stream);
-    case 3: return dispatch<8, 1, false>(op, a, m, num_cus, stream);
-    default: return hipErrorInvalidValue;
-  }
+  if (gap) return u8 ? dispatch<8, 1, 2>(op, a, m, num_cus, stream) : dispatch<4, 1, 2>(op, a, m, num_cus, stream);
+  if (fixed) return u8 ? dispatch<8, 1, 1>(op, a, m, num_cus, stream) : dispatch<4, 1, 1>(op, a, m, num_cus, stream);
+  if (split) return u8 ? dispatch<8, 1, 0>(op, a, m, num_cus, stream) : dispatch<4, 1, 0>(op, a, m, num_cus, stream);
+  return u8 ? dispatch<8, 0, 0>(op, a, m, num_cus, stream) : dispatch<4, 0, 0>(op, a, m, num_cus, stream);
 }
 
 }  // namespace tcpck

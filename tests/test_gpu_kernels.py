@@ -595,6 +595,39 @@ def test_vvstream_fixed_vs_oracle(ctx, oracle_c, variant, length, count):
                                                          threads=8))
 
 
+@pytest.mark.parametrize("variant", [0, 1, 4])
+@pytest.mark.parametrize("stride,length", [(4, 2), (34, 32), (100, 2), (128, 96), (1000, 30), (1536, 1492),
+                                           (2048, 1492), (70000, 65504)])
+@pytest.mark.parametrize("count", [1, 2, 65, 3001, 40000])
+def test_vvstream_fixed_gapped(ctx, oracle_c, variant, stride, length, count):
+    """stride > length: the run streams the gaps too, as virtual images whose sums are dropped."""
+    import tcpck
+    if count * stride > (600 << 20):
+        count = (600 << 20) // stride
+    rng = np.random.default_rng(stride + length + count + variant)
+    arena_np = rng.integers(0, 256, count * stride + 128, dtype=np.uint8)
+    buf = dev(arena_np)
+    for mis in (0, 2, 50):
+        for oversub in (0, 8):
+            out = torch.empty(count, dtype=torch.int16, device="cuda")
+            ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, buf.data_ptr() + mis, stride, length, count, out,
+                               tcpck.KERNEL_VVSTREAM, variant | (oversub << 16))
+            np.testing.assert_array_equal(host(out).view(np.uint16),
+                                          oracle_c.batch(arena_np[mis:], stride=stride, length=length, count=count,
+                                                         threads=8))
+    if length >= 30:
+        arena = dev(arena_np)
+        out = torch.empty(count, dtype=torch.int16, device="cuda")
+        ctx.batch_fixed_ex(tcpck.OP_FILL, arena, stride, length, count, out, tcpck.KERNEL_VVSTREAM, variant)
+        off = np.arange(count, dtype=np.uint64) * stride
+        exp, exp_arena = _fill_oracle(arena_np, off, np.full(count, length, np.uint32))
+        np.testing.assert_array_equal(host(out).view(np.uint16), exp)
+        np.testing.assert_array_equal(host(arena), exp_arena)  # gap bytes untouched
+        ok = torch.empty(count, dtype=torch.uint8, device="cuda")
+        ctx.batch_fixed_ex(tcpck.OP_VERIFY, arena, stride, length, count, ok, tcpck.KERNEL_VVSTREAM, variant)
+        assert bool(ok.all().item())
+
+
 @pytest.mark.parametrize("variant", [0, 4])
 @pytest.mark.parametrize("length", [30, 32, 96, 1492])
 def test_vvstream_fixed_fill_verify(ctx, variant, length):
