@@ -150,11 +150,16 @@ void free_stage(tcpck_ctx *ctx) {
   }
 }
 
-// ---- kernel selection --------------------------------------------------------
-// span: packed layouts in reference mode (the hot path for MSS-sized images);
-// seg:  everything else (gaps, unordered offsets, tiny images, RFC 1071 mode)
-//       and jumbo images, where one wave per image already streams 16-B-aligned
-//       1 KiB runs.
+// ---- kernel selection (AUTO; measurements in DESIGN.md section 4) ------------
+// reference mode:
+//   fixed, stride == len   < 512 B vvstream (prefix table), 512 B..16 KiB
+//                          rstream (scalar boundary walk), larger seg
+//   fixed, stride > len    small gaps vvstream (gaps streamed as virtual
+//                          images), larger gaps seg with 8 lanes per image
+//   packed variable        CHECKSUM / VERIFY vvstream, FILL span
+// everything else -- unordered offsets, gaps in variable layouts, RFC 1071
+// mode, jumbo images (where one wave per image already streams whole 1 KiB
+// steps) -- seg.
 constexpr uint64_t kSpanMaxLen = 16384;
 
 hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t stride, uint32_t len,
