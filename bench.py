@@ -138,7 +138,7 @@ def main():
         else:
             dist.init_process_group(backend)
 
-    from tcpck.shard import max_over_ranks, shard_range
+    from tcpck.shard import gather_ranks, max_over_ranks, shard_range
     desc, kind, count, L = CONFIGS[args.config]
     ctx = tcpck.Context(local)
     stream = torch.cuda.current_stream()
@@ -216,6 +216,7 @@ def main():
     launch_ms = float(np.sum([s.elapsed_time(e) for s, e in zip(starts, ends)])) / args.steps
 
     tmax = max_over_ranks(elapsed, device=coll_dev)
+    launch_ms_all = gather_ranks(launch_ms, device=coll_dev)  # per-GPU kernel time (ranks start together)
     shard_bytes = torch.tensor([img_bytes], dtype=torch.int64, device=coll_dev)
     if world > 1:
         dist.all_reduce(shard_bytes)  # bytes all ranks processed per step (shards may differ by one image)
@@ -236,6 +237,8 @@ def main():
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(args.config),
                 "algorithmic_bytes_per_launch": algo_bytes, "avg_launch_ms": round(launch_ms, 5)}
+    if world > 1:  # rank 0's kernel above; every GPU's fraction here (equal shards)
+        roofline["per_gpu_frac"] = [round(algo_bytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) for ms in launch_ms_all]
 
     rec = {
         "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world,

@@ -47,3 +47,16 @@ def max_over_ranks(seconds: float, device=None) -> float:
     t = torch.tensor([seconds], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def gather_ranks(value: float, device=None) -> list[float]:
+    """Every rank's `value`, in rank order (one all-reduce of a one-hot vector);
+    [value] without a process group."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return [float(value)]
+    t = torch.zeros(dist.get_world_size(), dtype=torch.float64, device=device)
+    t[dist.get_rank()] = value
+    dist.all_reduce(t)
+    return [float(x) for x in t.cpu().tolist()]

@@ -20,7 +20,7 @@ import torch.multiprocessing as mp
 
 from oracle.ref16 import ref16_batch_np
 from synth_np import arena_fixed, image, mixed_layout
-from tcpck.shard import max_over_ranks, shard_by_bytes, shard_range
+from tcpck.shard import gather_ranks, max_over_ranks, shard_by_bytes, shard_range
 
 WORLD = 2
 
@@ -55,6 +55,7 @@ def _worker(rank, world, port, q):
         res["weak"] = ref16_batch_np(warena, np.arange(wc) * 608, np.full(wc, 608))
         # timing reduction: the job's time is the slowest rank's
         res["tmax"] = max_over_ranks(1.0 + rank)
+        res["all"] = gather_ranks(0.25 * (rank + 1))  # per-GPU kernel times for per-GPU roofline fractions
         gathered = [None] * world
         dist.all_gather_object(gathered, res)
         if rank == 0:
@@ -104,6 +105,11 @@ def test_weak_batches(gathered):
 
 def test_max_over_ranks(gathered):
     assert [g["tmax"] for g in gathered] == [2.0, 2.0]
+
+
+def test_gather_ranks(gathered):
+    assert [g["all"] for g in gathered] == [[0.25, 0.5], [0.25, 0.5]]
+    assert gather_ranks(3.0) == [3.0]  # no process group in this process
 
 
 @pytest.mark.parametrize("count,world", [(0, 3), (1, 2), (7, 8), (8 << 20, 8), (1000003, 7)])
