@@ -38,7 +38,13 @@
 #include <ostream>
 #include <utility>
 
+// tcpck.h sits one directory up; a build that reaches this header through
+// another path (e.g. a directory of symlinks) finds it on the include path
+#if __has_include("../tcpck.h")
 #include "../tcpck.h"
+#else
+#include "tcpck.h"
+#endif
 
 namespace tcp_stack {
 

@@ -33,6 +33,7 @@ for s in ${STEPS:-tests smoke bench prof}; do
     vv) step vv 900 python -m pytest tests/test_gpu_kernels.py -x -q -k vvstream ;;
     vs) step vs 900 python -m pytest tests/test_gpu_kernels.py -x -q -k vstream ;;
     bench_c4) step bench_c4 600 python bench.py --config c4 --no-cpu-baseline ;;
+    bench_c5) step bench_c5 600 python bench.py --config c5 --no-cpu-baseline --no-e2e ;;
     mrank) step mrank 600 env TCPCK_BENCH_BACKEND=gloo TCPCK_BENCH_DEVICE=0 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29561 bench.py --gpus 2 --steps 5 --warmup 2 &&
       step mrank_c5 600 env TCPCK_BENCH_BACKEND=gloo TCPCK_BENCH_DEVICE=0 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29562 bench.py --gpus 2 --config c5 --steps 5 --warmup 2 ;;
     vvprobe) step vvprobe 600 python scripts/vv_probe.py ;;
@@ -47,6 +48,7 @@ for s in ${STEPS:-tests smoke bench prof}; do
     cpol) step cpol 300 python scripts/cpol_probe.py ;;
     os_c4) step os_c4 600 python scripts/oversub.py --what c4,c4r,c4v --ms 1,2,4,8,16,32 ;;
     gap) step gap 600 python scripts/gap_probe.py ;;
+    os_c5) step os_c5 600 python scripts/oversub.py --what c5,c5v,c2v --variants 0,1,10 --ms 8,16,32,64 ;;
     oversub) step oversub 600 python scripts/oversub.py ;;
     os_c2) step os_c2 600 python scripts/oversub.py --what c2 --variants 0,9,10 --ms 8,16,24,32,40,48 ;;
     os_c3) step os_c3 600 python scripts/oversub.py --what c3 --variants 2,3 --ms 8,16,32 ;;

@@ -137,3 +137,19 @@ def test_recv_burst_gpu(built_lib, segments, payload, batch, every):
     verdict equals CalculateChecksum on the same bytes (odd lengths stay on the CPU)."""
     d = _recv_burst([segments, payload, batch, every], gpu=True)
     assert d["gpu"] is True and d["batches"] == -(-segments // batch)
+
+
+@pytest.mark.skipif(not os.path.exists("/root/reference/src/socket-manager.cc"),
+                    reason="the reference checkout exists only in the build container")
+def test_reference_stack_compiles_against_drop_in(built_lib):
+    """The reference's own translation units that use tcp-header.h compile
+    unchanged with tcp-header.h resolved to include/tcp_stack/tcp-header.h, and
+    link against libtcpck.so with nothing left undefined but TimeoutQueue::Worker
+    (src/timeout-queue.cc, which g++ 11 rejects on the reference header too).
+    CalculateChecksum at socket-manager.cc:10 / socket-manager.h:182,260 now
+    calls tcpck_checksum16 (oracle/Makefile `dropin`)."""
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "dropin"], check=True)
+    d = os.path.join(ROOT, "oracle", "_ref", "dropin")
+    unresolved = open(os.path.join(d, "unresolved.txt")).read().split("\n")
+    assert [u for u in unresolved if u] == ["undefined reference to `TimeoutQueue::Worker()'"]
+    assert open(os.path.join(d, "uses_tcpck.txt")).read().strip() == "1"
