@@ -17,15 +17,8 @@ extern "C" {
 #define TCPCK_KERNEL_SEG 1  /* G lanes per image, any layout; param = shape + 1
                                (1: G8/U2, 2: G16/U6, 3: G64/U4, 4: G64/U2,
                                 5: G32/U3, 6: G4/U8), 0 = by length               */
-#define TCPCK_KERNEL_SPAN 2 /* packed images streamed per wave tile, MODE_REF only;
-                               param = images per tile (1..63), 0 = by length     */
-#define TCPCK_KERNEL_STREAM 3 /* packed images, one byte-balanced run per wave,
-                                 MODE_REF only; param = variant (0: 4 loads in
-                                 flight nt, 1: 8 nt, 2: 4 plain, 3: 2 nt)        */
-#define TCPCK_KERNEL_FSTREAM 4 /* fixed stride == len only, MODE_REF: interleaved
-                                  tiles, arithmetic boundaries; param = images
-                                  per tile (low 16 bits, 0 = auto) | variant << 16
-                                  (0: 4 loads in flight, 1: 2)                  */
+/* 2, 3, 4, 6, 7: span, stream, fstream, rvstream and vstream, measured in
+   round 1 and removed; the numbers are not reused. */
 #define TCPCK_KERNEL_RSTREAM 5 /* fixed stride == len only, MODE_REF: one run per
                                   wave, scalar boundary walk; param = variant
                                   (0: 4 loads in flight, 1: 2, 2: 8, 3: 4 with
@@ -33,30 +26,21 @@ extern "C" {
                                   4/8/2 loads with slot-graded s_setprio, 5: 4
                                   with s_setprio 1 for slots >= 4, 7: 3 + graded
                                   priority, 9: 4 with v_dot2 sums, 10/12/13:
-                                  4/2/8 with v_dot2 sums and buffer loads, 11:
-                                  4 with buffer loads) | (blocks per CU cap << 8)
+                                  4/2/8 with v_dot2 sums and buffer loads (10 =
+                                  the policy's), 11: 4 with buffer loads)
+                                  | (blocks per CU cap << 8)
                                   | (grid oversubscription << 16: 0 = by batch
                                   size, 1 = none, M = M x the resident grid)    */
-#define TCPCK_KERNEL_VSTREAM 7 /* fixed stride == len >= 16, MODE_REF: run per
-                                  wave, all boundaries of a step resolved by the
-                                  lanes in parallel (small images); param =
-                                  variant (0: 4 loads in flight, 1: 2, 2: 8)
-                                  | (grid oversubscription << 16: 0 = by batch
-                                  size, 1 = none, M = M x the resident grid)    */
-#define TCPCK_KERNEL_VVSTREAM 8 /* packed variable layouts, MODE_REF, CHECKSUM /
-                                   VERIFY: run per wave, a step's boundaries
-                                   resolved in parallel from an LDS ring of
-                                   image ends; param = variant (0: 4 loads in
-                                   flight, 1: 8; 2/3: same with equal-count
-                                   instead of byte-balanced runs; 5-8: 0-3
-                                   with the prefix-table resolution, any
-                                   image lengths; 4/9: policy)
+#define TCPCK_KERNEL_VVSTREAM 8 /* MODE_REF, all ops: packed variable layouts and
+                                   fixed strides (stride >= len, gaps streamed),
+                                   any even image length; run per wave, a step's
+                                   image ends resolved in parallel from an LDS
+                                   prefix table; param = variant (0: 4 loads in
+                                   flight, byte-balanced runs, 1: 8; 2/3: same
+                                   with equal-count runs -- fixed layouts are
+                                   always equal-count; 4: policy)
                                    | (grid oversubscription << 16: 0 = by batch
-                                  size, 1 = none, M = M x the resident grid)    */
-#define TCPCK_KERNEL_RVSTREAM 6 /* packed variable layouts, MODE_REF: byte-balanced
-                                   run per wave, scalar walk over the lengths;
-                                   param = variant (0: 4 loads in flight, 1: 2,
-                                   2: 8) | (blocks per CU cap << 8)             */
+                                   size, 1 = none, M = M x the resident grid)   */
 
 int tcpck_batch_fixed_ex(tcpck_ctx *ctx, int op, int mode, void *d_arena,
                          uint64_t stride, uint32_t len, uint64_t count, void *d_out,

@@ -51,9 +51,7 @@ def main():
 
     def chk():
         assert torch.equal(out, ref)
-    for label, fn in (("C3 fill span", lambda: ctx.batch_var_ex(K.OP_FILL, a, d_off, d_ln, n, out, K.KERNEL_SPAN, 0,
-                                                                stream=s, **lay)),
-                      ("C3 fill vvstream policy", lambda: ctx.batch_var_ex(K.OP_FILL, a, d_off, d_ln, n, out,
+    for label, fn in (("C3 fill vvstream policy", lambda: ctx.batch_var_ex(K.OP_FILL, a, d_off, d_ln, n, out,
                                                                            K.KERNEL_VVSTREAM, 4, stream=s, **lay)),
                       ("C3 fill auto", lambda: ctx.batch_var(K.OP_FILL, a, d_off, d_ln, n, out, stream=s, **lay)),
                       ("C3 checksum auto", lambda: ctx.batch_var(K.OP_CHECKSUM, a, d_off, d_ln, n, out, stream=s,
@@ -70,8 +68,8 @@ def main():
 
         def chk():
             assert torch.equal(out, ref)
-        for label, kern, p in (("rstream", K.KERNEL_RSTREAM, 10), ("vstream U8", K.KERNEL_VSTREAM, 2),
-                               ("vvstream fixed", K.KERNEL_VVSTREAM, 4), ("auto", None, 0)):
+        for label, kern, p in (("rstream", K.KERNEL_RSTREAM, 10), ("vvstream fixed", K.KERNEL_VVSTREAM, 4),
+                               ("auto", None, 0)):
             for op in (K.OP_FILL, K.OP_CHECKSUM):
                 if kern is None:
                     fn = (lambda op=op: ctx.batch_fixed(op, a, L, L, n, out, stream=s))

@@ -22,16 +22,14 @@ for s in ${STEPS:-tests smoke bench prof}; do
     bench_c3) step bench_c3 600 python bench.py --config c3 --no-cpu-baseline ;;
     sweep) step sweep 900 python scripts/sweep.py ;;
     sweep_c3) step sweep_c3 600 python scripts/sweep.py --configs c3 ;;
-    rv) step rv 900 python -m pytest tests/test_gpu_kernels.py -x -q -k "rvstream or rstream" ;;
+    rv) step rv 900 python -m pytest tests/test_gpu_kernels.py -x -q -k rstream ;;
     sweep_c2) step sweep_c2 600 python scripts/sweep.py --configs c2 ;;
-    rvprobe) step rvprobe 600 python scripts/rv_probe.py ;;
     diagstream) step diagstream 600 python scripts/diag_stream.py ;;
     policy) step policy 900 python scripts/policy_sweep.py ;;
     policy_fixed) step policy_fixed 900 python scripts/policy_sweep.py --no-mixes ;;
     policy_small) step policy_small 900 python scripts/policy_sweep.py --no-mixes --lengths 32,64,96,192,256,512,768,1024 --reps 4 ;;
     policy_mix) step policy_mix 900 python scripts/policy_sweep.py --no-fixed ;;
     vv) step vv 900 python -m pytest tests/test_gpu_kernels.py -x -q -k vvstream ;;
-    vs) step vs 900 python -m pytest tests/test_gpu_kernels.py -x -q -k vstream ;;
     bench_c4) step bench_c4 600 python bench.py --config c4 --no-cpu-baseline ;;
     bench_c5) step bench_c5 600 python bench.py --config c5 --no-cpu-baseline --no-e2e ;;
     mrank) step mrank 600 env TCPCK_BENCH_BACKEND=gloo TCPCK_BENCH_DEVICE=0 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29561 bench.py --gpus 2 --steps 5 --warmup 2 &&

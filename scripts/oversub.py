@@ -31,8 +31,8 @@ FIXED = {"c2": (1492, 1 << 20, tcpck.KERNEL_RSTREAM, (0, 10)),
          "c4": (65536, 256 << 10, tcpck.KERNEL_SEG, (3,)),
          "c4r": (65536, 256 << 10, tcpck.KERNEL_RSTREAM, (0, 10)),
          "c4v": (65536, 256 << 10, tcpck.KERNEL_VVSTREAM, (0, 1)),
-         "v256": (256, 6 << 20, tcpck.KERNEL_VSTREAM, (2,)),
-         "v96": (96, 16 << 20, tcpck.KERNEL_VSTREAM, (2,))}
+         "v256": (256, 6 << 20, tcpck.KERNEL_VVSTREAM, (0, 1)),
+         "v96": (96, 16 << 20, tcpck.KERNEL_VVSTREAM, (0, 1))}
 
 
 def timed(fn, params, rounds=8, reps=3):

@@ -61,25 +61,11 @@ def main():
         ln = torch.full((n,), L, dtype=torch.int32, device="cuda")
         cand = [("auto", lambda: ctx.batch_fixed(K.OP_CHECKSUM, a, L, L, n, out, stream=s)),
                 ("seg", lambda: ctx.batch_fixed_ex(K.OP_CHECKSUM, a, L, L, n, out, K.KERNEL_SEG, 0, stream=s)),
-                ("span", lambda: ctx.batch_fixed_ex(K.OP_CHECKSUM, a, L, L, n, out, K.KERNEL_SPAN, 0, stream=s)),
-                ("stream", lambda: ctx.batch_fixed_ex(K.OP_CHECKSUM, a, L, L, n, out, K.KERNEL_STREAM, 0, stream=s)),
-                ("fstream", lambda: ctx.batch_fixed_ex(K.OP_CHECKSUM, a, L, L, n, out, K.KERNEL_FSTREAM, 0, stream=s)),
                 ("rstream", lambda: ctx.batch_fixed_ex(K.OP_CHECKSUM, a, L, L, n, out, K.KERNEL_RSTREAM, 0, stream=s)),
-                ("vstream", lambda: ctx.batch_fixed_ex(K.OP_CHECKSUM, a, L, L, n, out, K.KERNEL_VSTREAM, 0, stream=s)),
-                ("vstream U2", lambda: ctx.batch_fixed_ex(K.OP_CHECKSUM, a, L, L, n, out, K.KERNEL_VSTREAM, 1,
-                                                          stream=s)),
-                ("vstream U8", lambda: ctx.batch_fixed_ex(K.OP_CHECKSUM, a, L, L, n, out, K.KERNEL_VSTREAM, 2,
-                                                          stream=s)),
                 ("vvstream fix", lambda: ctx.batch_fixed_ex(K.OP_CHECKSUM, a, L, L, n, out, K.KERNEL_VVSTREAM, 4,
                                                             stream=s)),
                 ("rstream U2", lambda: ctx.batch_fixed_ex(K.OP_CHECKSUM, a, L, L, n, out, K.KERNEL_RSTREAM, 1,
                                                           stream=s)),
-                ("var rvstream", lambda: ctx.batch_var_ex(K.OP_CHECKSUM, a, off, ln, n, out, K.KERNEL_RVSTREAM, 0,
-                                                          packed=True, stream=s)),
-                ("var stream", lambda: ctx.batch_var_ex(K.OP_CHECKSUM, a, off, ln, n, out, K.KERNEL_STREAM, 0,
-                                                        packed=True, stream=s)),
-                ("var span", lambda: ctx.batch_var_ex(K.OP_CHECKSUM, a, off, ln, n, out, K.KERNEL_SPAN, 0,
-                                                      packed=True, stream=s)),
                 ("var vvstream", lambda: ctx.batch_var_ex(K.OP_CHECKSUM, a, off, ln, n, out, K.KERNEL_VVSTREAM, 4,
                                                           packed=True, total_bytes=n * L, stream=s))]
         runs = []
@@ -116,12 +102,6 @@ def main():
         lay = dict(total_bytes=total, min_len=int(ln_np.min()), max_len=int(ln_np.max()), packed=True)
         cand = [("auto", lambda: ctx.batch_var(K.OP_CHECKSUM, a, off, ln, n, out, stream=s, **lay)),
                 ("seg", lambda: ctx.batch_var_ex(K.OP_CHECKSUM, a, off, ln, n, out, K.KERNEL_SEG, 0, stream=s, **lay)),
-                ("span", lambda: ctx.batch_var_ex(K.OP_CHECKSUM, a, off, ln, n, out, K.KERNEL_SPAN, 0, stream=s,
-                                                  **lay)),
-                ("stream", lambda: ctx.batch_var_ex(K.OP_CHECKSUM, a, off, ln, n, out, K.KERNEL_STREAM, 0, stream=s,
-                                                    **lay)),
-                ("rvstream", lambda: ctx.batch_var_ex(K.OP_CHECKSUM, a, off, ln, n, out, K.KERNEL_RVSTREAM, 0,
-                                                      stream=s, **lay)),
                 ("vvstream", lambda: ctx.batch_var_ex(K.OP_CHECKSUM, a, off, ln, n, out, K.KERNEL_VVSTREAM, 0,
                                                       stream=s, **lay)),
                 ("vvstream U8", lambda: ctx.batch_var_ex(K.OP_CHECKSUM, a, off, ln, n, out, K.KERNEL_VVSTREAM, 1,
@@ -129,8 +109,6 @@ def main():
                 ("vvstream pol", lambda: ctx.batch_var_ex(K.OP_CHECKSUM, a, off, ln, n, out, K.KERNEL_VVSTREAM, 4,
                                                           stream=s, **lay)),
                 ("vvstream cnt", lambda: ctx.batch_var_ex(K.OP_CHECKSUM, a, off, ln, n, out, K.KERNEL_VVSTREAM, 2,
-                                                          stream=s, **lay)),
-                ("rvstream cnt", lambda: ctx.batch_var_ex(K.OP_CHECKSUM, a, off, ln, n, out, K.KERNEL_RVSTREAM, 3,
                                                           stream=s, **lay))]
         runs = []
         for label, fn in cand:

@@ -41,9 +41,9 @@ def main():
     tiny = torch.zeros(1 << 12, dtype=torch.uint8, device="cuda")
     print("empty-ish launch (1 image):", time_launch(lambda: ctx.batch_fixed_ex(
         tcpck.OP_CHECKSUM, tiny, 1492, 1492, 1, out, tcpck.KERNEL_SEG, 2, stream=stream)), flush=True)
-    cases = [("stream U4 1492", 1492, tcpck.KERNEL_STREAM, 0), ("stream U2 1492", 1492, tcpck.KERNEL_STREAM, 3),
-             ("span T16 1492", 1492, tcpck.KERNEL_SPAN, 16), ("seg G16 1492", 1492, tcpck.KERNEL_SEG, 2),
-             ("seg G64U4 64K", 65536, tcpck.KERNEL_SEG, 3), ("stream U4 64K", 65536, tcpck.KERNEL_STREAM, 0)]
+    cases = [("rstream 1492", 1492, tcpck.KERNEL_RSTREAM, 10), ("vvstream 1492", 1492, tcpck.KERNEL_VVSTREAM, 4),
+             ("seg G16 1492", 1492, tcpck.KERNEL_SEG, 2), ("seg G64U4 64K", 65536, tcpck.KERNEL_SEG, 3),
+             ("vvstream 96", 96, tcpck.KERNEL_VVSTREAM, 4)]
     for name, L, k, p in cases:
         xs, ys = [], []
         for gb in (0.25, 0.5, 1, 1.5, 2, 4, 8, 16):

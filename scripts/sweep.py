@@ -46,16 +46,9 @@ def build(cfg):
 def variants(w):
     v = [("auto", tcpck.KERNEL_AUTO, 0)]
     v += [(f"seg {n}", tcpck.KERNEL_SEG, p) for p, n in tcpck.SEG_SHAPES.items()]
-    tiles = [4, 8, 12, 16, 24, 32, 48, 63] if w["fixed"] and w["L"] < 8192 else [16, 24, 33, 48, 63]
-    if w["fixed"] and w["L"] >= 8192:
-        tiles = [1, 2, 4]
-    v += [(f"span T{t}", tcpck.KERNEL_SPAN, t) for t in tiles]
-    if not (w["fixed"] and w["L"] > 16384):
-        v += [(f"stream {n}", tcpck.KERNEL_STREAM, p) for p, n in tcpck.STREAM_VARIANTS.items()]
+    v += [(f"vvstream v{p}", tcpck.KERNEL_VVSTREAM, p) for p in (0, 1, 2, 3, 4)]
     if w["fixed"] and w["L"] <= 16384:
         v += [(f"rstream v{p}", tcpck.KERNEL_RSTREAM, p) for p in (0, 1, 2, 9, 10, 11, 12, 13)]
-    if not w["fixed"]:
-        v += [(f"rvstream v{p}", tcpck.KERNEL_RVSTREAM, p) for p in (0, 1, 2)]
     return v
 
 

@@ -160,38 +160,35 @@ void free_stage(tcpck_ctx *ctx) {
 // everything else -- unordered offsets, gaps in variable layouts, RFC 1071
 // mode, jumbo images (where one wave per image already streams whole 1 KiB
 // steps) -- seg.
-constexpr uint64_t kSpanMaxLen = 16384;
+constexpr uint64_t kRunMaxLen = 16384;  // above: seg (one wave per jumbo image already streams whole steps)
 
 hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t stride, uint32_t len,
                      uint64_t count, void *out, int kernel, int param, hipStream_t s) {
-  const bool span_ok = mode == TCPCK_MODE_REF && stride == len && len >= 16 && len <= (1u << 24);
-  // packed fixed stride, reference mode, by image length (scripts/policy_sweep.py,
-  // profiles/r01/policy_small.log): below 512 B boundaries are dense enough
-  // that resolving all of a step's ends in parallel from the prefix table
-  // (vvstream, FIXED) wins (+3-4% over vstream U8 at 32-256 B); from 512 B the
-  // run-stream kernel's scalar boundary walk (~87% of the HBM roof on C2 at
-  // 32x oversubscription); jumbo images stay on seg (G64/U4), which streams
-  // whole images per wave at the same rate.  FILL below 30 B is not defined.
-  // gapped fixed strides (stride > len, e.g. MSS slots), reference mode
-  // (scripts/gap_probe.py, profiles/r01/gap_probe.log): streaming the gaps with
-  // the images (vvstream, virtual gap images) wins while they are small --
-  // 128/96 B 57% of the roof for image bytes vs seg's 39% -- else seg with
-  // 8 lanes per image (1536/1492 B 81% vs 77% for the length-based shape)
-  if (kernel == TCPCK_KERNEL_AUTO && mode == TCPCK_MODE_REF && stride > len && len >= 2 && len <= kSpanMaxLen) {
-    const uint64_t l = len;
-    const bool hull = len < 512 ? stride <= 2 * l : (len < 1024 ? 4 * stride <= 5 * l : 16 * stride <= 17 * l);
-    if (hull && stride <= (1u << 24) && (op != TCPCK_OP_FILL || len >= 30)) {
-      kernel = TCPCK_KERNEL_VVSTREAM;
-      param = 4;
-    } else {
-      kernel = TCPCK_KERNEL_SEG;
-      param = tcpck::kShapeSmall + 1;
-    }
-  }
+  const uint32_t num_cus = static_cast<uint32_t>(ctx->num_cus);
   if (kernel == TCPCK_KERNEL_AUTO) {
-    if (!span_ok || len > kSpanMaxLen) {
+    if (mode != TCPCK_MODE_REF || len < 2 || len > kRunMaxLen || stride > (1u << 24)) {
       kernel = TCPCK_KERNEL_SEG;
+    } else if (stride > len) {
+      // gapped fixed strides (e.g. MSS slots) (scripts/gap_probe.py,
+      // profiles/r01/gap_probe.log): streaming the gaps with the images
+      // (vvstream, virtual gap images) wins while they are small -- 128/96 B
+      // 57% of the roof for image bytes vs seg's 39% -- else seg with 8 lanes
+      // per image (1536/1492 B 81% vs 77% for the length-based shape)
+      const uint64_t l = len;
+      const bool hull = len < 512 ? stride <= 2 * l : (len < 1024 ? 4 * stride <= 5 * l : 16 * stride <= 17 * l);
+      if (hull && (op != TCPCK_OP_FILL || len >= 30)) {
+        kernel = TCPCK_KERNEL_VVSTREAM;
+        param = 4;
+      } else {
+        kernel = TCPCK_KERNEL_SEG;
+        param = tcpck::kShapeSmall + 1;
+      }
     } else if (len < 512) {
+      // packed, by image length (scripts/policy_sweep.py, profiles/r01/policy_small.log):
+      // below 512 B boundaries are dense enough that resolving all of a step's
+      // ends in parallel from the prefix table wins (vvstream FIXED, 73-81% at
+      // 32-256 B); from 512 B the scalar boundary walk (rstream: ~87% of the
+      // HBM roof on C2 at 32x oversubscription)
       kernel = (op == TCPCK_OP_FILL && len < 30) ? TCPCK_KERNEL_SEG : TCPCK_KERNEL_VVSTREAM;
       param = 4;
     } else {
@@ -199,39 +196,8 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
       param = 10;  // v_dot2 chunk sums, buffer loads (C2 +0.5%, profiles/r01/b2b_c2c3.log)
     }
   }
-  if (kernel == TCPCK_KERNEL_SPAN) {
-    if (!span_ok) return hipErrorInvalidValue;
-    tcpck::SpanArgs a{};
-    a.arena = arena;
-    a.stride = stride;
-    a.count = count;
-    a.out = out;
-    a.tile = param > 0 ? static_cast<uint32_t>(param) : tcpck::span_tile_for_len(len);
-    return tcpck::launch_span(op, true, a, static_cast<uint32_t>(ctx->num_cus), s);
-  }
-  if (kernel == TCPCK_KERNEL_STREAM) {
-    if (!span_ok) return hipErrorInvalidValue;
-    tcpck::SpanArgs a{};
-    a.arena = arena;
-    a.stride = stride;
-    a.count = count;
-    a.out = out;
-    return tcpck::launch_stream(op, true, param, a, static_cast<uint32_t>(ctx->num_cus), s);
-  }
-  if (kernel == TCPCK_KERNEL_FSTREAM) {
-    if (!span_ok || len > (1u << 20)) return hipErrorInvalidValue;
-    const int variant = (param >> 16) & 0xFF;
-    const uint32_t tile = static_cast<uint32_t>(param & 0xFFFF);
-    tcpck::FixedStreamArgs a{};
-    a.arena = arena;
-    a.stride = stride;
-    a.count = count;
-    a.out = out;
-    a.tile = tile ? tile : tcpck::fstream_tile_for_len(len, variant);
-    return tcpck::launch_fstream(op, variant, a, static_cast<uint32_t>(ctx->num_cus), s);
-  }
   if (kernel == TCPCK_KERNEL_RSTREAM) {
-    if (!span_ok) return hipErrorInvalidValue;
+    if (mode != TCPCK_MODE_REF || stride != len || len < 16 || len > (1u << 24)) return hipErrorInvalidValue;
     tcpck::FixedStreamArgs a{};
     a.arena = arena;
     a.stride = stride;
@@ -240,29 +206,19 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
     a.dbg = static_cast<uint64_t *>(ctx->dbg);
     a.blocks_per_cu = static_cast<uint32_t>(param >> 8) & 0xFFu;
     a.oversub = static_cast<uint32_t>(param >> 16) & 0xFFu;
-    return tcpck::launch_rstream(op, param & 0xFF, a, static_cast<uint32_t>(ctx->num_cus), s);
+    return tcpck::launch_rstream(op, param & 0xFF, a, num_cus, s);
   }
   if (kernel == TCPCK_KERNEL_VVSTREAM) {  // any even length: the prefix table takes any number of ends per step
     if (mode != TCPCK_MODE_REF || len == 0 || stride > (1u << 24) || (op == TCPCK_OP_FILL && len < 30))
       return hipErrorInvalidValue;
-    tcpck::SpanArgs a{};
+    tcpck::RunArgs a{};
     a.arena = arena;
     a.stride = stride;
     a.len = len;
     a.count = count;
     a.out = out;
     a.oversub = static_cast<uint32_t>(param >> 16) & 0xFFu;
-    return tcpck::launch_vvstream(op, param & 0xFF, true, a, static_cast<uint32_t>(ctx->num_cus), s);
-  }
-  if (kernel == TCPCK_KERNEL_VSTREAM) {
-    if (!span_ok) return hipErrorInvalidValue;
-    tcpck::FixedStreamArgs a{};
-    a.arena = arena;
-    a.stride = stride;
-    a.count = count;
-    a.out = out;
-    a.oversub = static_cast<uint32_t>(param >> 16) & 0xFFu;
-    return tcpck::launch_vstream(op, param & 0xFF, a, static_cast<uint32_t>(ctx->num_cus), s);
+    return tcpck::launch_vvstream(op, param & 0xFF, true, a, num_cus, s);
   }
   if (kernel != TCPCK_KERNEL_SEG) return hipErrorInvalidValue;
   SegArgs a{};
@@ -273,7 +229,7 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
   a.out = out;
   a.oversub = static_cast<uint32_t>(param >> 16) & 0xFFu;
   const auto shape = (param & 0xFF) > 0 ? static_cast<tcpck::SegShape>((param & 0xFF) - 1) : tcpck::shape_for_len(len);
-  return tcpck::launch_seg(op, mode, true, shape, a, static_cast<uint32_t>(ctx->num_cus), s);
+  return tcpck::launch_seg(op, mode, true, shape, a, num_cus, s);
 }
 
 hipError_t run_var(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const uint64_t *off, const uint32_t *len,
@@ -281,36 +237,20 @@ hipError_t run_var(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const uint6
                    hipStream_t s) {
   const uint64_t typical = (layout && layout->total_bytes) ? layout->total_bytes / count : 1500;
   const bool packed = mode == TCPCK_MODE_REF && layout && (layout->flags & TCPCK_LAYOUT_PACKED);
-  // packed, reference mode: checksum / verify on vvstream (any image lengths;
-  // C3 85% at 32x oversubscription, profiles/r01/oversub_c2c3.log); fill on
-  // span, whose one-end-per-chunk hand-off needs images >= 16 B
+  // packed, reference mode: vvstream for every op (any image lengths; C3 85.9%
+  // at 32x oversubscription, profiles/r01/c3_bench_vv_u8x32_settle.log); a
+  // wrong packed hint costs speed, never correctness (waves re-check)
   if (kernel == TCPCK_KERNEL_AUTO) {
-    if (!packed || typical > kSpanMaxLen)
+    if (!packed || typical > kRunMaxLen || (op == TCPCK_OP_FILL && layout->min_len != 0 && layout->min_len < 30)) {
       kernel = TCPCK_KERNEL_SEG;
-    else if (op == TCPCK_OP_FILL)
-      kernel = (layout->min_len == 0 || layout->min_len >= 16) ? TCPCK_KERNEL_SPAN : TCPCK_KERNEL_SEG;
-    else {
+    } else {
       kernel = TCPCK_KERNEL_VVSTREAM;
       param = 4;
     }
   }
-  if (kernel == TCPCK_KERNEL_SPAN) {
-    // the kernel re-checks packing and lengths per tile, so a wrong hint
-    // costs speed, never correctness
-    if (mode != TCPCK_MODE_REF) return hipErrorInvalidValue;
-    tcpck::SpanArgs a{};
-    a.arena = arena;
-    a.offsets = off;
-    a.lengths = len;
-    a.base = base;
-    a.count = count;
-    a.out = out;
-    a.tile = param > 0 ? static_cast<uint32_t>(param) : tcpck::span_tile_for_len(typical);
-    return tcpck::launch_span(op, false, a, static_cast<uint32_t>(ctx->num_cus), s);
-  }
   if (kernel == TCPCK_KERNEL_VVSTREAM) {
     if (mode != TCPCK_MODE_REF) return hipErrorInvalidValue;
-    tcpck::SpanArgs a{};
+    tcpck::RunArgs a{};
     a.arena = arena;
     a.offsets = off;
     a.lengths = len;
@@ -320,32 +260,6 @@ hipError_t run_var(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const uint6
     a.oversub = static_cast<uint32_t>(param >> 16) & 0xFFu;
     a.total_bytes = layout ? layout->total_bytes : 0;
     return tcpck::launch_vvstream(op, param & 0xFF, false, a, static_cast<uint32_t>(ctx->num_cus), s);
-  }
-  if (kernel == TCPCK_KERNEL_RVSTREAM) {
-    // offsets ascending and packed (the layout hint); a wave whose length walk
-    // disagrees with the offsets recomputes its images one by one
-    if (mode != TCPCK_MODE_REF) return hipErrorInvalidValue;
-    tcpck::SpanArgs a{};
-    a.arena = arena;
-    a.offsets = off;
-    a.lengths = len;
-    a.base = base;
-    a.count = count;
-    a.out = out;
-    return tcpck::launch_rvstream(op, param, a, static_cast<uint32_t>(ctx->num_cus), s);
-  }
-  if (kernel == TCPCK_KERNEL_STREAM) {
-    // offsets must be ascending (the run split searches them); each wave
-    // re-validates packing of its run and falls back per image if it fails
-    if (mode != TCPCK_MODE_REF) return hipErrorInvalidValue;
-    tcpck::SpanArgs a{};
-    a.arena = arena;
-    a.offsets = off;
-    a.lengths = len;
-    a.base = base;
-    a.count = count;
-    a.out = out;
-    return tcpck::launch_stream(op, false, param, a, static_cast<uint32_t>(ctx->num_cus), s);
   }
   if (kernel != TCPCK_KERNEL_SEG) return hipErrorInvalidValue;
   SegArgs a{};

@@ -305,6 +305,15 @@ __device__ __forceinline__ void count_split(uint64_t wid, uint64_t q, uint64_t r
   ke = kb + q + (wid < r ? 1u : 0u);
 }
 
+// XCD-aware block order (bijective for any grid): blocks b and b + 8 share an
+// XCD (round-robin dispatch; MI355X_MICROARCH.md, Workgroup dispatch), so
+// the blocks labelled x = b % 8 get one contiguous range of logical ids.
+// Speed only: correctness never depends on where a block runs.
+__device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb) {
+  const uint32_t q = nb >> 3, r = nb & 7u, x = b & 7u;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
+}
+
 // SPLIT 0: byte-balanced runs (two 64-ary searches over the offsets);
 // SPLIT 1: equal image counts (no search; balance only statistical) -- tuning.
 

@@ -1,5 +1,6 @@
 // tcpck_internal.h -- private interface between the C-ABI layer (tcpck_api.hip)
-// and the gfx950 kernels (tcpck_kernels.hip, tcpck_span.hip).  Not installed.
+// and the gfx950 kernels (tcpck_kernels.hip, tcpck_rstream.hip, tcpck_vvstream.hip).
+// Not installed.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -37,65 +38,45 @@ SegShape shape_for_len(uint64_t typical_len);
 hipError_t launch_seg(int op, int mode, bool fixed, SegShape shape, const SegArgs &a,
                       uint32_t num_cus, hipStream_t stream);
 
-// ---- span kernel: packed layouts, reference mode, tiles of whole images ------
-struct SpanArgs {
+// ---- run kernels: one contiguous run of whole images per wave ---------------
+// Packed and fixed layouts for vvstream (tcpck_vvstream.hip).
+struct RunArgs {
   uint8_t *arena;
   const uint64_t *offsets;   // variable layout (packed: offsets[k+1] == offsets[k] + lengths[k])
   const uint32_t *lengths;
-  uint64_t stride;           // fixed layout: stride == image length (packed)
-  uint64_t base;
+  uint64_t stride;           // fixed layouts: image k at k * stride
+  uint32_t len;              // fixed layouts: image length (<= stride)
+  uint64_t base;             // subtracted from offsets[k] (chunked host batches)
   uint64_t count;
   void *out;
-  uint32_t tile;             // images per wave tile, 1..63
-  uint32_t oversub;          // grid = resident blocks x this (run-stream kernels; 0 = by size)
+  uint32_t oversub;          // grid = resident blocks x this (0 = by size)
   uint64_t total_bytes;      // batch byte span hint (0 = unknown)
-  uint32_t len;              // fixed layouts: image length (vvstream: <= stride)
 };
 
-uint32_t span_tile_for_len(uint64_t typical_len);
-hipError_t launch_span(int op, bool fixed, const SpanArgs &a, uint32_t num_cus, hipStream_t stream);
-
-}  // namespace tcpck
-
-namespace tcpck {
-// ---- stream kernel: packed layouts, reference mode, one byte-balanced run per wave
-// variant: 0 = U4/nt (default), 1 = U8/nt, 2 = U4/plain loads, 3 = U2/nt
-hipError_t launch_stream(int op, bool fixed, int variant, const SpanArgs &a, uint32_t num_cus,
-                         hipStream_t stream);
-
-// ---- fixed-stride stream kernel: packed fixed stride (stride == len >= 16),
-// reference mode, interleaved tiles, arithmetic boundaries
+// Fixed stride == len for rstream (tcpck_rstream.hip).
 struct FixedStreamArgs {
   uint8_t *arena;
   uint64_t stride;  // == image length
   uint64_t count;
   void *out;
-  uint32_t tile;    // images per tile (>= fstream_min_tile)
   uint64_t *dbg;    // optional per-wave {start, end} s_memrealtime stamps (timing builds)
   uint32_t blocks_per_cu;  // optional occupancy cap (0 = as many as fit)
   uint32_t oversub;        // grid = resident blocks x this (0 = by size, 1 = none)
   uint64_t per_wave;       // run split, set by the launcher: count = per_wave * waves + rem,
   uint64_t rem;            // wave w owns per_wave + (w < rem) images (no 64-bit division on device)
 };
-// ---- run-stream kernel (fixed stride == len): one run per wave, scalar boundaries
-// variant: 0 = 4 loads in flight, 1 = 2, 2 = 8, 3 = 4 with per-wave time stamps
+
+// ---- rstream (fixed stride == len): one run per wave, scalar boundary walk.
+// variant: 0 = 4 loads in flight, 1 = 2, 2 = 8, 3 = 4 with per-wave time stamps,
+// 4-8 issue-priority experiments, 9-13 v_dot2 sums and/or buffer loads (10 = policy)
 hipError_t launch_rstream(int op, int variant, const FixedStreamArgs &a, uint32_t num_cus, hipStream_t stream);
-// ---- vector-boundary run stream (fixed stride == len, small images), MODE_REF:
-// variant = loads in flight (0: 4, 1: 2, 2: 8)
-hipError_t launch_vstream(int op, int variant, const FixedStreamArgs &a, uint32_t num_cus, hipStream_t stream);
-// ---- run-stream kernel for packed variable layouts (tcpck_rvstream.hip), MODE_REF:
-// variant = loads in flight (0: 4, 1: 2, 2: 8) | blocks-per-CU cap << 8
-hipError_t launch_rvstream(int op, int variant, const SpanArgs &a, uint32_t num_cus, hipStream_t stream);
-// ---- prefix-table run stream (tcpck_vvstream.hip), MODE_REF, all ops: packed
-// variable layouts (fixed = false) or fixed strides (fixed = true: a.stride >= a.len).
+// ---- vvstream (prefix table), MODE_REF, all ops: packed variable layouts
+// (fixed = false) or fixed strides (fixed = true: a.stride >= a.len).
 // variant 0 U4 byte split, 1 U8, 2 U4 count split, 3 U8 (fixed: 0/2 U4, 1/3 U8),
 // 4 = policy (oversubscription, split and loads in flight by size)
-hipError_t launch_vvstream(int op, int variant, bool fixed, const SpanArgs &a, uint32_t num_cus, hipStream_t stream);
+hipError_t launch_vvstream(int op, int variant, bool fixed, const RunArgs &a, uint32_t num_cus, hipStream_t stream);
 // timing-only streaming micro-kernels (tcpck_diag.hip)
 hipError_t launch_diag_stream(int variant, const uint8_t *buf, uint64_t bytes, uint32_t *out, uint32_t num_cus,
                               hipStream_t s);
-uint32_t fstream_min_tile(uint32_t stride, int variant);
-uint32_t fstream_tile_for_len(uint32_t stride, int variant);
-// variant: 0 = 4 loads in flight per lane, 1 = 2
-hipError_t launch_fstream(int op, int variant, const FixedStreamArgs &a, uint32_t num_cus, hipStream_t stream);
+
 }  // namespace tcpck

@@ -7,7 +7,8 @@
 //
 // This kernel accepts every layout the C ABI allows (fixed stride with gaps,
 // arbitrary even offsets/lengths in any order, zero-length images, both
-// modes); the packed-layout fast path is the span kernel (tcpck_span.hip).
+// modes); the packed-layout fast paths are the run kernels (tcpck_rstream.hip,
+// tcpck_vvstream.hip).
 // Shape of the work: a pure HBM-read streaming reduction (~0.5 integer add per
 // byte, no MFMA):
 //   * G consecutive lanes own one image; lane l of the group reads the image's

@@ -327,7 +327,7 @@ __global__ void __launch_bounds__(kBlock) vvstream_kernel(VVArgs a) {
 }
 
 template <int U, int OP, int SPLIT, int LAYOUT>
-hipError_t launch_one(const SpanArgs &s, uint32_t oversub, uint32_t num_cus, hipStream_t stream) {
+hipError_t launch_one(const RunArgs &s, uint32_t oversub, uint32_t num_cus, hipStream_t stream) {
   static const uint32_t per_cu = dev::resident_blocks_per_cu(vvstream_kernel<U, OP, SPLIT, LAYOUT>);
   const uint64_t resident = static_cast<uint64_t>(per_cu) * num_cus;
   uint64_t blocks = resident * (oversub ? oversub : 1);
@@ -351,7 +351,7 @@ hipError_t launch_one(const SpanArgs &s, uint32_t oversub, uint32_t num_cus, hip
 }
 
 template <int U, int SPLIT, int LAYOUT>
-hipError_t dispatch(int op, const SpanArgs &a, uint32_t oversub, uint32_t num_cus, hipStream_t s) {
+hipError_t dispatch(int op, const RunArgs &a, uint32_t oversub, uint32_t num_cus, hipStream_t s) {
   switch (op) {
     case kChecksum: return launch_one<U, kChecksum, SPLIT, LAYOUT>(a, oversub, num_cus, s);
     case kVerify: return launch_one<U, kVerify, SPLIT, LAYOUT>(a, oversub, num_cus, s);
@@ -362,7 +362,7 @@ hipError_t dispatch(int op, const SpanArgs &a, uint32_t oversub, uint32_t num_cu
 
 }  // namespace
 
-hipError_t launch_vvstream(int op, int variant, bool fixed, const SpanArgs &a, uint32_t num_cus,
+hipError_t launch_vvstream(int op, int variant, bool fixed, const RunArgs &a, uint32_t num_cus,
                            hipStream_t stream) {
   if (a.count == 0) return hipSuccess;
   if (fixed && (a.len == 0 || a.stride < a.len || a.stride > (1u << 24))) return hipErrorInvalidValue;

@@ -38,14 +38,8 @@ LAYOUT_PACKED = 1
 # include/tcpck_tuning.h
 KERNEL_AUTO = 0
 KERNEL_SEG = 1    # param: seg shape + 1 (1..6), 0 = by length
-KERNEL_SPAN = 2   # param: images per tile (1..63), 0 = by length
-KERNEL_STREAM = 3  # param: variant 0 (U4 nt), 1 (U8 nt), 2 (U4 plain), 3 (U2 nt)
-STREAM_VARIANTS = {0: "U4/nt", 1: "U8/nt", 2: "U4/plain", 3: "U2/nt"}
-KERNEL_FSTREAM = 4  # fixed stride == len: param = tile (low 16 bits, 0 = auto) | variant << 16
-KERNEL_RSTREAM = 5  # fixed stride == len: param = variant 0 (U4), 1 (U2), 2 (U8), 3 (U4 + stamps)
-KERNEL_VSTREAM = 7   # fixed stride == len >= 16: param = variant 0 (U4), 1 (U2), 2 (U8)
-KERNEL_VVSTREAM = 8  # packed variable layouts, checksum/verify: param = 0 U4, 1 U8, 2/3 count split, 5-8 prefix table, 4 policy
-KERNEL_RVSTREAM = 6  # packed variable layouts: param = variant 0 (U4), 1 (U2), 2 (U8) | cap << 8
+KERNEL_RSTREAM = 5  # fixed stride == len: param = variant (10 = policy) | cap << 8 | oversub << 16
+KERNEL_VVSTREAM = 8  # packed variable or fixed (stride >= len): param = 0/1 U4/U8 byte split, 2/3 count split, 4 policy | oversub << 16
 SEG_SHAPES = {1: "G8/U2", 2: "G16/U6", 3: "G64/U4", 4: "G64/U2", 5: "G32/U3", 6: "G4/U8"}
 TUNING_EXPORTS = ("tcpck_batch_fixed_ex", "tcpck_batch_var_ex", "tcpck_ctx_set_debug", "tcpck_diag_stream")
 

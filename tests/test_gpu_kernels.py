@@ -1,6 +1,8 @@
-"""GPU parity of every kernel variant (include/tcpck_tuning.h): each seg shape
-and span tile size must give the reference's answers bit for bit, including the
-span kernel's in-launch fallback for tiles that are not packed."""
+"""GPU parity of every kernel and variant (include/tcpck_tuning.h) against the
+reference's golden vectors and the oracle: seg (each shape), rstream (each
+variant) and vvstream (each variant; packed variable, fixed and gapped fixed
+layouts), all three ops, misaligned arenas, wrong layout hints, tiny and empty
+images, and grid oversubscription."""
 import numpy as np
 import pytest
 
@@ -9,8 +11,8 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 SEG = [1, 2, 3, 4, 5, 6]
-TILES = [1, 2, 7, 16, 33, 63]
-STREAM = [0, 1, 2, 3]
+RSTREAM = [0, 1, 2, 9, 10, 11, 12, 13]  # 9-13: v_dot2 sums and/or buffer loads
+VVSTREAM = [0, 1, 2, 3, 4]  # 0/1 byte split U4/U8, 2/3 count split, 4 policy
 
 
 @pytest.fixture(scope="module")
@@ -31,15 +33,38 @@ def host(t):
     return t.cpu().numpy()
 
 
-def variants():
+def var_kernels():
     import tcpck
-    return ([(tcpck.KERNEL_SEG, p) for p in SEG] + [(tcpck.KERNEL_SPAN, t) for t in TILES]
-            + [(tcpck.KERNEL_STREAM, v) for v in STREAM])
+    return [(tcpck.KERNEL_SEG, p) for p in SEG] + [(tcpck.KERNEL_VVSTREAM, v) for v in VVSTREAM]
 
 
-def packed_golden(golden):
-    """All golden checksum images of length >= 16, re-packed back to back."""
-    cases = [c for c in golden.by_kind("checksum") if c["len"] >= 16]
+def fixed_kernels():
+    import tcpck
+    return var_kernels() + [(tcpck.KERNEL_RSTREAM, v) for v in RSTREAM]
+
+
+def packed_layout(count, seed, payloads, header=32):
+    rng = np.random.default_rng(seed)
+    ln = (np.asarray(payloads, np.int64)[rng.integers(0, len(payloads), count)] + header).astype(np.uint32)
+    off = np.zeros(count, np.uint64)
+    if count > 1:
+        off[1:] = np.cumsum(ln[:-1].astype(np.uint64))
+    return off, ln, int(ln.astype(np.int64).sum())
+
+
+def _fill_oracle(arena_np, off, ln):
+    exp_arena = arena_np.copy()
+    exp = np.empty(len(off), np.uint16)
+    from oracle import ref16 as R
+    for k in range(len(off)):
+        o, n = int(off[k]), int(ln[k])
+        exp[k] = R.fill_np(exp_arena[o:o + n])
+    return exp, exp_arena
+
+
+def packed_golden(golden, min_len=16):
+    """Golden checksum images of length >= min_len, re-packed back to back."""
+    cases = [c for c in golden.by_kind("checksum") if c["len"] >= min_len]
     imgs = [golden.image(c) for c in cases]
     ln = np.array([c["len"] for c in cases], np.uint32)
     off = np.zeros(len(cases), np.uint64)
@@ -47,7 +72,8 @@ def packed_golden(golden):
     return np.concatenate(imgs), off, ln, np.array([c["expected"] for c in cases], np.uint16)
 
 
-@pytest.mark.parametrize("kernel,param", variants())
+# ---- every kernel ----------------------------------------------------------
+@pytest.mark.parametrize("kernel,param", var_kernels())
 def test_packed_golden_all_kernels(ctx, golden, kernel, param):
     import tcpck
     arena, off, ln, exp = packed_golden(golden)
@@ -57,7 +83,18 @@ def test_packed_golden_all_kernels(ctx, golden, kernel, param):
     np.testing.assert_array_equal(host(out).view(np.uint16), exp)
 
 
-@pytest.mark.parametrize("kernel,param", variants())
+@pytest.mark.parametrize("variant", VVSTREAM)
+def test_vvstream_golden_all_lengths(ctx, golden, variant):
+    """Every golden checksum image (0..65536 B, incl. < 16 B and empty) packed back to back."""
+    import tcpck
+    arena, off, ln, exp = packed_golden(golden, min_len=0)
+    out = torch.empty(len(exp), dtype=torch.int16, device="cuda")
+    ctx.batch_var_ex(tcpck.OP_CHECKSUM, dev(arena), dev(off), dev(ln), len(exp), out, tcpck.KERNEL_VVSTREAM,
+                     variant, packed=True)
+    np.testing.assert_array_equal(host(out).view(np.uint16), exp)
+
+
+@pytest.mark.parametrize("kernel,param", fixed_kernels())
 @pytest.mark.parametrize("length", [16, 32, 96, 606, 1492, 1494, 4096])
 def test_fixed_packed_all_kernels(ctx, oracle_c, kernel, param, length):
     import tcpck
@@ -71,7 +108,7 @@ def test_fixed_packed_all_kernels(ctx, oracle_c, kernel, param, length):
     np.testing.assert_array_equal(host(out).view(np.uint16), exp)
 
 
-@pytest.mark.parametrize("kernel,param", variants())
+@pytest.mark.parametrize("kernel,param", fixed_kernels())
 @pytest.mark.parametrize("mis", [2, 6, 14])
 def test_misaligned_arena_pointer(ctx, oracle_c, kernel, param, mis):
     """The arena pointer itself need not be 16-B aligned (e.g. a sliced buffer)."""
@@ -85,24 +122,22 @@ def test_misaligned_arena_pointer(ctx, oracle_c, kernel, param, mis):
     ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, ptr, L, L, count, out, kernel, param)
     exp = oracle_c.batch(arena_np[mis:], stride=L, length=L, count=count)
     np.testing.assert_array_equal(host(out).view(np.uint16), exp)
+    if kernel == tcpck.KERNEL_RSTREAM:
+        return  # fixed layouts only
     off = (np.arange(count, dtype=np.uint64) * L)
     ln = np.full(count, L, np.uint32)
     ctx.batch_var_ex(tcpck.OP_CHECKSUM, ptr, dev(off), dev(ln), count, out, kernel, param, packed=True)
     np.testing.assert_array_equal(host(out).view(np.uint16), exp)
 
 
-MIXED = [(2, t) for t in TILES] + [(3, v) for v in STREAM]
-
-
-@pytest.mark.parametrize("kernel,tile", MIXED)
-def test_span_var_mixed_and_fallback(ctx, oracle_c, kernel, tile):
-    """Packed C3-style batch with some non-packed and short regions mixed in."""
+@pytest.mark.parametrize("kernel,param", var_kernels())
+def test_var_mixed_with_gaps_and_short_images(ctx, oracle_c, kernel, param):
+    """Packed C3-style batch with a wrong packed hint (a few gaps) and images below 16 B."""
     import tcpck
     import synth_np
-    rng = np.random.default_rng(tile + 100 * kernel)
+    rng = np.random.default_rng(param + 100 * kernel)
     count = 20000
-    off, ln, total = synth_np.mixed_layout(count, seed=tile)
-    # break packing in a few places (gaps) and shrink a few images below 16 B
+    off, ln, total = synth_np.mixed_layout(count, seed=param)
     off = off.copy()
     ln = ln.copy()
     for k in rng.integers(1, count, 40):
@@ -111,160 +146,30 @@ def test_span_var_mixed_and_fallback(ctx, oracle_c, kernel, tile):
     total = int(off[-1] + ln[-1]) + 64
     arena_np = rng.integers(0, 256, total, dtype=np.uint8)
     out = torch.empty(count, dtype=torch.int16, device="cuda")
-    ctx.batch_var_ex(tcpck.OP_CHECKSUM, dev(arena_np), dev(off), dev(ln), count, out,
-                     kernel, tile, packed=True)
-    exp = oracle_c.batch(arena_np, off, ln, threads=8)
-    np.testing.assert_array_equal(host(out).view(np.uint16), exp)
+    ctx.batch_var_ex(tcpck.OP_CHECKSUM, dev(arena_np), dev(off), dev(ln), count, out, kernel, param, packed=True)
+    np.testing.assert_array_equal(host(out).view(np.uint16), oracle_c.batch(arena_np, off, ln, threads=8))
 
 
-@pytest.mark.parametrize("variant", STREAM)
-@pytest.mark.parametrize("count", [1, 2, 63, 64, 65, 127, 129, 1000, 70000])
-def test_stream_var_sizes(ctx, oracle_c, variant, count):
-    """Byte-balanced run split at every size, including fewer images than waves."""
-    import tcpck
-    import synth_np
-    off, ln, total = synth_np.mixed_layout(count, seed=count, payloads=(0, 64, 576, 1460, 9000))
-    rng = np.random.default_rng(count)
-    arena_np = rng.integers(0, 256, total + 16, dtype=np.uint8)
-    out = torch.empty(count, dtype=torch.int16, device="cuda")
-    ctx.batch_var_ex(tcpck.OP_CHECKSUM, dev(arena_np), dev(off), dev(ln), count, out,
-                     tcpck.KERNEL_STREAM, variant, packed=True)
-    np.testing.assert_array_equal(host(out).view(np.uint16), oracle_c.batch(arena_np, off, ln))
-    if count > 1:
-        out2 = torch.empty(count, dtype=torch.int16, device="cuda")
-        L = 16
-        ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, dev(arena_np), L, L, min(count, total // L), out2,
-                           tcpck.KERNEL_STREAM, variant)
-        n = min(count, total // L)
-        np.testing.assert_array_equal(host(out2).view(np.uint16)[:n],
-                                      oracle_c.batch(arena_np, stride=L, length=L, count=n))
-
-
-FV = [(2, t) for t in (1, 16, 63)] + [(3, v) for v in STREAM]
-
-
-@pytest.mark.parametrize("kernel,tile", FV)
-@pytest.mark.parametrize("fixed", [True, False])
-def test_span_fill_verify(ctx, oracle_c, kernel, tile, fixed):
-    import tcpck
-    import synth_np
-    from oracle import ref16 as R
-    rng = np.random.default_rng(50 + tile + 7 * kernel)
-    if fixed:
-        L, count = 1492, 4000
-        off = (np.arange(count, dtype=np.uint64) * L)
-        ln = np.full(count, L, np.uint32)
-        total = L * count
-    else:
-        count = 4000
-        off, ln, total = synth_np.mixed_layout(count, seed=tile)
-    arena_np = rng.integers(0, 256, total, dtype=np.uint8)
-    arena = dev(arena_np)
-    out = torch.empty(count, dtype=torch.int16, device="cuda")
-    if fixed:
-        ctx.batch_fixed_ex(tcpck.OP_FILL, arena, L, L, count, out, kernel, tile)
-    else:
-        ctx.batch_var_ex(tcpck.OP_FILL, arena, dev(off), dev(ln), count, out, kernel, tile,
-                         packed=True)
-    got = host(arena)
-    exp_arena = arena_np.copy()
-    exp = np.empty(count, np.uint16)
-    for k in range(count):
-        o, n = int(off[k]), int(ln[k])
-        exp[k] = R.fill_np(exp_arena[o:o + n])
-    np.testing.assert_array_equal(host(out).view(np.uint16), exp)
-    np.testing.assert_array_equal(got, exp_arena)
-    ok = torch.empty(count, dtype=torch.uint8, device="cuda")
-    bad = rng.choice(count, 50, replace=False)
-    for k in bad:
-        got[int(off[k]) + int(rng.integers(0, int(ln[k])))] ^= 0x11
-    arena2 = dev(got)
-    if fixed:
-        ctx.batch_fixed_ex(tcpck.OP_VERIFY, arena2, L, L, count, ok, kernel, tile)
-    else:
-        ctx.batch_var_ex(tcpck.OP_VERIFY, arena2, dev(off), dev(ln), count, ok, kernel, tile,
-                         packed=True)
-    np.testing.assert_array_equal(np.nonzero(host(ok) == 0)[0], np.unique(bad))
-
-
-def test_span_rejects_rfc_and_gaps(ctx):
-    import tcpck
-    a = torch.zeros(1 << 16, dtype=torch.uint8, device="cuda")
-    o = torch.zeros(64, dtype=torch.int16, device="cuda")
-    with pytest.raises(tcpck.TcpckError):
-        ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, a, 1000, 1000, 8, o, tcpck.KERNEL_SPAN, 4, mode=1)
-    with pytest.raises(tcpck.TcpckError):
-        ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, a, 1000, 996, 8, o, tcpck.KERNEL_SPAN, 4)
-    with pytest.raises(tcpck.TcpckError):
-        ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, a, 1000, 1000, 8, o, tcpck.KERNEL_SPAN, 64)
-
-
-# ---- fixed-stride stream kernel (KERNEL_FSTREAM = 4: fixed stride == len only) ----
-FSTREAM = [(0, 0), (1 << 16, 0), (0, 3), (0, 5), (1 << 16, 2), (0, 64)]  # (variant << 16, tile)
-
-
-@pytest.mark.parametrize("vt", FSTREAM)
-@pytest.mark.parametrize("length", [16, 30, 32, 96, 606, 1024, 1026, 1492, 1494, 4096, 9000, 65536])
-@pytest.mark.parametrize("count", [1, 7, 3001])
-def test_fstream_fixed_vs_oracle(ctx, oracle_c, vt, length, count):
-    import tcpck
-    variant, tile = vt
-    lo = (4 if variant == 0 else 2) * 1024
-    if tile and tile * length < lo:
-        pytest.skip("tile shorter than the load ring (rejected by design)")
-    rng = np.random.default_rng(length * 3 + count + tile)
-    arena_np = rng.integers(0, 256, count * length + 32, dtype=np.uint8)
-    arena_np[:length] = 0xFF
-    buf = dev(arena_np)
-    for mis in (0, 2, 14):
-        out = torch.empty(count, dtype=torch.int16, device="cuda")
-        ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, buf.data_ptr() + mis, length, length, count, out,
-                           tcpck.KERNEL_FSTREAM, variant | tile)
-        exp = oracle_c.batch(arena_np[mis:], stride=length, length=length, count=count)
-        np.testing.assert_array_equal(host(out).view(np.uint16), exp)
-
-
-@pytest.mark.parametrize("vt", [(0, 0), (1 << 16, 0), (0, 3)])
-@pytest.mark.parametrize("length", [30, 96, 1492, 2000])
-def test_fstream_fill_verify(ctx, vt, length):
-    import tcpck
-    from oracle import ref16 as R
-    variant, tile = vt
-    if tile and tile * length < 4096:
-        tile = 0
-    rng = np.random.default_rng(length + variant)
-    count = 5000
-    arena_np = rng.integers(0, 256, count * length, dtype=np.uint8)
-    arena = dev(arena_np)
-    out = torch.empty(count, dtype=torch.int16, device="cuda")
-    ctx.batch_fixed_ex(tcpck.OP_FILL, arena, length, length, count, out, tcpck.KERNEL_FSTREAM, variant | tile)
-    exp_arena = arena_np.copy()
-    exp = np.array([R.fill_np(exp_arena[k * length:(k + 1) * length]) for k in range(count)], np.uint16)
-    np.testing.assert_array_equal(host(out).view(np.uint16), exp)
-    got = host(arena)
-    np.testing.assert_array_equal(got, exp_arena)
-    bad = rng.choice(count, 64, replace=False)
-    for k in bad:
-        got[k * length + int(rng.integers(0, length))] ^= 0x24
-    ok = torch.empty(count, dtype=torch.uint8, device="cuda")
-    ctx.batch_fixed_ex(tcpck.OP_VERIFY, dev(got), length, length, count, ok, tcpck.KERNEL_FSTREAM, variant | tile)
-    np.testing.assert_array_equal(np.nonzero(host(ok) == 0)[0], np.sort(bad))
-
-
-def test_fstream_rejects(ctx):
+def test_run_kernels_reject(ctx):
     import tcpck
     a = torch.zeros(1 << 20, dtype=torch.uint8, device="cuda")
     o = torch.zeros(1024, dtype=torch.int16, device="cuda")
-    with pytest.raises(tcpck.TcpckError):  # gaps between images
-        ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, a, 1500, 1492, 100, o, tcpck.KERNEL_FSTREAM, 0)
-    with pytest.raises(tcpck.TcpckError):  # RFC 1071 mode
-        ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, a, 1492, 1492, 100, o, tcpck.KERNEL_FSTREAM, 0, mode=1)
-    with pytest.raises(tcpck.TcpckError):  # tile shorter than the ring
-        ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, a, 1492, 1492, 100, o, tcpck.KERNEL_FSTREAM, 1)
+    off = torch.arange(8, dtype=torch.int64, device="cuda") * 1000
+    ln = torch.full((8,), 1000, dtype=torch.int32, device="cuda")
+    with pytest.raises(tcpck.TcpckError):  # rstream: gaps
+        ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, a, 1500, 1492, 100, o, tcpck.KERNEL_RSTREAM, 0)
+    for kern in (tcpck.KERNEL_RSTREAM, tcpck.KERNEL_VVSTREAM):  # RFC 1071 mode: seg only
+        with pytest.raises(tcpck.TcpckError):
+            ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, a, 1492, 1492, 100, o, kern, 0, mode=1)
+    with pytest.raises(tcpck.TcpckError):
+        ctx.batch_var_ex(tcpck.OP_CHECKSUM, a, off, ln, 8, o, tcpck.KERNEL_VVSTREAM, 0, mode=1)
+    with pytest.raises(tcpck.TcpckError):  # removed kernels
+        ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, a, 1492, 1492, 100, o, 2, 0)
+    with pytest.raises(tcpck.TcpckError):
+        ctx.batch_var_ex(tcpck.OP_CHECKSUM, a, off, ln, 8, o, 7, 0)
 
 
 # ---- run-stream kernel (KERNEL_RSTREAM = 5: fixed stride == len, scalar boundary walk) ----
-RSTREAM = [0, 1, 2, 9, 10, 11, 12, 13]  # 9-13: v_dot2 sums and/or buffer loads
 
 
 @pytest.mark.parametrize("variant", RSTREAM)
@@ -310,165 +215,7 @@ def test_rstream_fill_verify(ctx, variant, length):
     np.testing.assert_array_equal(np.nonzero(host(ok) == 0)[0], np.sort(bad))
 
 
-# ---- run-stream kernel for packed variable layouts (KERNEL_RVSTREAM = 6) ----
-RVSTREAM = [0, 1, 2]
-TINY = (0, 2, 4, 6, 8, 10, 12, 14)  # payloads below 16 B: several boundaries per chunk
-
-
-def packed_layout(count, seed, payloads, header=32):
-    rng = np.random.default_rng(seed)
-    ln = (np.asarray(payloads, np.int64)[rng.integers(0, len(payloads), count)] + header).astype(np.uint32)
-    off = np.zeros(count, np.uint64)
-    if count > 1:
-        off[1:] = np.cumsum(ln[:-1].astype(np.uint64))
-    return off, ln, int(ln.astype(np.int64).sum())
-
-
-@pytest.mark.parametrize("variant", RVSTREAM)
-def test_rvstream_golden_all_lengths(ctx, golden, variant):
-    """Every golden checksum image (0..65536 B, incl. < 16 B) packed back to back."""
-    import tcpck
-    cases = golden.by_kind("checksum")
-    imgs = [golden.image(c) for c in cases]
-    ln = np.array([c["len"] for c in cases], np.uint32)
-    off = np.zeros(len(cases), np.uint64)
-    off[1:] = np.cumsum(ln[:-1].astype(np.uint64))
-    exp = np.array([c["expected"] for c in cases], np.uint16)
-    out = torch.empty(len(exp), dtype=torch.int16, device="cuda")
-    ctx.batch_var_ex(tcpck.OP_CHECKSUM, dev(np.concatenate(imgs)), dev(off), dev(ln), len(exp), out,
-                     tcpck.KERNEL_RVSTREAM, variant, packed=True)
-    np.testing.assert_array_equal(host(out).view(np.uint16), exp)
-
-
-@pytest.mark.parametrize("variant", RVSTREAM)
-@pytest.mark.parametrize("payloads", [(64, 576, 1460), TINY + (64, 1460), (0,), (-32, -30, 0, 9000, 65504)])
-@pytest.mark.parametrize("count", [1, 2, 63, 64, 65, 1000, 70001])
-def test_rvstream_var_vs_oracle(ctx, oracle_c, variant, payloads, count):
-    import tcpck
-    off, ln, total = packed_layout(count, count * 7 + len(payloads), payloads)
-    if total > (96 << 20):
-        return
-    rng = np.random.default_rng(count + variant)
-    arena_np = rng.integers(0, 256, total + 128, dtype=np.uint8)
-    buf = dev(arena_np)
-    d_off, d_ln = dev(off), dev(ln)
-    for mis in (0, 2, 14, 126):
-        out = torch.empty(count, dtype=torch.int16, device="cuda")
-        ctx.batch_var_ex(tcpck.OP_CHECKSUM, buf.data_ptr() + mis, d_off, d_ln, count, out,
-                         tcpck.KERNEL_RVSTREAM, variant, packed=True)
-        exp = oracle_c.batch(arena_np[mis:], off, ln, threads=8)
-        np.testing.assert_array_equal(host(out).view(np.uint16), exp)
-
-
-@pytest.mark.parametrize("variant", RVSTREAM)
-def test_rvstream_not_packed_falls_back(ctx, oracle_c, variant):
-    """Gaps and a non-zero first offset: waves whose length walk disagrees
-    with the offsets recompute per image -- results stay exact."""
-    import tcpck
-    import synth_np
-    rng = np.random.default_rng(variant)
-    count = 30000
-    off, ln, _ = synth_np.mixed_layout(count, seed=3)
-    off = off.copy()
-    for k in rng.integers(1, count, 25):
-        off[k:] += 10
-    off += np.uint64(4096)
-    total = int(off[-1] + ln[-1]) + 64
-    arena_np = rng.integers(0, 256, total, dtype=np.uint8)
-    out = torch.empty(count, dtype=torch.int16, device="cuda")
-    ctx.batch_var_ex(tcpck.OP_CHECKSUM, dev(arena_np), dev(off), dev(ln), count, out,
-                     tcpck.KERNEL_RVSTREAM, variant, packed=True)
-    np.testing.assert_array_equal(host(out).view(np.uint16), oracle_c.batch(arena_np, off, ln, threads=8))
-
-
-@pytest.mark.parametrize("variant", RVSTREAM)
-@pytest.mark.parametrize("payloads", [(64, 576, 1460), (0, 2, 30, 1460), (65504,)])
-def test_rvstream_fill_verify(ctx, variant, payloads):
-    import tcpck
-    from oracle import ref16 as R
-    count = 6000 if max(payloads) < 10000 else 300
-    off, ln, total = packed_layout(count, 11 + variant, payloads)
-    rng = np.random.default_rng(variant + len(payloads))
-    arena_np = rng.integers(0, 256, total, dtype=np.uint8)
-    arena = dev(arena_np)
-    out = torch.empty(count, dtype=torch.int16, device="cuda")
-    ctx.batch_var_ex(tcpck.OP_FILL, arena, dev(off), dev(ln), count, out, tcpck.KERNEL_RVSTREAM, variant,
-                     packed=True)
-    exp_arena = arena_np.copy()
-    exp = np.array([R.fill_np(exp_arena[int(off[k]):int(off[k]) + int(ln[k])]) for k in range(count)], np.uint16)
-    np.testing.assert_array_equal(host(out).view(np.uint16), exp)
-    got = host(arena)
-    np.testing.assert_array_equal(got, exp_arena)
-    bad = rng.choice(count, 40, replace=False)
-    for k in bad:
-        got[int(off[k]) + int(rng.integers(0, int(ln[k])))] ^= 0x42
-    ok = torch.empty(count, dtype=torch.uint8, device="cuda")
-    ctx.batch_var_ex(tcpck.OP_VERIFY, dev(got), dev(off), dev(ln), count, ok, tcpck.KERNEL_RVSTREAM, variant,
-                     packed=True)
-    np.testing.assert_array_equal(np.nonzero(host(ok) == 0)[0], np.sort(bad))
-
-
-# ---- vector-boundary run stream (KERNEL_VSTREAM = 7: fixed stride == len, small images) ----
-VSTREAM = [0, 1, 2]
-
-
-@pytest.mark.parametrize("variant", VSTREAM)
-@pytest.mark.parametrize("length", [16, 18, 30, 32, 34, 64, 96, 126, 128, 606, 1024, 1026, 1492, 4096])
-@pytest.mark.parametrize("count", [1, 2, 7, 64, 65, 3001, 70001])
-def test_vstream_fixed_vs_oracle(ctx, oracle_c, variant, length, count):
-    import tcpck
-    if count * length > (64 << 20):
-        count = (64 << 20) // length
-    rng = np.random.default_rng(length * 11 + count + variant)
-    arena_np = rng.integers(0, 256, count * length + 128, dtype=np.uint8)
-    arena_np[:length] = 0xFF
-    buf = dev(arena_np)
-    for mis in (0, 2, 14, 126):
-        out = torch.empty(count, dtype=torch.int16, device="cuda")
-        ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, buf.data_ptr() + mis, length, length, count, out,
-                           tcpck.KERNEL_VSTREAM, variant)
-        exp = oracle_c.batch(arena_np[mis:], stride=length, length=length, count=count, threads=8)
-        np.testing.assert_array_equal(host(out).view(np.uint16), exp)
-
-
-@pytest.mark.parametrize("variant", VSTREAM)
-@pytest.mark.parametrize("length", [30, 32, 34, 96, 1024, 1492])
-def test_vstream_fill_verify(ctx, variant, length):
-    import tcpck
-    from oracle import ref16 as R
-    rng = np.random.default_rng(length + 20 * variant)
-    count = 9000
-    arena_np = rng.integers(0, 256, count * length, dtype=np.uint8)
-    arena = dev(arena_np)
-    out = torch.empty(count, dtype=torch.int16, device="cuda")
-    ctx.batch_fixed_ex(tcpck.OP_FILL, arena, length, length, count, out, tcpck.KERNEL_VSTREAM, variant)
-    exp_arena = arena_np.copy()
-    exp = np.array([R.fill_np(exp_arena[k * length:(k + 1) * length]) for k in range(count)], np.uint16)
-    np.testing.assert_array_equal(host(out).view(np.uint16), exp)
-    got = host(arena)
-    np.testing.assert_array_equal(got, exp_arena)
-    bad = rng.choice(count, 64, replace=False)
-    for k in bad:
-        got[k * length + int(rng.integers(0, length))] ^= 0x18
-    ok = torch.empty(count, dtype=torch.uint8, device="cuda")
-    ctx.batch_fixed_ex(tcpck.OP_VERIFY, dev(got), length, length, count, ok, tcpck.KERNEL_VSTREAM, variant)
-    np.testing.assert_array_equal(np.nonzero(host(ok) == 0)[0], np.sort(bad))
-
-
 # ---- prefix-table run stream (KERNEL_VVSTREAM = 8): packed variable and fixed layouts ----
-VVSTREAM = [0, 1, 2, 3, 4]  # 0/1 byte split U4/U8, 2/3 count split, 4 policy
-
-
-def _fill_oracle(arena_np, off, ln):
-    exp_arena = arena_np.copy()
-    exp = np.empty(len(off), np.uint16)
-    from oracle import ref16 as R
-    for k in range(len(off)):
-        o, n = int(off[k]), int(ln[k])
-        exp[k] = R.fill_np(exp_arena[o:o + n])
-    return exp, exp_arena
-
-
 @pytest.mark.parametrize("variant", VVSTREAM)
 @pytest.mark.parametrize("payloads", [(64, 576, 1460), (-16, 0, 1460), (-16,), (0, 9000, 65504), (-32, 64, 1460)])
 @pytest.mark.parametrize("count", [1, 2, 63, 64, 65, 255, 256, 257, 1000, 70001])
@@ -655,7 +402,7 @@ def test_vvstream_fixed_fill_verify(ctx, variant, length):
 
 
 # ---- grid oversubscription (param bits 16..23): more, shorter runs per launch ----
-@pytest.mark.parametrize("kernel,variant,length", [(5, 0, 1492), (5, 10, 1024), (7, 2, 96), (7, 0, 256), (7, 2, 34)])
+@pytest.mark.parametrize("kernel,variant,length", [(5, 0, 1492), (5, 10, 1024), (8, 4, 96), (8, 0, 256), (8, 1, 34)])
 @pytest.mark.parametrize("oversub", [2, 8, 32])
 def test_oversubscribed_fixed(ctx, oracle_c, kernel, variant, length, oversub):
     import tcpck
