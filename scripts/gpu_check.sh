@@ -38,6 +38,7 @@ for s in ${STEPS:-tests smoke bench prof}; do
     vvtests) step vvtests 600 python -u -m pytest tests/test_gpu_kernels.py -x -q --timeout 120 --timeout-method thread -k vvstream ;;
     b2b_c3) step b2b_c3 600 python scripts/b2b_probe.py --what c3 ;;
     b2b_c2) step b2b_c2 600 python scripts/b2b_probe.py --what c2 ;;
+    xcd_c2) step xcd_c2 600 python scripts/b2b_probe.py --what c2 --params 524298,524302,2097162,2097166,2097167,1048586,1048590 ;;
     tr_c3) step tr_c3 300 python scripts/transient.py --what c3 ;;
     tr_c2) step tr_c2 300 python scripts/transient.py --what c2 --n 800 ;;
     fillprobe) step fillprobe 600 python scripts/fill_probe.py ;;
@@ -47,6 +48,10 @@ for s in ${STEPS:-tests smoke bench prof}; do
     os_c4) step os_c4 600 python scripts/oversub.py --what c4,c4r,c4v --ms 1,2,4,8,16,32 ;;
     gap) step gap 600 python scripts/gap_probe.py ;;
     os_c5) step os_c5 600 python scripts/oversub.py --what c5,c5v,c2v --variants 0,1,10 --ms 8,16,32,64 ;;
+    xcd) step xcd_c2 300 python scripts/xcd_probe.py --what c2 && step xcd_c3 300 python scripts/xcd_probe.py --what c3 &&
+      step xcd_c4 300 python scripts/xcd_probe.py --what c4 && step xcd_c5 300 python scripts/xcd_probe.py --what c5 ;;
+    xccmap) step xccmap 300 python scripts/xcc_map.py ;;
+    xcdplace) step xcdplace 600 python scripts/xcd_place_probe.py ;;
     oversub) step oversub 600 python scripts/oversub.py ;;
     os_c2) step os_c2 600 python scripts/oversub.py --what c2 --variants 0,9,10 --ms 8,16,24,32,40,48 ;;
     os_c3) step os_c3 600 python scripts/oversub.py --what c3 --variants 2,3 --ms 8,16,32 ;;

@@ -23,11 +23,12 @@ def main():
     arena = torch.empty(n * L, dtype=torch.uint8, device="cuda")
     tcpck.synth_fixed(arena, L, L, n, seed=5)
     out = torch.empty(n, dtype=torch.int16, device="cuda")
-    dbg = torch.zeros(4 * 16384, dtype=torch.int64, device="cuda")
+    dbg = torch.zeros(4 * 65536, dtype=torch.int64, device="cuda")  # 4 x u64 per wave of the x1 grid
     ctx.set_debug(dbg)
     for rep in range(3):
         dbg.zero_()
-        ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, arena, L, L, n, out, tcpck.KERNEL_RSTREAM, 3)
+        # variant 3 (stamps) on the resident grid only (x1): one stamp slot per wave
+        ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, arena, L, L, n, out, tcpck.KERNEL_RSTREAM, 3 | (1 << 16))
         torch.cuda.synchronize()
     ctx.set_debug(None)
     d = dbg.cpu().numpy().reshape(-1, 4)

@@ -1,0 +1,110 @@
+#!/usr/bin/env python3
+"""XCD-aware run order (dev::xcd_block): bare stream (diag) and the checksum
+kernels, default block order vs the blocks of one XCD taking consecutive runs.
+Median of back-to-back rounds.  Run one workload per process (--what c2, ...):
+a batch allocated after other large buffers were freed can land on fragmented
+memory, which hides the effect.
+
+    python scripts/xcd_probe.py --what bare|c2|c5|c3|c4
+"""
+import argparse
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "tcp-stack_amd"), os.path.join(ROOT, "tests")]
+
+import torch  # noqa: E402
+import tcpck  # noqa: E402
+
+K = tcpck
+
+
+def b2b(fn, s, reps=20, rounds=5):
+    for _ in range(10):
+        fn()
+    torch.cuda.synchronize()
+    t = []
+    for _ in range(rounds):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for _ in range(reps):
+            fn()
+        e1.record(s)
+        torch.cuda.synchronize()
+        t.append(e0.elapsed_time(e1) / reps)
+    return float(np.median(t))
+
+
+def fixed_case(ctx, s, label, n, L, runs, reps):
+    a = torch.empty(n * L, dtype=torch.uint8, device="cuda")
+    K.synth_fixed(a, L, L, n, seed=42)
+    ref = torch.empty(n, dtype=torch.int16, device="cuda")
+    ctx.batch_fixed_ex(K.OP_CHECKSUM, a, L, L, n, ref, K.KERNEL_SEG, 0)
+    out = torch.empty(n, dtype=torch.int16, device="cuda")
+    for name, kern, p in runs:
+        ctx.batch_fixed_ex(K.OP_CHECKSUM, a, L, L, n, out, kern, p)
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref), name
+        ms = b2b(lambda: ctx.batch_fixed_ex(K.OP_CHECKSUM, a, L, L, n, out, kern, p, stream=s), s, reps=reps)
+        print(f"{label} {name}: {ms:.4f} ms ({(n * L + 2 * n) / ms / 1e6 / 80:.1f}%)", flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--what", default="c2")
+    what = ap.parse_args().what
+    ctx = tcpck.Context(0)
+    s = torch.cuda.current_stream()
+    if what == "bare":
+        buf = torch.empty(17 << 30, dtype=torch.uint8, device="cuda")
+        tcpck.synth_fixed(buf, 65536, 65536, (17 << 30) // 65536, seed=1)
+        dout = torch.empty(1 << 22, dtype=torch.int32, device="cuda")
+        for nbytes in (1566572544, 17 << 30):
+            for k, m in ((2, 8), (8, 32)):
+                for x in (0, 1):
+                    v = 0x3000 | (k << 8) | x
+                    ms = b2b(lambda: ctx.diag_stream(v, buf, nbytes, dout, stream=s), s,
+                             reps=20 if nbytes < 4e9 else 4)
+                    print(f"bare stream {nbytes / 1e9:5.2f} GB x{m} {'xcd' if x else 'default'}: {ms:.4f} ms "
+                          f"({nbytes / ms / 1e6 / 80:.1f}%)", flush=True)
+    elif what in ("c2", "c5"):
+        n = (1 << 20) if what == "c2" else (8 << 20)
+        runs = [(f"rstream v{v} x{m}", K.KERNEL_RSTREAM, v | (m << 16))
+                for v, m in ((10, 32), (14, 32), (17, 32), (18, 32), (19, 32), (18, 8))]
+        runs += [("vvstream fixed x32", K.KERNEL_VVSTREAM, 3 | (32 << 16)),
+                 ("vvstream fixed x32 xcd16", K.KERNEL_VVSTREAM, 11 | (32 << 16))]
+        fixed_case(ctx, s, what, n, 1492, runs, 20 if what == "c2" else 4)
+    elif what == "c4":
+        runs = [(f"seg G64U4 x{m}{' xcd16' if x else ''}", K.KERNEL_SEG, 3 | (m << 16) | (x << 24))
+                for m in (1, 8) for x in (0, 1)]
+        runs += [(f"rstream v{v} x{m}", K.KERNEL_RSTREAM, v | (m << 16))
+                 for v, m in ((10, 8), (14, 8), (18, 8), (18, 32))]
+        fixed_case(ctx, s, "c4", 256 << 10, 65536, runs, 4)
+    elif what == "c3":
+        from synth_np import mixed_layout
+        off, ln, total = mixed_layout(4 << 20, seed=42)
+        n = ln.size
+        a = torch.empty(total, dtype=torch.uint8, device="cuda")
+        d_off, d_ln = torch.from_numpy(off).cuda(), torch.from_numpy(ln).cuda()
+        K.synth_var(a, d_off, d_ln, 1492, n, seed=42)
+        ref = torch.empty(n, dtype=torch.int16, device="cuda")
+        ctx.batch_var_ex(K.OP_CHECKSUM, a, d_off, d_ln, n, ref, K.KERNEL_SEG, 0)
+        out = torch.empty(n, dtype=torch.int16, device="cuda")
+        for p in (4, 12, 3 | (32 << 16), 11 | (32 << 16), 2 | (32 << 16), 10 | (32 << 16)):
+            ctx.batch_var_ex(K.OP_CHECKSUM, a, d_off, d_ln, n, out, K.KERNEL_VVSTREAM, p, packed=True,
+                             total_bytes=total)
+            torch.cuda.synchronize()
+            assert torch.equal(out, ref), p
+            ms = b2b(lambda: ctx.batch_var_ex(K.OP_CHECKSUM, a, d_off, d_ln, n, out, K.KERNEL_VVSTREAM, p,
+                                              packed=True, total_bytes=total, stream=s), s)
+            print(f"c3 vvstream variant {p & 0xFF} x{p >> 16}: {ms:.4f} ms ({(total + 2 * n) / ms / 1e6 / 80:.1f}%)",
+                  flush=True)
+    else:
+        raise SystemExit(f"unknown --what {what}")
+
+
+if __name__ == "__main__":
+    main()

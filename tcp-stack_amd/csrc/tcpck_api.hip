@@ -161,6 +161,14 @@ void free_stage(tcpck_ctx *ctx) {
 // mode, jumbo images (where one wave per image already streams whole 1 KiB
 // steps) -- seg.
 constexpr uint64_t kRunMaxLen = 16384;  // above: seg (one wave per jumbo image already streams whole steps)
+// Policy parameters.  Every kernel takes its runs in the XCD-chunked block
+// order (dev::ordered_block, groups of 16 blocks per XCD): neighbouring runs
+// share an XCD's L2, so the run-edge lines and the partial lines of out[] that
+// neighbouring blocks share merge there (C2 86.3% -> 90.6%, C3 82.7 -> 84.1%,
+// C4 85.5 -> 87.4%, profiles/r01/xcd_*.log).
+constexpr int kRstreamPolicy = 18;       // v_dot2 sums, buffer loads, XCD-chunked order
+constexpr int kVvPolicy = 4 | 8;         // size policy, XCD-chunked order
+constexpr int kSegXcdOrder = 1 << 24;    // seg: XCD-chunked order
 
 hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t stride, uint32_t len,
                      uint64_t count, void *out, int kernel, int param, hipStream_t s) {
@@ -168,6 +176,7 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
   if (kernel == TCPCK_KERNEL_AUTO) {
     if (mode != TCPCK_MODE_REF || len < 2 || len > kRunMaxLen || stride > (1u << 24)) {
       kernel = TCPCK_KERNEL_SEG;
+      param = kSegXcdOrder;  // shape by length
     } else if (stride > len) {
       // gapped fixed strides (e.g. MSS slots) (scripts/gap_probe.py,
       // profiles/r01/gap_probe.log): streaming the gaps with the images
@@ -178,10 +187,10 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
       const bool hull = len < 512 ? stride <= 2 * l : (len < 1024 ? 4 * stride <= 5 * l : 16 * stride <= 17 * l);
       if (hull && (op != TCPCK_OP_FILL || len >= 30)) {
         kernel = TCPCK_KERNEL_VVSTREAM;
-        param = 4;
+        param = kVvPolicy;
       } else {
         kernel = TCPCK_KERNEL_SEG;
-        param = tcpck::kShapeSmall + 1;
+        param = (tcpck::kShapeSmall + 1) | kSegXcdOrder;
       }
     } else if (len < 512) {
       // packed, by image length (scripts/policy_sweep.py, profiles/r01/policy_small.log):
@@ -190,10 +199,10 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
       // 32-256 B); from 512 B the scalar boundary walk (rstream: ~87% of the
       // HBM roof on C2 at 32x oversubscription)
       kernel = (op == TCPCK_OP_FILL && len < 30) ? TCPCK_KERNEL_SEG : TCPCK_KERNEL_VVSTREAM;
-      param = 4;
+      param = kernel == TCPCK_KERNEL_SEG ? kSegXcdOrder : kVvPolicy;
     } else {
       kernel = TCPCK_KERNEL_RSTREAM;
-      param = 10;  // v_dot2 chunk sums, buffer loads (C2 +0.5%, profiles/r01/b2b_c2c3.log)
+      param = kRstreamPolicy;
     }
   }
   if (kernel == TCPCK_KERNEL_RSTREAM) {
@@ -202,6 +211,7 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
     a.arena = arena;
     a.stride = stride;
     a.count = count;
+    a.order = 0xFFu;  // default block order (variants 14-19 choose an XCD order)
     a.out = out;
     a.dbg = static_cast<uint64_t *>(ctx->dbg);
     a.blocks_per_cu = static_cast<uint32_t>(param >> 8) & 0xFFu;
@@ -228,6 +238,7 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
   a.count = count;
   a.out = out;
   a.oversub = static_cast<uint32_t>(param >> 16) & 0xFFu;
+  a.order = ((param >> 24) & 1u) ? 4u : 0xFFu;  // bit 24: XCD-chunked order, groups of 16 blocks
   const auto shape = (param & 0xFF) > 0 ? static_cast<tcpck::SegShape>((param & 0xFF) - 1) : tcpck::shape_for_len(len);
   return tcpck::launch_seg(op, mode, true, shape, a, num_cus, s);
 }
@@ -243,9 +254,10 @@ hipError_t run_var(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const uint6
   if (kernel == TCPCK_KERNEL_AUTO) {
     if (!packed || typical > kRunMaxLen || (op == TCPCK_OP_FILL && layout->min_len != 0 && layout->min_len < 30)) {
       kernel = TCPCK_KERNEL_SEG;
+      param = kSegXcdOrder;
     } else {
       kernel = TCPCK_KERNEL_VVSTREAM;
-      param = 4;
+      param = kVvPolicy;
     }
   }
   if (kernel == TCPCK_KERNEL_VVSTREAM) {
@@ -270,6 +282,7 @@ hipError_t run_var(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const uint6
   a.count = count;
   a.out = out;
   a.oversub = static_cast<uint32_t>(param >> 16) & 0xFFu;
+  a.order = ((param >> 24) & 1u) ? 4u : 0xFFu;  // bit 24: XCD-chunked order, groups of 16 blocks
   const auto shape = (param & 0xFF) > 0 ? static_cast<tcpck::SegShape>((param & 0xFF) - 1) : tcpck::shape_for_len(typical);
   return tcpck::launch_seg(op, mode, false, shape, a, static_cast<uint32_t>(ctx->num_cus), s);
 }

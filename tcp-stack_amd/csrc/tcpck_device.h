@@ -314,6 +314,28 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
 }
 
+// XCD-chunked block order: the blocks of one XCD take groups of 2^lc
+// consecutive ids, the groups of the 8 XCDs interleaved -- neighbouring runs
+// share an XCD (and its L2) while the 8 XCDs still stream nearby addresses.
+// Bijective on the largest multiple of 8 * 2^lc blocks; the rest keep their id.
+__device__ __forceinline__ uint32_t xcd_chunk_block(uint32_t b, uint32_t nb, uint32_t lc) {
+  const uint32_t full = (nb >> (3 + lc)) << (3 + lc);
+  if (b >= full) return b;
+  const uint32_t i = b >> 3;  // the block's index among its XCD's blocks
+  return ((((i >> lc) << 3) + (b & 7u)) << lc) + (i & ((1u << lc) - 1u));
+}
+
+// Block order selector for the run kernels' runtime argument: kOrderDefault
+// keeps blockIdx, kOrderXcd is xcd_block, anything else the chunked order
+// with groups of 2^lc blocks.
+constexpr uint32_t kOrderDefault = 0xFFu;
+constexpr uint32_t kOrderXcd = 0xFEu;
+__device__ __forceinline__ uint32_t ordered_block(uint32_t b, uint32_t nb, uint32_t lc) {
+  if (lc == kOrderDefault) return b;
+  if (lc == kOrderXcd) return xcd_block(b, nb);
+  return xcd_chunk_block(b, nb, lc);
+}
+
 // SPLIT 0: byte-balanced runs (two 64-ary searches over the offsets);
 // SPLIT 1: equal image counts (no search; balance only statistical) -- tuning.
 

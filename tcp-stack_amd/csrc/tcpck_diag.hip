@@ -135,11 +135,12 @@ hipError_t launch_dyn(const uint8_t *buf, uint64_t bytes, uint32_t *out, uint32_
 // Cache-policy bits of the stream's loads: the bare stream (1x16 B, U4, scan,
 // one run per wave, grid oversubscribed 8x) with raw buffer loads whose aux
 // operand is AUX (bit 0 sc0, bit 1 nt, bit 4 sc1 on gfx950).
-template <int AUX>
+// XCD: blocks that share an XCD take consecutive runs (dev::xcd_block).
+template <int AUX, bool XCD = false>
 __global__ void __launch_bounds__(kBlock) diag_cpol_kernel(const uint8_t *buf, uint64_t bytes, uint32_t *out) {
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t NW = static_cast<uint64_t>(gridDim.x) * kWavesPerBlock;
-  const uint64_t wid = static_cast<uint64_t>(blockIdx.x) * kWavesPerBlock +
+  const uint64_t wid = static_cast<uint64_t>(XCD ? dev::xcd_block(blockIdx.x, gridDim.x) : blockIdx.x) * kWavesPerBlock +
                        static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6)));
   const uint64_t lines = bytes >> 7;
   const uint64_t b0 = (wid * lines / NW) << 7;
@@ -168,10 +169,11 @@ __global__ void __launch_bounds__(kBlock) diag_cpol_kernel(const uint8_t *buf, u
   if (lane == 0) out[wid] = carry;
 }
 
-template <int AUX>
-hipError_t launch_cpol(const uint8_t *buf, uint64_t bytes, uint32_t *out, uint32_t num_cus, hipStream_t s) {
-  static const uint32_t per_cu = dev::resident_blocks_per_cu(diag_cpol_kernel<AUX>);
-  hipLaunchKernelGGL((diag_cpol_kernel<AUX>), dim3(per_cu * num_cus * 8), dim3(kBlock), 0, s, buf, bytes, out);
+template <int AUX, bool XCD = false>
+hipError_t launch_cpol(const uint8_t *buf, uint64_t bytes, uint32_t *out, uint32_t num_cus, hipStream_t s,
+                       uint32_t m = 8) {
+  static const uint32_t per_cu = dev::resident_blocks_per_cu(diag_cpol_kernel<AUX, XCD>);
+  hipLaunchKernelGGL((diag_cpol_kernel<AUX, XCD>), dim3(per_cu * num_cus * m), dim3(kBlock), 0, s, buf, bytes, out);
   return hipGetLastError();
 }
 
@@ -270,6 +272,11 @@ hipError_t launch_one(const uint8_t *buf, uint64_t bytes, uint32_t *out, uint32_
 // image (w = 0 none, 1 2 B, 2 4 B, 3 16 B, 4 32 B, 5 64 B, 6 128 B)
 hipError_t launch_diag_stream(int variant, const uint8_t *buf, uint64_t bytes, uint32_t *out, uint32_t num_cus,
                               hipStream_t s) {
+  if (variant >= 0x3000) {  // nt stream, run order by XCD (bit 0) and grid multiple (bits 8..15)
+    const uint32_t m = (variant >> 8) & 0xFu ? static_cast<uint32_t>((variant >> 8) & 0xFu) * 4u : 8u;
+    return (variant & 1) ? launch_cpol<2, true>(buf, bytes, out, num_cus, s, m)
+                         : launch_cpol<2, false>(buf, bytes, out, num_cus, s, m);
+  }
   if (variant >= 0x2000) {  // load cache-policy bits
     switch (variant & 0xFF) {
       case 0: return launch_cpol<0>(buf, bytes, out, num_cus, s);

@@ -32,6 +32,7 @@ struct SegArgs {
   void *out;                 // u16[count] or u8[count] (verify); may be null for fill
   uint32_t len;              // fixed layout: image length
   uint32_t oversub;          // grid = resident blocks x this (0/1: one block per resident slot)
+  uint32_t order;            // block order (dev::ordered_block; 0xFF default)
 };
 
 SegShape shape_for_len(uint64_t typical_len);
@@ -64,6 +65,7 @@ struct FixedStreamArgs {
   uint32_t oversub;        // grid = resident blocks x this (0 = by size, 1 = none)
   uint64_t per_wave;       // run split, set by the launcher: count = per_wave * waves + rem,
   uint64_t rem;            // wave w owns per_wave + (w < rem) images (no 64-bit division on device)
+  uint32_t order;          // block order (dev::ordered_block; 0xFF default)
 };
 
 // ---- rstream (fixed stride == len): one run per wave, scalar boundary walk.

@@ -40,7 +40,8 @@ __global__ void __launch_bounds__(kBlock) seg_kernel(SegArgs a) {
   static_assert(G >= 1 && G <= 64 && (G & (G - 1)) == 0, "G must be a power of two <= 64");
   const uint32_t gl = threadIdx.x & (G - 1);
   const uint64_t groups_per_grid = static_cast<uint64_t>(gridDim.x) * (kBlock / G);
-  for (uint64_t k = (static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x) / G; k < a.count;
+  const uint32_t bid = dev::ordered_block(blockIdx.x, gridDim.x, a.order);
+  for (uint64_t k = (static_cast<uint64_t>(bid) * kBlock + threadIdx.x) / G; k < a.count;
        k += groups_per_grid) {
     const uint64_t start = FIXED ? k * a.stride : a.offsets[k] - a.base;
     const uint32_t len = FIXED ? a.len : a.lengths[k];

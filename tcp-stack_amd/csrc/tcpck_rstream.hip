@@ -43,18 +43,18 @@ using dev::u32x4;
 // 224 us in slot 7 of a C2 launch (scripts/stamps.py).
 // FLAV bit 0: chunk sums with v_dot2_u32_u16; bit 1: buffer (SRSRC) loads with
 // the step offset in an SGPR instead of per-lane 64-bit clamped addresses;
-// bit 2: XCD-aware run order -- blocks that share an XCD (blockIdx % 8) take
-// consecutive runs, so the few results of neighbouring blocks that share a
-// 128-B line of out[] are written through one L2 (whole lines leave it)
-// instead of as partial lines from up to four XCDs.
+// a.order (runtime): the block order, dev::ordered_block -- the XCD orders let
+// neighbouring runs share an XCD, so the results of neighbouring blocks that
+// share a 128-B line of out[] leave one L2 as whole lines instead of partial
+// lines from up to four XCDs.
 template <int U, int OP, bool STAMP, int PRIO = 0, int FLAV = 0>
 __global__ void __launch_bounds__(kBlock) rstream_kernel(FixedStreamArgs a) {
   const uint32_t lane = threadIdx.x & 63;
   // readfirstlane: the wave index is uniform, but hipcc cannot prove anything
   // derived from threadIdx is; without it every boundary variable below lives
   // in VGPRs and each uniform test becomes an exec-masked region
-  const uint64_t wid = static_cast<uint64_t>((FLAV & 4) ? dev::xcd_block(blockIdx.x, gridDim.x) : blockIdx.x) *
-                           kWavesPerBlock +
+  const uint32_t bid = dev::ordered_block(blockIdx.x, gridDim.x, a.order);
+  const uint64_t wid = static_cast<uint64_t>(bid) * kWavesPerBlock +
                        static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6)));
   uint64_t t_start = 0;
   if (STAMP) t_start = __builtin_amdgcn_s_memrealtime();
@@ -243,8 +243,13 @@ hipError_t launch_rstream(int op, int variant, const FixedStreamArgs &a, uint32_
     case 11: return dispatch<4, false, 0, 2>(op, a, num_cus, stream);
     case 12: return dispatch<2, false, 0, 3>(op, a, num_cus, stream);
     case 13: return dispatch<8, false, 0, 3>(op, a, num_cus, stream);
-    case 14: return dispatch<4, false, 0, 7>(op, a, num_cus, stream);  // 10 + XCD-aware run order
-    case 15: return dispatch<8, false, 0, 7>(op, a, num_cus, stream);
+    case 14: case 15: case 16: case 17: case 18: case 19: {
+      // 10 (14, 16-19) or 13 (15) with an XCD order: whole regions (14, 15) or
+      // interleaved groups of 2, 4, 16, 64 blocks (16-19)
+      FixedStreamArgs b = a;
+      b.order = variant <= 15 ? dev::kOrderXcd : (variant == 16 ? 1u : (variant == 17 ? 2u : (variant == 18 ? 4u : 6u)));
+      return variant == 15 ? dispatch<8, false, 0, 3>(op, b, num_cus, stream) : dispatch<4, false, 0, 3>(op, b, num_cus, stream);
+    }
     default: return hipErrorInvalidValue;
   }
 }

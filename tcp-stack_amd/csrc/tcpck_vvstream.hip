@@ -60,6 +60,7 @@ struct VVArgs {
   uint64_t per_wave, rem;   // equal-count split: count = per_wave * waves + rem
   uint32_t stride;          // fixed layouts: image k at k * stride
   uint32_t len;             // fixed layouts: image length (<= stride)
+  uint32_t order;           // block order (dev::ordered_block)
 };
 
 // Word wi (0..7) of a 16-byte chunk set to zero.
@@ -84,7 +85,8 @@ __global__ void __launch_bounds__(kBlock) vvstream_kernel(VVArgs a) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wv = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6)));
   const uint64_t W = static_cast<uint64_t>(gridDim.x) * kWavesPerBlock;
-  const uint64_t wid = static_cast<uint64_t>(blockIdx.x) * kWavesPerBlock + wv;
+  const uint32_t bid = dev::ordered_block(blockIdx.x, gridDim.x, a.order);
+  const uint64_t wid = static_cast<uint64_t>(bid) * kWavesPerBlock + wv;
   const uint64_t N = a.count;
   const uint32_t S = a.stride;
   const uint32_t L = FIXED ? a.len : 0u;
@@ -327,7 +329,7 @@ __global__ void __launch_bounds__(kBlock) vvstream_kernel(VVArgs a) {
 }
 
 template <int U, int OP, int SPLIT, int LAYOUT>
-hipError_t launch_one(const RunArgs &s, uint32_t oversub, uint32_t num_cus, hipStream_t stream) {
+hipError_t launch_one(const RunArgs &s, uint32_t oversub, bool xcd, uint32_t num_cus, hipStream_t stream) {
   static const uint32_t per_cu = dev::resident_blocks_per_cu(vvstream_kernel<U, OP, SPLIT, LAYOUT>);
   const uint64_t resident = static_cast<uint64_t>(per_cu) * num_cus;
   uint64_t blocks = resident * (oversub ? oversub : 1);
@@ -345,17 +347,18 @@ hipError_t launch_one(const RunArgs &s, uint32_t oversub, uint32_t num_cus, hipS
   a.rem = s.count % (blocks * kWavesPerBlock);
   a.stride = static_cast<uint32_t>(s.stride);
   a.len = s.len;
+  a.order = xcd ? 4u : dev::kOrderDefault;  // groups of 16 blocks per XCD
   hipLaunchKernelGGL((vvstream_kernel<U, OP, SPLIT, LAYOUT>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0,
                      stream, a);
   return hipGetLastError();
 }
 
 template <int U, int SPLIT, int LAYOUT>
-hipError_t dispatch(int op, const RunArgs &a, uint32_t oversub, uint32_t num_cus, hipStream_t s) {
+hipError_t dispatch(int op, const RunArgs &a, uint32_t oversub, bool xcd, uint32_t num_cus, hipStream_t s) {
   switch (op) {
-    case kChecksum: return launch_one<U, kChecksum, SPLIT, LAYOUT>(a, oversub, num_cus, s);
-    case kVerify: return launch_one<U, kVerify, SPLIT, LAYOUT>(a, oversub, num_cus, s);
-    case kFill: return launch_one<U, kFill, SPLIT, LAYOUT>(a, oversub, num_cus, s);
+    case kChecksum: return launch_one<U, kChecksum, SPLIT, LAYOUT>(a, oversub, xcd, num_cus, s);
+    case kVerify: return launch_one<U, kVerify, SPLIT, LAYOUT>(a, oversub, xcd, num_cus, s);
+    case kFill: return launch_one<U, kFill, SPLIT, LAYOUT>(a, oversub, xcd, num_cus, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -369,6 +372,8 @@ hipError_t launch_vvstream(int op, int variant, bool fixed, const RunArgs &a, ui
   const bool gap = fixed && a.stride != a.len;
   const uint64_t bytes = fixed ? a.count * a.stride : a.total_bytes;
   uint32_t m = a.oversub ? a.oversub : 1;
+  const bool xcd = (variant & 8) != 0;  // XCD-chunked run order
+  variant &= 7;
   int u8 = (variant & 1);
   int split = variant >= 2 ? 1 : 0;
   if (variant == 4) {
@@ -383,10 +388,10 @@ hipError_t launch_vvstream(int op, int variant, bool fixed, const RunArgs &a, ui
   } else if (variant > 4 || variant < 0) {
     return hipErrorInvalidValue;
   }
-  if (gap) return u8 ? dispatch<8, 1, 2>(op, a, m, num_cus, stream) : dispatch<4, 1, 2>(op, a, m, num_cus, stream);
-  if (fixed) return u8 ? dispatch<8, 1, 1>(op, a, m, num_cus, stream) : dispatch<4, 1, 1>(op, a, m, num_cus, stream);
-  if (split) return u8 ? dispatch<8, 1, 0>(op, a, m, num_cus, stream) : dispatch<4, 1, 0>(op, a, m, num_cus, stream);
-  return u8 ? dispatch<8, 0, 0>(op, a, m, num_cus, stream) : dispatch<4, 0, 0>(op, a, m, num_cus, stream);
+  if (gap) return u8 ? dispatch<8, 1, 2>(op, a, m, xcd, num_cus, stream) : dispatch<4, 1, 2>(op, a, m, xcd, num_cus, stream);
+  if (fixed) return u8 ? dispatch<8, 1, 1>(op, a, m, xcd, num_cus, stream) : dispatch<4, 1, 1>(op, a, m, xcd, num_cus, stream);
+  if (split) return u8 ? dispatch<8, 1, 0>(op, a, m, xcd, num_cus, stream) : dispatch<4, 1, 0>(op, a, m, xcd, num_cus, stream);
+  return u8 ? dispatch<8, 0, 0>(op, a, m, xcd, num_cus, stream) : dispatch<4, 0, 0>(op, a, m, xcd, num_cus, stream);
 }
 
 }  // namespace tcpck
