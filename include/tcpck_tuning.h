@@ -18,7 +18,7 @@ extern "C" {
                                (1: G8/U2, 2: G16/U6, 3: G64/U4, 4: G64/U2,
                                 5: G32/U3, 6: G4/U8), 0 = by length
                                | (grid oversubscription << 16)
-                               | (1 << 24: XCD-aware block order)               */
+                               | (1 << 24: each XCD takes groups of 16 blocks)  */
 /* 2, 3, 4, 6, 7: span, stream, fstream, rvstream and vstream, measured in
    round 1 and removed; the numbers are not reused. */
 #define TCPCK_KERNEL_RSTREAM 5 /* fixed stride == len only, MODE_REF: one run per
@@ -28,8 +28,11 @@ extern "C" {
                                   4/8/2 loads with slot-graded s_setprio, 5: 4
                                   with s_setprio 1 for slots >= 4, 7: 3 + graded
                                   priority, 9: 4 with v_dot2 sums, 10/12/13:
-                                  4/2/8 with v_dot2 sums and buffer loads (10 =
-                                  the policy's), 11: 4 with buffer loads)
+                                  4/2/8 with v_dot2 sums and buffer loads, 11: 4
+                                  with buffer loads; 14/15: 10/13 with each XCD
+                                  taking one contiguous region of runs; 16-19: 10
+                                  with each XCD taking groups of 2/4/16/64
+                                  consecutive runs, 18 = the policy's)
                                   | (blocks per CU cap << 8)
                                   | (grid oversubscription << 16: 0 = by batch
                                   size, 1 = none, M = M x the resident grid)    */
@@ -40,7 +43,9 @@ extern "C" {
                                    prefix table; param = variant (0: 4 loads in
                                    flight, byte-balanced runs, 1: 8; 2/3: same
                                    with equal-count runs -- fixed layouts are
-                                   always equal-count; 4: policy)
+                                   always equal-count; 4: policy; + 8: each XCD
+                                   takes groups of 16 consecutive runs, 12 = the
+                                   policy's)
                                    | (grid oversubscription << 16: 0 = by batch
                                    size, 1 = none, M = M x the resident grid)   */
 

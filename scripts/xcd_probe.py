@@ -22,8 +22,22 @@ import tcpck  # noqa: E402
 K = tcpck
 
 
+_SETTLED = [False]
+
+
 def b2b(fn, s, reps=20, rounds=5):
-    for _ in range(10):
+    # the first config measured in a process would otherwise pay the idle GPU's
+    # clock ramp (profiles/r01/transient.log): settle ~300 ms of launches first
+    warm = 10
+    if not _SETTLED[0]:
+        _SETTLED[0] = True
+        import time
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < 0.3:
+            for _ in range(8):
+                fn()
+            torch.cuda.synchronize()
+    for _ in range(warm):
         fn()
     torch.cuda.synchronize()
     t = []
@@ -93,7 +107,7 @@ def main():
         ref = torch.empty(n, dtype=torch.int16, device="cuda")
         ctx.batch_var_ex(K.OP_CHECKSUM, a, d_off, d_ln, n, ref, K.KERNEL_SEG, 0)
         out = torch.empty(n, dtype=torch.int16, device="cuda")
-        for p in (4, 12, 3 | (32 << 16), 11 | (32 << 16), 2 | (32 << 16), 10 | (32 << 16)):
+        for p in (12, 4, 3 | (32 << 16), 11 | (32 << 16), 2 | (32 << 16), 10 | (32 << 16), 12):
             ctx.batch_var_ex(K.OP_CHECKSUM, a, d_off, d_ln, n, out, K.KERNEL_VVSTREAM, p, packed=True,
                              total_bytes=total)
             torch.cuda.synchronize()
