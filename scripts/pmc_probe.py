@@ -1,0 +1,55 @@
+#!/usr/bin/env python3
+"""Launches for SQ counter passes (run under rocprofv3 --pmc ...): the C2 batch
+through rstream (policy) and through vvstream's fixed mode, and the C3 batch
+through vvstream (policy), a few launches each after a settle.  Compare the
+kernels' instruction mix and stall buckets with scripts/pmc_sq.py.
+
+    rocprofv3 --kernel-trace --pmc SQ_WAVE_CYCLES ... -d gpurun_out/sq1 -o run \
+        --output-format csv -- python3 scripts/pmc_probe.py
+"""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "tcp-stack_amd"), os.path.join(ROOT, "tests")]
+
+import torch  # noqa: E402
+import tcpck  # noqa: E402
+
+K = tcpck
+
+
+def run(fn, n=5):
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < 0.1:
+        fn()
+        torch.cuda.synchronize()
+    for _ in range(n):
+        fn()
+    torch.cuda.synchronize()
+
+
+def main():
+    ctx = tcpck.Context(0)
+    n, L = 1 << 20, 1492
+    a = torch.empty(n * L, dtype=torch.uint8, device="cuda")
+    K.synth_fixed(a, L, L, n, seed=42)
+    out = torch.empty(n, dtype=torch.int16, device="cuda")
+    run(lambda: ctx.batch_fixed_ex(K.OP_CHECKSUM, a, L, L, n, out, K.KERNEL_RSTREAM, 18 | (32 << 16)))
+    run(lambda: ctx.batch_fixed_ex(K.OP_CHECKSUM, a, L, L, n, out, K.KERNEL_VVSTREAM, 11 | (32 << 16)))
+    del a, out
+    from synth_np import mixed_layout
+    off, ln, total = mixed_layout(4 << 20, seed=42)
+    n = ln.size
+    a = torch.empty(total, dtype=torch.uint8, device="cuda")
+    d_off, d_ln = torch.from_numpy(off).cuda(), torch.from_numpy(ln).cuda()
+    K.synth_var(a, d_off, d_ln, 1492, n, seed=42)
+    out = torch.empty(n, dtype=torch.int16, device="cuda")
+    run(lambda: ctx.batch_var_ex(K.OP_CHECKSUM, a, d_off, d_ln, n, out, K.KERNEL_VVSTREAM, 12, packed=True,
+                                 total_bytes=total))
+    print("ok", flush=True)
+
+
+if __name__ == "__main__":
+    main()
