@@ -116,6 +116,32 @@ def main():
                                               packed=True, total_bytes=total, stream=s), s)
             print(f"c3 vvstream variant {p & 0xFF} x{p >> 16}: {ms:.4f} ms ({(total + 2 * n) / ms / 1e6 / 80:.1f}%)",
                   flush=True)
+    elif what == "iso":
+        # what separates C3 from the fixed layouts on vvstream: the descriptors
+        # (packed var over uniform lengths vs the same fixed batch) and the end
+        # density (744-B vs 1492-B images)
+        for L, n in ((1492, 1 << 20), (744, 2 << 20)):
+            a = torch.empty(n * L, dtype=torch.uint8, device="cuda")
+            K.synth_fixed(a, L, L, n, seed=42)
+            ref = torch.empty(n, dtype=torch.int16, device="cuda")
+            ctx.batch_fixed_ex(K.OP_CHECKSUM, a, L, L, n, ref, K.KERNEL_SEG, 0)
+            out = torch.empty(n, dtype=torch.int16, device="cuda")
+            d_off = torch.arange(n, dtype=torch.int64, device="cuda") * L
+            d_ln = torch.full((n,), L, dtype=torch.int32, device="cuda")
+            runs = [("fixed", lambda st=None: ctx.batch_fixed_ex(K.OP_CHECKSUM, a, L, L, n, out, K.KERNEL_VVSTREAM, 12,
+                                                                 **({"stream": st} if st else {}))),
+                    ("var  ", lambda st=None: ctx.batch_var_ex(K.OP_CHECKSUM, a, d_off, d_ln, n, out, K.KERNEL_VVSTREAM,
+                                                               12, packed=True, total_bytes=n * L,
+                                                               **({"stream": st} if st else {})))]
+            for name, fn in runs:
+                out.zero_()
+                fn()
+                torch.cuda.synchronize()
+                assert torch.equal(out, ref), name
+                ms = b2b(lambda: fn(s), s)
+                print(f"iso L={L} {name} vvstream policy: {ms:.4f} ms ({(n * L + 2 * n) / ms / 1e6 / 80:.1f}%)",
+                      flush=True)
+            del a, out, ref, d_off, d_ln
     else:
         raise SystemExit(f"unknown --what {what}")
 

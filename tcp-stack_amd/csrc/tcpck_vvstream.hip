@@ -36,6 +36,8 @@
 //   * a wave whose lengths disagree with the offsets (layout hint wrong)
 //     recomputes its images one by one.  kFill checks this before it writes
 //     anything into the arena.
+#include <type_traits>
+
 #include "tcpck_device.h"
 #include "tcpck_internal.h"
 
@@ -49,6 +51,7 @@ using dev::u32x4;
 
 constexpr uint32_t kRound = 256;  // ends loaded per round (4 per lane)
 constexpr uint32_t kRing = 512;   // LDS ring entries per wave (two rounds)
+constexpr uint32_t kMirror = 64;  // slots 0..63 repeated after the ring: a step's 64 reads never wrap
 
 struct VVArgs {
   uint8_t *arena;
@@ -79,7 +82,7 @@ template <int U, int OP, int SPLIT, int LAYOUT>
 __global__ void __launch_bounds__(kBlock) vvstream_kernel(VVArgs a) {
   constexpr bool FIXED = LAYOUT != 0;
   constexpr bool GAP = LAYOUT == 2;
-  __shared__ uint32_t s_end[kWavesPerBlock][FIXED ? 1 : kRing];
+  __shared__ uint32_t s_end[kWavesPerBlock][FIXED ? 1 : kRing + kMirror];
   __shared__ __attribute__((aligned(16))) uint32_t s_pre[kWavesPerBlock][256];  // packed u16 prefixes
   __shared__ uint32_t s_fld[kWavesPerBlock][OP == kFill ? 64 : 1];              // kFill: field word + 1 per chunk
   const uint32_t lane = threadIdx.x & 63;
@@ -165,10 +168,14 @@ __global__ void __launch_bounds__(kBlock) vvstream_kernel(VVArgs a) {
     uint32_t loaded = FIXED ? nv : 0;  // ends available (run-relative image count)
     uint32_t pos = lead;                 // end of the last written image
     bool short_fill = false;             // kFill: an image < 30 B (two fields per chunk possible)
+    // every end so far 4-B aligned: the step's prefix table then holds u32 P
+    // at dword positions (no packing), else packed u16 P at word positions
+    bool al4 = (lead & 3u) == 0 && (!FIXED || ((S & 3u) == 0 && (!GAP || (L & 3u) == 0)));
     auto fill_round = [&]() {            // write round (loaded / 256) from dnext, prefetch the next
       uint32_t d[4] = {dnext[0], dnext[1], dnext[2], dnext[3]};
       const uint32_t r = loaded / kRound;
       load_round(r + 1, dnext);
+      al4 = al4 && __ballot(((d[0] | d[1] | d[2] | d[3]) & 3u) != 0) == 0;  // lengths past nimg are 0
       const uint32_t e1 = d[0], e2 = e1 + d[1], e3 = e2 + d[2], e4 = e3 + d[3];
       const uint32_t incl = dev::wave_inclusive_scan(e4);
       const uint32_t ex = pos + incl - e4;
@@ -179,13 +186,30 @@ __global__ void __launch_bounds__(kBlock) vvstream_kernel(VVArgs a) {
         for (int i = 0; i < 4; ++i) sh |= (jb + i < nimg) && d[i] < 30;
         short_fill |= __ballot(sh) != 0;
       }
+      // ends past the batch read as ~0 (never inside a step)
+      const uint32_t jb = r * kRound + 4 * lane;
+      const uint32_t v0 = jb < nimg ? ex + e1 : ~0u, v1 = jb + 1 < nimg ? ex + e2 : ~0u;
+      const uint32_t v2 = jb + 2 < nimg ? ex + e3 : ~0u, v3 = jb + 3 < nimg ? ex + e4 : ~0u;
       const uint32_t si = (r * kRound) % kRing + 4 * lane;
-      ring_end[si] = ex + e1;
-      ring_end[si + 1] = ex + e2;
-      ring_end[si + 2] = ex + e3;
-      ring_end[si + 3] = ex + e4;
+      ring_end[si] = v0;
+      ring_end[si + 1] = v1;
+      ring_end[si + 2] = v2;
+      ring_end[si + 3] = v3;
+      if (si < kMirror) {
+        ring_end[kRing + si] = v0;
+        ring_end[kRing + si + 1] = v1;
+        ring_end[kRing + si + 2] = v2;
+        ring_end[kRing + si + 3] = v3;
+      }
       pos = pos + dev::read_lane(incl, 63);
       loaded += kRound;
+      if (loaded >= nimg) {
+        // the last round: the 64 slots after it (consumed ends of the round
+        // before) read as ~0 too, for the steps' reads past nimg
+        const uint32_t sn = loaded % kRing + lane;
+        ring_end[sn] = ~0u;
+        if (sn < kMirror) ring_end[kRing + sn] = ~0u;
+      }
       __builtin_amdgcn_wave_barrier();  // ends are read by other lanes
     };
     if constexpr (!FIXED) {
@@ -220,92 +244,115 @@ __global__ void __launch_bounds__(kBlock) vvstream_kernel(VVArgs a) {
         return ring_end[j % kRing];
       }
     };
-
-    for (uint32_t g = 0; g < nsteps && !bad; g += U) {
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const uint32_t st = g + u;
-        const uint32_t sb = st << 10;
-        const uint32_t c = sb + (lane << 4);
-        u32x4 w = ring[u];
-        if (sb == 0 || sb + 1024 > span) {
-          const int32_t lo = min(max(static_cast<int32_t>(lead) - static_cast<int32_t>(c), 0), 16);
-          const int32_t hi = min(max(static_cast<int32_t>(span) - static_cast<int32_t>(c), 0), 16);
-          w = dev::apply_mask(w, dev::word_mask(lo, hi));
-        }
-        // the step's first ends, read before the sums (the LDS latency overlaps them)
-        if (!FIXED && jn + 66 > loaded && loaded < nimg) fill_round();  // >= 64 ends (+ 1 field) ahead
-        uint32_t j = jn + lane;
-        uint32_t e = j < nv ? end_of(j) : ~0u;
-        if constexpr (OP == kFill) {  // zero the checksum fields that lie in this step
-          const uint32_t i = fj + lane;
-          uint32_t f;
-          if constexpr (FIXED)
-            f = lead + i * S + 28;
-          else
-            f = (i == 0 ? lead : (i < nimg ? end_of(i - 1) : span)) + 28;
-          const bool inf = i < nimg && f < sb + 1024;
-          const uint64_t bf = __ballot(inf);
-          if (bf) {
-            if (inf) fld[(f - sb) >> 4] = ((f & 15u) >> 1) + 1u;  // post the word to the chunk's lane
-            __builtin_amdgcn_wave_barrier();
-            const uint32_t q = fld[lane];
-            if (q) {
-              fld[lane] = 0u;
-              w = zero_word(w, q - 1u);
-            }
-            __builtin_amdgcn_wave_barrier();
-            fj += static_cast<uint32_t>(__popcll(bf));
-          }
-        }
-        const uint32_t q1 = dev::dot2_u16(w.x, 0u);
-        const uint32_t q2 = dev::dot2_u16(w.y, q1);
-        const uint32_t q3 = dev::dot2_u16(w.z, q2);
-        const uint32_t tot = dev::dot2_u16(w.w, q3);
-        const uint32_t incl = dev::wave_inclusive_scan(tot);
-        bool table = false;
-        for (;;) {  // once per step unless it holds more than 64 ends
-          const bool inb = e < sb + 1024;
-          const uint64_t bal = __ballot(inb);
-          if (!bal) break;
-          if (!table) {
-            // P at the chunk start, then at word positions 2i (P = a + q_i) and
-            // 2i + 1 (+ the low word of dword i), packed low/high per dword
-            const uint32_t p0 = carry + incl - tot;
-            const uint32_t b1 = p0 + q1, b2 = p0 + q2, b3 = p0 + q3;
-            pre4[lane] = u32x4{__builtin_amdgcn_perm(p0 + w.x, p0, 0x05040100u),
-                               __builtin_amdgcn_perm(b1 + w.y, b1, 0x05040100u),
-                               __builtin_amdgcn_perm(b2 + w.z, b2, 0x05040100u),
-                               __builtin_amdgcn_perm(b3 + w.w, b3, 0x05040100u)};
-            __builtin_amdgcn_wave_barrier();  // cross-lane LDS reads below
-            table = true;
-          }
-          const uint32_t cnt = static_cast<uint32_t>(__popcll(bal));  // lanes 0..cnt-1 (ends ascend)
-          const uint32_t P = pre16[inb ? ((e - sb) >> 1) : 0u];      // the table is laid out like the step
-          const uint32_t pl = static_cast<uint32_t>(
-              __builtin_amdgcn_update_dpp(static_cast<int>(p_last), static_cast<int>(P), 0x138, 0xF, 0xF, false));
-          const uint32_t pprev = lane == 0 ? p_last : pl;  // wave_shr:1
-          if constexpr (OP == kFill) {
-            const uint32_t el = static_cast<uint32_t>(
-                __builtin_amdgcn_update_dpp(static_cast<int>(e_last), static_cast<int>(e), 0x138, 0xF, 0xF, false));
-            const uint32_t start = lane == 0 ? e_last : el;  // image jn + lane starts where jn + lane - 1 ends
-            if (inb && (!GAP || (j & 1u))) store(kb + (GAP ? j >> 1 : j), P - pprev, A0 + start);
-          } else {
-            if (inb && (!GAP || (j & 1u))) store(kb + (GAP ? j >> 1 : j), P - pprev, 0);
-          }
-          p_last = dev::read_lane(P, cnt - 1);
-          e_last = dev::read_lane(e, cnt - 1);
-          jn += cnt;
-          if (cnt < 64) break;
-          if (!FIXED && jn + 66 > loaded && loaded < nimg) fill_round();
-          j = jn + lane;
-          e = j < nv ? end_of(j) : ~0u;
-        }
-        __builtin_amdgcn_wave_barrier();  // the next step rewrites the table
-        carry += dev::read_lane(incl, 63);
-        ring[u] = load_step(st + U);
+    // the ends of images jn + lane, ~0 past the batch
+    auto ends_at = [&](uint32_t jn0) -> uint32_t {
+      if constexpr (FIXED) {
+        const uint32_t j = jn0 + lane;
+        return j < nv ? end_of(j) : ~0u;
+      } else {
+        return ring_end[jn0 % kRing + lane];  // mirrored: no wrap
       }
-    }
+    };
+
+    // AL4 (every end of the run 4-B aligned; decided once per run): the
+    // prefix table holds u32 P at dword positions, no packing
+    auto stream_run = [&](auto al4_tag) {
+      constexpr bool AL4 = decltype(al4_tag)::value;
+      for (uint32_t g = 0; g < nsteps && !bad; g += U) {
+  #pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const uint32_t st = g + u;
+          const uint32_t sb = st << 10;
+          const uint32_t c = sb + (lane << 4);
+          u32x4 w = ring[u];
+          if (sb == 0 || sb + 1024 > span) {
+            const int32_t lo = min(max(static_cast<int32_t>(lead) - static_cast<int32_t>(c), 0), 16);
+            const int32_t hi = min(max(static_cast<int32_t>(span) - static_cast<int32_t>(c), 0), 16);
+            w = dev::apply_mask(w, dev::word_mask(lo, hi));
+          }
+          // the step's first ends, read before the sums (the LDS latency overlaps them)
+          if (!FIXED && jn + 66 > loaded && loaded < nimg) fill_round();  // >= 64 ends (+ 1 field) ahead
+          uint32_t j = jn + lane;
+          uint32_t e = ends_at(jn);
+          if constexpr (OP == kFill) {  // zero the checksum fields that lie in this step
+            const uint32_t i = fj + lane;
+            uint32_t f;
+            if constexpr (FIXED)
+              f = lead + i * S + 28;
+            else
+              f = (i == 0 ? lead : (i < nimg ? end_of(i - 1) : span)) + 28;
+            const bool inf = i < nimg && f < sb + 1024;
+            const uint64_t bf = __ballot(inf);
+            if (bf) {
+              if (inf) fld[(f - sb) >> 4] = ((f & 15u) >> 1) + 1u;  // post the word to the chunk's lane
+              __builtin_amdgcn_wave_barrier();
+              const uint32_t q = fld[lane];
+              if (q) {
+                fld[lane] = 0u;
+                w = zero_word(w, q - 1u);
+              }
+              __builtin_amdgcn_wave_barrier();
+              fj += static_cast<uint32_t>(__popcll(bf));
+            }
+          }
+          const uint32_t q1 = dev::dot2_u16(w.x, 0u);
+          const uint32_t q2 = dev::dot2_u16(w.y, q1);
+          const uint32_t q3 = dev::dot2_u16(w.z, q2);
+          const uint32_t tot = dev::dot2_u16(w.w, q3);
+          const uint32_t incl = dev::wave_inclusive_scan(tot);
+          bool table = false;
+          for (;;) {  // once per step unless it holds more than 64 ends
+            const bool inb = e < sb + 1024;
+            const uint64_t bal = __ballot(inb);
+            if (!bal) break;
+            if (!table) {
+              // P at the chunk start, then at word positions 2i (P = a + q_i) and
+              // 2i + 1 (+ the low word of dword i): u32 at the dword positions
+              // when every end is 4-B aligned, else packed low/high per dword
+              const uint32_t p0 = carry + incl - tot;
+              const uint32_t b1 = p0 + q1, b2 = p0 + q2, b3 = p0 + q3;
+              if constexpr (AL4)
+                pre4[lane] = u32x4{p0, b1, b2, b3};
+              else
+                pre4[lane] = u32x4{__builtin_amdgcn_perm(p0 + w.x, p0, 0x05040100u),
+                                   __builtin_amdgcn_perm(b1 + w.y, b1, 0x05040100u),
+                                   __builtin_amdgcn_perm(b2 + w.z, b2, 0x05040100u),
+                                   __builtin_amdgcn_perm(b3 + w.w, b3, 0x05040100u)};
+              __builtin_amdgcn_wave_barrier();  // cross-lane LDS reads below
+              table = true;
+            }
+            const uint32_t cnt = static_cast<uint32_t>(__popcll(bal));  // lanes 0..cnt-1 (ends ascend)
+            const uint32_t off = min(e - sb, 1022u);                    // the table is laid out like the step
+            const uint32_t P = AL4 ? s_pre[wv][off >> 2] : static_cast<uint32_t>(pre16[off >> 1]);
+            // P of image jn + lane - 1: lane 0 keeps p_last (wave_shr:1, bound_ctrl off)
+            const uint32_t pprev = static_cast<uint32_t>(
+                __builtin_amdgcn_update_dpp(static_cast<int>(p_last), static_cast<int>(P), 0x138, 0xF, 0xF, false));
+            if constexpr (OP == kFill) {
+              const uint32_t el = static_cast<uint32_t>(
+                  __builtin_amdgcn_update_dpp(static_cast<int>(e_last), static_cast<int>(e), 0x138, 0xF, 0xF, false));
+              const uint32_t start = lane == 0 ? e_last : el;  // image jn + lane starts where jn + lane - 1 ends
+              if (inb && (!GAP || (j & 1u))) store(kb + (GAP ? j >> 1 : j), P - pprev, A0 + start);
+            } else {
+              if (inb && (!GAP || (j & 1u))) store(kb + (GAP ? j >> 1 : j), P - pprev, 0);
+            }
+            p_last = dev::read_lane(P, cnt - 1);
+            e_last = dev::read_lane(e, cnt - 1);
+            jn += cnt;
+            if (cnt < 64) break;
+            if (!FIXED && jn + 66 > loaded && loaded < nimg) fill_round();  // never with AL4
+            j = jn + lane;
+            e = ends_at(jn);
+          }
+          __builtin_amdgcn_wave_barrier();  // the next step rewrites the table
+          carry += dev::read_lane(incl, 63);
+          ring[u] = load_step(st + U);
+        }
+      }
+    };
+    if (al4 && (FIXED || loaded >= nimg))
+      stream_run(std::true_type{});
+    else
+      stream_run(std::false_type{});
     if constexpr (!FIXED) bad = bad || pos != span || loaded < nimg;
     if (!bad && jn < nv) {  // ends exactly at the last step's end (= span): the first gets the rest
       const uint32_t rem = nv - jn;
