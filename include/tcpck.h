@@ -118,6 +118,25 @@ int tcpck_batch_var(tcpck_ctx *ctx, int op, int mode, void *d_arena,
                     uint64_t count, void *d_out, const tcpck_layout *layout,
                     tcpck_stream stream);
 
+/* ---- batched retransmit: ACK rewrite, incremental checksum update --------
+ * The resend path: ResendPredicate rewrites the ACK number of each queued
+ * packet (include/socket-internal.h:376-377, AcknowledgementNumber() =
+ * htonl(rcv_nxt)) and SendPacket then recomputes the whole checksum
+ * (src/socket-manager.cc:9-10).  Here, for every image k: bytes 20-23
+ * (TCPCK_ACK_OFFSET, AcknowledgementNumber) := htonl(ack_k), and the stored
+ * checksum (bytes 28-29) is updated from the two old and new u16 words --
+ * C' = ~(~C - old + new) mod 2^16 (TCPCK_MODE_REF) or RFC 1624 eqn. 3
+ * (TCPCK_MODE_RFC1071) -- which equals the full recompute whenever C was the
+ * valid checksum of the old image (e.g. written by TCPCK_OP_FILL).
+ * d_offsets == NULL: image k at k * stride (stride even, >= 30); else image k
+ * at d_offsets[k] (precondition: even, image >= 30 B).  d_acks: u32[count],
+ * host order; NULL: every image gets `ack`.  d_out: u16[count] receiving C'
+ * (may be NULL).  Asynchronous on `stream`. */
+#define TCPCK_ACK_OFFSET 20
+int tcpck_batch_set_ack(tcpck_ctx *ctx, int mode, void *d_arena, const uint64_t *d_offsets,
+                        uint64_t stride, uint64_t count, const uint32_t *d_acks, uint32_t ack,
+                        uint16_t *d_out, tcpck_stream stream);
+
 /* ---- batched, host memory (end to end incl. PCIe) ------------------------
  * Segments start and end in host memory (the loopback/socket buffers of
  * network-service.cc / tcp-buffer.h).  The batch is split into chunks that are

@@ -447,6 +447,31 @@ int tcpck_batch_var_ex(tcpck_ctx *ctx, int op, int mode, void *d_arena, const ui
                             d_out, layout, kernel, param, static_cast<hipStream_t>(stream)));
 }
 
+// ---- batched retransmit: ACK rewrite + incremental update ----------------------
+int tcpck_batch_set_ack(tcpck_ctx *ctx, int mode, void *d_arena, const uint64_t *d_offsets, uint64_t stride,
+                        uint64_t count, const uint32_t *d_acks, uint32_t ack, uint16_t *d_out,
+                        tcpck_stream stream) {
+  if (!ctx || (mode != TCPCK_MODE_REF && mode != TCPCK_MODE_RFC1071)) return TCPCK_EINVAL;
+  if (count == 0) return TCPCK_OK;
+  if (!d_arena) return TCPCK_EINVAL;
+  if (!d_offsets) {
+    if ((stride & 1) || (count > 1 && stride < 30)) return TCPCK_EINVAL;
+    if (count > 1 && stride > (UINT64_MAX - 30) / (count - 1)) return TCPCK_EINVAL;
+  }
+  DeviceGuard g(ctx->device);
+  if (g.status() != hipSuccess) return hip_status(g.status());
+  tcpck::AckArgs a{};
+  a.arena = static_cast<uint8_t *>(d_arena);
+  a.offsets = d_offsets;
+  a.stride = stride;
+  a.count = count;
+  a.acks = d_acks;
+  a.ack = ack;
+  a.out = d_out;
+  return hip_status(tcpck::launch_set_ack(mode, a, static_cast<uint32_t>(ctx->num_cus),
+                                          static_cast<hipStream_t>(stream)));
+}
+
 // ---- batched, host memory: chunked H2D -> kernel -> D2H on two streams ---------
 int tcpck_host_batch_fixed(tcpck_ctx *ctx, int op, int mode, void *h_arena, uint64_t stride,
                            uint32_t len, uint64_t count, void *h_out) {

@@ -78,6 +78,18 @@ hipError_t launch_rstream(int op, int variant, const FixedStreamArgs &a, uint32_
 // 4 = policy (oversubscription, split and loads in flight by size)
 hipError_t launch_vvstream(int op, int variant, bool fixed, const RunArgs &a, uint32_t num_cus, hipStream_t stream);
 // timing-only streaming micro-kernels (tcpck_diag.hip)
+// ---- retransmit ACK rewrite with incremental checksum update (tcpck_resend.hip) ----
+struct AckArgs {
+  uint8_t *arena;
+  const uint64_t *offsets;  // null: image k at k * stride
+  uint64_t stride;
+  uint64_t count;
+  const uint32_t *acks;     // per-image ACK numbers (host order); null: `ack` for all
+  uint32_t ack;
+  uint16_t *out;            // new checksums (may be null)
+};
+hipError_t launch_set_ack(int mode, const AckArgs &a, uint32_t num_cus, hipStream_t stream);
+
 hipError_t launch_diag_stream(int variant, const uint8_t *buf, uint64_t bytes, uint32_t *out, uint32_t num_cus,
                               hipStream_t s);
 

@@ -48,7 +48,7 @@ EXPORTS = (
     "tcpck_abi_version", "tcpck_strerror", "tcpck_device_supported",
     "tcpck_ctx_create", "tcpck_ctx_destroy", "tcpck_ctx_device",
     "tcpck_checksum16", "tcpck_fill16", "tcpck_update16",
-    "tcpck_batch_fixed", "tcpck_batch_var",
+    "tcpck_batch_fixed", "tcpck_batch_var", "tcpck_batch_set_ack",
     "tcpck_host_batch_fixed", "tcpck_host_batch_var", "tcpck_ctx_set_chunk_bytes",
     "tcpck_host_alloc", "tcpck_host_free", "tcpck_device_alloc", "tcpck_device_free",
     "tcpck_memcpy_h2d", "tcpck_memcpy_d2h", "tcpck_stream_sync",
@@ -92,6 +92,7 @@ def lib() -> ctypes.CDLL:
         "tcpck_update16": (ctypes.c_uint16, [ctypes.c_uint16, ctypes.c_uint16, ctypes.c_uint16, i32]),
         "tcpck_batch_fixed": (i32, [vp, i32, i32, vp, u64, u32, u64, vp, vp]),
         "tcpck_batch_var": (i32, [vp, i32, i32, vp, vp, vp, u64, vp, ctypes.POINTER(Layout), vp]),
+        "tcpck_batch_set_ack": (i32, [vp, i32, vp, vp, u64, u64, vp, u32, vp, vp]),
         "tcpck_host_batch_fixed": (i32, [vp, i32, i32, vp, u64, u32, u64, vp]),
         "tcpck_host_batch_var": (i32, [vp, i32, i32, vp, vp, vp, u64, vp]),
         "tcpck_ctx_set_chunk_bytes": (i32, [vp, u64]),
@@ -232,6 +233,14 @@ class Context:
         _check(lib().tcpck_batch_var(self._h, op, mode, _ptr(arena), _ptr(offsets), _ptr(lengths),
                                      count, _ptr(out), ctypes.byref(lay), _stream(stream)),
                "tcpck_batch_var")
+
+    def batch_set_ack(self, arena, count: int, ack: int = 0, acks=None, offsets=None, stride: int = 0,
+                      out=None, mode: int = MODE_REF, stream=None) -> None:
+        """Retransmit batch (socket-internal.h:376-377 + socket-manager.cc:9-10): bytes 20-23 of every
+        image := htonl(ack or acks[k]), checksum at 28-29 updated incrementally (tcpck_batch_set_ack)."""
+        _check(lib().tcpck_batch_set_ack(self._h, mode, _ptr(arena), _ptr(offsets), stride, count,
+                                         _ptr(acks), ack & 0xFFFFFFFF, _ptr(out), _stream(stream)),
+               "tcpck_batch_set_ack")
 
     # explicit kernel choice (include/tcpck_tuning.h)
     def batch_fixed_ex(self, op: int, arena, stride: int, length: int, count: int, out, kernel: int,

@@ -283,3 +283,83 @@ def test_host_batch_var_vs_oracle(ctx, oracle_c):
     ctx.set_chunk_bytes(16 << 20)
     ctx.host_batch_var(tcpck.OP_CHECKSUM, arena, off, ln, count, out)
     np.testing.assert_array_equal(out, oracle_c.batch(arena, off, ln, threads=8))
+
+
+# ---- retransmit: batched ACK rewrite + incremental update ----
+
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("layout", ["fixed", "var"])
+@pytest.mark.parametrize("per_image", [False, True])
+def test_set_ack_vs_resend_oracle(ctx, mode, layout, per_image):
+    """tcpck_batch_set_ack after FILL == the reference's resend path (ACK
+    rewrite, socket-internal.h:376-377, then SendPacket's full recompute,
+    socket-manager.cc:9-10) on every image: arena bytes and checksums."""
+    import tcpck
+    import synth_np
+    from oracle import ref16 as R
+    rng = np.random.default_rng(500 + mode + 2 * per_image)
+    if layout == "fixed":
+        stride, length, count = 1500, 1492, 20000
+        off = np.arange(count, dtype=np.int64) * stride
+        ln = np.full(count, length, np.int64)
+        total = stride * count
+    else:
+        count = 20000
+        off, ln, total = synth_np.mixed_layout(count, seed=11)
+        gaps = 2 * (np.arange(count) % 3 == 0)  # 2-B gaps: starts that are 2 mod 4
+        off = off.astype(np.int64) + np.cumsum(gaps)
+        total = int(off[-1] + ln[-1])
+    arena_np = rng.integers(0, 256, total + 64, dtype=np.uint8)
+    arena = dev(arena_np)
+    d_off = dev(off.astype(np.uint64))
+    d_ln = dev(ln.astype(np.uint32))
+    ctx.batch_var(tcpck.OP_FILL, arena, d_off, d_ln, count, None, mode=mode)
+    filled = host(arena)
+    acks = rng.integers(0, 2**32, count, dtype=np.uint64).astype(np.uint32) if per_image else np.uint32(0x9ABCDEF1)
+    out = torch.zeros(count, dtype=torch.int16, device="cuda")
+    kw = dict(acks=dev(acks)) if per_image else dict(ack=int(acks))
+    if layout == "fixed":
+        ctx.batch_set_ack(arena, count, stride=stride, out=out, mode=mode, **kw)
+    else:
+        ctx.batch_set_ack(arena, count, offsets=d_off, out=out, mode=mode, **kw)
+    exp_arena = filled.copy()
+    exp = R.resend_batch_np(exp_arena, off, ln, acks, mode)
+    np.testing.assert_array_equal(host(out).view(np.uint16), exp)
+    np.testing.assert_array_equal(host(arena), exp_arena)
+    ok = torch.empty(count, dtype=torch.uint8, device="cuda")
+    ctx.batch_var(tcpck.OP_VERIFY, arena, d_off, d_ln, count, ok, mode=mode)
+    assert bool(host(ok).all())
+
+
+def test_set_ack_c2_full_size_roundtrip(ctx, oracle_c):
+    """BASELINE C2 (1M x 1492 B): FILL, then two successive ACK rewrites; every image
+    verifies and the checksums equal a fresh FILL of the rewritten images."""
+    import tcpck
+    count, L = 1 << 20, 1492
+    a = _synth_fixed_dev(count, L, L)
+    ctx.batch_fixed(tcpck.OP_FILL, a, L, L, count, None)
+    acks = torch.arange(count, dtype=torch.int32, device="cuda") * 7 + 12345
+    out = torch.empty(count, dtype=torch.int16, device="cuda")
+    ctx.batch_set_ack(a, count, ack=0xFFFFFFFF, stride=L)
+    ctx.batch_set_ack(a, count, acks=acks, stride=L, out=out)
+    ok = torch.empty(count, dtype=torch.uint8, device="cuda")
+    ctx.batch_fixed(tcpck.OP_VERIFY, a, L, L, count, ok)
+    assert bool(host(ok).all())
+    b = a.clone()
+    refill = torch.empty(count, dtype=torch.int16, device="cuda")
+    ctx.batch_fixed(tcpck.OP_FILL, b, L, L, count, refill)
+    assert torch.equal(out, refill) and torch.equal(a, b)
+    hdr = host(a[: 64])
+    assert hdr[20:24].tolist() == list((12345).to_bytes(4, "big"))
+
+
+def test_set_ack_argument_errors(ctx):
+    import tcpck
+    a = torch.zeros(4096, dtype=torch.uint8, device="cuda")
+    with pytest.raises(tcpck.TcpckError):
+        ctx.batch_set_ack(a, 4, stride=63)   # odd stride
+    with pytest.raises(tcpck.TcpckError):
+        ctx.batch_set_ack(a, 4, stride=28)   # images shorter than the header
+    with pytest.raises(tcpck.TcpckError):
+        ctx.batch_set_ack(a, 4, stride=64, mode=5)
+    ctx.batch_set_ack(a, 0, stride=64)       # empty batch is a no-op
