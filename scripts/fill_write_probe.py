@@ -21,18 +21,27 @@ def main():
     buf = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
     tcpck.synth_fixed(buf, 1492, 1492, 1 << 20, seed=1)
     out = torch.empty(1 << 22, dtype=torch.int32, device="cuda")
-    names = {0: "no write", 1: "2 B", 2: "4 B", 3: "16 B", 4: "32 B", 5: "64 B", 6: "128 B", 7: "2 B, write-only pass", 8: "none, then a 2-B write-only pass"}
+    if "--store-policy" in sys.argv:
+        # store cache-policy bits (bit 0 sc0, bit 1 nt, bit 4 sc1) on the 2-B and 64-B field stores
+        names = {0x1000: "no write", 0x1001: "2 B", 0x1005: "64 B"}
+        for w, base in ((2, 0x4000), (64, 0x4100)):
+            for aux in (0, 1, 2, 3, 16, 17, 18, 19):
+                names[base | aux] = f"{w} B aux {aux}"
+    else:
+        names = {0x1000 | k: v for k, v in {
+            0: "no write", 1: "2 B", 2: "4 B", 3: "16 B", 4: "32 B", 5: "64 B", 6: "128 B",
+            7: "2 B, write-only pass", 8: "none, then a 2-B write-only pass"}.items()}
     t = {v: [] for v in names}
     for v in names:
         for _ in range(20):
-            ctx.diag_stream(0x1000 | v, buf, nbytes, out, stream=s)
+            ctx.diag_stream(v, buf, nbytes, out, stream=s)
     torch.cuda.synchronize()
     for _ in range(5):
         for v in names:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(s)
             for _ in range(10):
-                ctx.diag_stream(0x1000 | v, buf, nbytes, out, stream=s)
+                ctx.diag_stream(v, buf, nbytes, out, stream=s)
             e1.record(s)
             torch.cuda.synchronize()
             t[v].append(e0.elapsed_time(e1) / 10)

@@ -56,6 +56,7 @@ for s in ${STEPS:-tests smoke bench prof}; do
       step sq2 120 rocprofv3 --kernel-trace --pmc SQ_BUSY_CYCLES SQ_WAVES SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_WAIT_INST_LDS SQ_INST_CYCLES_VMEM_RD -d gpurun_out/sq2 -o run --output-format csv -- python3 scripts/pmc_probe.py ;;
     resend) step resend_tests 300 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread -k set_ack &&
       step resend 300 python scripts/resend_probe.py ;;
+    fillpol) step fillpol 300 python scripts/fill_write_probe.py --store-policy ;;
     iso) step iso 300 python scripts/xcd_probe.py --what iso ;;
     os_c3x) step os_c3x 600 python scripts/oversub.py --what c3 --variants 3,11 --ms 8,16,32,64 ;;
     xccmap) step xccmap 300 python scripts/xcc_map.py ;;

@@ -110,6 +110,13 @@ __device__ __forceinline__ uint32_t ref_chunk_sum_dot(u32x4 w) {
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *p, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), 0, static_cast<int>(bytes), 0x00020000);
 }
+// In-place 2-B store of a FILL result into the image's checksum field, with
+// the sc1 cache-policy bit: 4 % less time than a default-policy store for the
+// scattered field writes (scripts/fill_write_probe.py --store-policy,
+// profiles/r01/fill_store_policy.log; nt is worse).
+__device__ __forceinline__ void store16_field(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint16_t v) {
+  __builtin_amdgcn_raw_buffer_store_b16(v, r, static_cast<int>(voff), 0, 16);
+}
 __device__ __forceinline__ u32x4 load16_buf_nt(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
   typedef unsigned v4u __attribute__((ext_vector_type(4)));
   const v4u v = __builtin_amdgcn_raw_buffer_load_b128(r, static_cast<int>(voff), static_cast<int>(soff), 2);

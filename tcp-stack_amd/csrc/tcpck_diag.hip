@@ -183,7 +183,11 @@ hipError_t launch_cpol(const uint8_t *buf, uint64_t bytes, uint32_t *out, uint32
 // whose 16-B chunk lies in the W-byte block, writing back the data it read).
 // Answers: is the cost of FILL the sub-line write itself, and does a wider,
 // aligned write-back of data already in registers avoid it?
-template <int W>
+// SAUX >= 0: the field stores are raw buffer stores with cache-policy bits SAUX
+// (bit 0 sc0, bit 1 nt, bit 4 sc1): does a write-through / streaming store
+// reach HBM while the image's DRAM row is still open, instead of as a later
+// write-back of a partially dirty line?
+template <int W, int SAUX = -1>
 __global__ void __launch_bounds__(kBlock) diag_fill_kernel(uint8_t *buf, uint64_t bytes, uint32_t *out) {
   constexpr uint32_t kS = 1492;
   const uint32_t lane = threadIdx.x & 63;
@@ -200,6 +204,7 @@ __global__ void __launch_bounds__(kBlock) diag_fill_kernel(uint8_t *buf, uint64_
   auto ld = [&](uint32_t st) -> u32x4 {
     return dev::load16_nt(base + 16 * static_cast<uint64_t>(min((st << 6) + lane, last_chunk)));
   };
+  const auto wrsrc = dev::make_rsrc(base, static_cast<uint32_t>(b1 - b0));
   // first field at or after b0 (absolute), then every kS bytes
   uint64_t nf = ((b0 + kS - 1 - 28) / kS) * kS + 28;
   if (nf < b0) nf += kS;
@@ -222,12 +227,23 @@ __global__ void __launch_bounds__(kBlock) diag_fill_kernel(uint8_t *buf, uint64_
           if constexpr (W < 16) {
             const uint64_t blk = nf & ~static_cast<uint64_t>(W - 1);
             if (c <= blk && blk < c + 16) {
-              if (W == 2) *reinterpret_cast<uint16_t *>(buf + blk) = static_cast<uint16_t>(t);
-              if (W == 4) *reinterpret_cast<uint32_t *>(buf + blk) = t;
+              if constexpr (SAUX >= 0) {
+                __builtin_amdgcn_raw_buffer_store_b16(static_cast<uint16_t>(t), wrsrc, static_cast<int>(blk - b0), 0, SAUX);
+              } else {
+                if (W == 2) *reinterpret_cast<uint16_t *>(buf + blk) = static_cast<uint16_t>(t);
+                if (W == 4) *reinterpret_cast<uint32_t *>(buf + blk) = t;
+              }
             }
           } else {
             const uint64_t blk = nf & ~static_cast<uint64_t>(W - 1);
-            if (c >= blk && c + 16 <= blk + W && c + 16 <= b1) *reinterpret_cast<u32x4 *>(buf + c) = w;
+            if (c >= blk && c + 16 <= blk + W && c + 16 <= b1) {
+              if constexpr (SAUX >= 0) {
+                typedef unsigned v4u __attribute__((ext_vector_type(4)));
+                __builtin_amdgcn_raw_buffer_store_b128(v4u{w.x, w.y, w.z, w.w}, wrsrc, static_cast<int>(c - b0), 0, SAUX);
+              } else {
+                *reinterpret_cast<u32x4 *>(buf + c) = w;
+              }
+            }
           }
           nf += kS;
         }
@@ -247,11 +263,26 @@ __global__ void __launch_bounds__(kBlock) diag_scatter_kernel(uint8_t *buf, uint
   if (W == 4) *reinterpret_cast<uint32_t *>(buf + k * 1492 + 28) = static_cast<uint32_t>(v + k);
 }
 
-template <int W>
+template <int W, int SAUX = -1>
 hipError_t launch_fill(uint8_t *buf, uint64_t bytes, uint32_t *out, uint32_t num_cus, hipStream_t s) {
-  static const uint32_t per_cu = dev::resident_blocks_per_cu(diag_fill_kernel<W>);
-  hipLaunchKernelGGL((diag_fill_kernel<W>), dim3(per_cu * num_cus * 8), dim3(kBlock), 0, s, buf, bytes, out);
+  static const uint32_t per_cu = dev::resident_blocks_per_cu(diag_fill_kernel<W, SAUX>);
+  hipLaunchKernelGGL((diag_fill_kernel<W, SAUX>), dim3(per_cu * num_cus * 8), dim3(kBlock), 0, s, buf, bytes, out);
   return hipGetLastError();
+}
+
+template <int W>
+hipError_t launch_fill_aux(int aux, uint8_t *buf, uint64_t bytes, uint32_t *out, uint32_t num_cus, hipStream_t s) {
+  switch (aux) {
+    case 0: return launch_fill<W, 0>(buf, bytes, out, num_cus, s);
+    case 1: return launch_fill<W, 1>(buf, bytes, out, num_cus, s);
+    case 2: return launch_fill<W, 2>(buf, bytes, out, num_cus, s);
+    case 3: return launch_fill<W, 3>(buf, bytes, out, num_cus, s);
+    case 16: return launch_fill<W, 16>(buf, bytes, out, num_cus, s);
+    case 17: return launch_fill<W, 17>(buf, bytes, out, num_cus, s);
+    case 18: return launch_fill<W, 18>(buf, bytes, out, num_cus, s);
+    case 19: return launch_fill<W, 19>(buf, bytes, out, num_cus, s);
+    default: return hipErrorInvalidValue;
+  }
 }
 
 template <int LPB, int U, bool SCAN>
@@ -272,6 +303,11 @@ hipError_t launch_one(const uint8_t *buf, uint64_t bytes, uint32_t *out, uint32_
 // image (w = 0 none, 1 2 B, 2 4 B, 3 16 B, 4 32 B, 5 64 B, 6 128 B)
 hipError_t launch_diag_stream(int variant, const uint8_t *buf, uint64_t bytes, uint32_t *out, uint32_t num_cus,
                               hipStream_t s) {
+  if (variant >= 0x4000) {  // in-place FILL write cost with store cache-policy bits: 0x4000 | aux (2 B), 0x4100 | aux (64 B)
+    uint8_t *wb = const_cast<uint8_t *>(buf);
+    return (variant & 0x100) ? launch_fill_aux<64>(variant & 0xFF, wb, bytes, out, num_cus, s)
+                             : launch_fill_aux<2>(variant & 0xFF, wb, bytes, out, num_cus, s);
+  }
   if (variant >= 0x3000) {  // nt stream, run order by XCD (bit 0) and grid multiple (bits 8..15)
     const uint32_t m = (variant >> 8) & 0xFu ? static_cast<uint32_t>((variant >> 8) & 0xFu) * 4u : 8u;
     return (variant & 1) ? launch_cpol<2, true>(buf, bytes, out, num_cus, s, m)

@@ -117,7 +117,7 @@ __global__ void __launch_bounds__(kBlock) rstream_kernel(FixedStreamArgs a) {
         static_cast<uint8_t *>(a.out)[k] = (c == 0) ? 1 : 0;
       } else {
         if (a.out) static_cast<uint16_t *>(a.out)[k] = c;
-        if (OP == kFill) *reinterpret_cast<uint16_t *>(a.arena + k * S + 28) = c;  // tcp-header.h:177
+        if (OP == kFill) dev::store16_field(rsrc, (out_rel + lane) * S + lead + 28, c);  // tcp-header.h:177
       }
     }
   };

@@ -131,6 +131,16 @@ __global__ void __launch_bounds__(kBlock) vvstream_kernel(VVArgs a) {
       if (OP == kFill) *reinterpret_cast<uint16_t *>(arena + start + 28) = c;  // raw, as the reference
     }
   };
+  // the streaming path's form: start_rel run-relative (from A0), field store through the run's rsrc
+  auto store_rel = [&](uint64_t k, uint32_t sum, uint32_t start_rel, __amdgpu_buffer_rsrc_t r) {
+    const uint16_t c = static_cast<uint16_t>(~sum);  // tcp-header.h:262
+    if constexpr (OP == kVerify) {
+      static_cast<uint8_t *>(a.out)[k] = (c == 0) ? 1 : 0;
+    } else {
+      if (a.out) static_cast<uint16_t *>(a.out)[k] = c;
+      if (OP == kFill) dev::store16_field(r, start_rel + 28, c);  // raw, as the reference
+    }
+  };
 
   if (!bad) {
     const uint32_t lead = static_cast<uint32_t>(s0 - A0);
@@ -331,7 +341,7 @@ __global__ void __launch_bounds__(kBlock) vvstream_kernel(VVArgs a) {
               const uint32_t el = static_cast<uint32_t>(
                   __builtin_amdgcn_update_dpp(static_cast<int>(e_last), static_cast<int>(e), 0x138, 0xF, 0xF, false));
               const uint32_t start = lane == 0 ? e_last : el;  // image jn + lane starts where jn + lane - 1 ends
-              if (inb && (!GAP || (j & 1u))) store(kb + (GAP ? j >> 1 : j), P - pprev, A0 + start);
+              if (inb && (!GAP || (j & 1u))) store_rel(kb + (GAP ? j >> 1 : j), P - pprev, start, rsrc);
             } else {
               if (inb && (!GAP || (j & 1u))) store(kb + (GAP ? j >> 1 : j), P - pprev, 0);
             }
@@ -358,7 +368,7 @@ __global__ void __launch_bounds__(kBlock) vvstream_kernel(VVArgs a) {
       const uint32_t rem = nv - jn;
       for (uint32_t i = lane; i < rem; i += 64) {
         const uint32_t v = jn + i;
-        if (!GAP || (v & 1u)) store(kb + (GAP ? v >> 1 : v), i == 0 ? carry - p_last : 0u, A0 + (i == 0 ? e_last : span));
+        if (!GAP || (v & 1u)) store_rel(kb + (GAP ? v >> 1 : v), i == 0 ? carry - p_last : 0u, i == 0 ? e_last : span, rsrc);
       }
       jn = nv;
     }
