@@ -57,6 +57,8 @@ for s in ${STEPS:-tests smoke bench prof}; do
     resend) step resend_tests 300 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread -k set_ack &&
       step resend 300 python scripts/resend_probe.py ;;
     fillpol) step fillpol 300 python scripts/fill_write_probe.py --store-policy ;;
+    pmc_rs) step pmc_rs 120 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d gpurun_out/pmc_rs -o run --output-format csv -- python3 scripts/pmc_probe.py --rs ;;
+    os_c5x) step os_c5x 600 python scripts/oversub.py --what c5,c2 --variants 18,20,21 --ms 16,32,64,128 ;;
     iso) step iso 300 python scripts/xcd_probe.py --what iso ;;
     os_c3x) step os_c3x 600 python scripts/oversub.py --what c3 --variants 3,11 --ms 8,16,32,64 ;;
     xccmap) step xccmap 300 python scripts/xcc_map.py ;;

@@ -33,6 +33,14 @@ def run(fn, n=5):
 def main():
     ctx = tcpck.Context(0)
     n, L = 1 << 20, 1492
+    if "--rs" in sys.argv:  # rstream 18 vs 20 (default-policy first step): FETCH_SIZE per launch
+        a = torch.empty(n * L, dtype=torch.uint8, device="cuda")
+        K.synth_fixed(a, L, L, n, seed=42)
+        out = torch.empty(n, dtype=torch.int16, device="cuda")
+        for v in (18, 20):
+            run(lambda: ctx.batch_fixed_ex(K.OP_CHECKSUM, a, L, L, n, out, K.KERNEL_RSTREAM, v | (32 << 16)))
+        print("ok", flush=True)
+        return
     a = torch.empty(n * L, dtype=torch.uint8, device="cuda")
     K.synth_fixed(a, L, L, n, seed=42)
     out = torch.empty(n, dtype=torch.int16, device="cuda")

@@ -162,11 +162,15 @@ void free_stage(tcpck_ctx *ctx) {
 // steps) -- seg.
 constexpr uint64_t kRunMaxLen = 16384;  // above: seg (one wave per jumbo image already streams whole steps)
 // Policy parameters.  Every kernel takes its runs in the XCD-chunked block
-// order (dev::ordered_block, groups of 16 blocks per XCD): neighbouring runs
-// share an XCD's L2, so the run-edge lines and the partial lines of out[] that
-// neighbouring blocks share merge there (C2 86.3% -> 90.6%, C3 82.7 -> 84.1%,
-// C4 85.5 -> 87.4%, profiles/r01/xcd_*.log).
-constexpr int kRstreamPolicy = 18;       // v_dot2 sums, buffer loads, XCD-chunked order
+// order (dev::ordered_block, groups of 16 blocks per XCD): each XCD streams
+// compact regions instead of every eighth run (C2 86.3% -> 90.6%, C3 82.7 ->
+// 84.1%, C4 85.5 -> 87.4%, profiles/r01/xcd_*.log; the HBM bytes do not
+// change, PMC).  rstream also reads each run's first step with the default
+// cache policy: that line is the previous run's last line, and the
+// neighbour's last step then finds it in L2 (PMC bytes x1.015 -> x1.000);
+// with up to 128 x the resident grid for large batches (C5 84.7 -> 88.3%,
+// profiles/r01/oversub_c5_first_step.log).
+constexpr int kRstreamPolicy = 20;       // v_dot2 sums, buffer loads, XCD-chunked order, L2-kept first step
 constexpr int kVvPolicy = 4 | 8;         // size policy, XCD-chunked order
 constexpr int kSegXcdOrder = 1 << 24;    // seg: XCD-chunked order
 

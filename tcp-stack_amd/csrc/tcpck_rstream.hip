@@ -43,6 +43,7 @@ using dev::u32x4;
 // 224 us in slot 7 of a C2 launch (scripts/stamps.py).
 // FLAV bit 0: chunk sums with v_dot2_u32_u16; bit 1: buffer (SRSRC) loads with
 // the step offset in an SGPR instead of per-lane 64-bit clamped addresses;
+// bit 2 (with bit 1): the run's first step read with the default cache policy;
 // a.order (runtime): the block order, dev::ordered_block -- the XCD orders let
 // neighbouring runs share an XCD, so the results of neighbouring blocks that
 // share a 128-B line of out[] leave one L2 as whole lines instead of partial
@@ -132,7 +133,18 @@ __global__ void __launch_bounds__(kBlock) rstream_kernel(FixedStreamArgs a) {
 
   u32x4 ring[U];
 #pragma unroll
-  for (int u = 0; u < U; ++u) ring[u] = load_step(static_cast<uint32_t>(u));
+  for (int u = 0; u < U; ++u) {
+    if (u == 0 && (FLAV & 6) == 6) {
+      // step 0 with the default policy: its first line is the previous run's
+      // last line; kept in L2 (nt lines go first), the neighbour's last step
+      // can find it there instead of reading it from HBM a second time
+      typedef unsigned v4u __attribute__((ext_vector_type(4)));
+      const v4u v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, static_cast<int>(lane << 4), 0, 0);
+      ring[0] = u32x4{v.x, v.y, v.z, v.w};
+    } else {
+      ring[u] = load_step(static_cast<uint32_t>(u));
+    }
+  }
 
   for (uint32_t g = 0; g < nsteps; g += U) {
 #pragma unroll
@@ -199,7 +211,8 @@ hipError_t launch_one(const FixedStreamArgs &a, uint32_t num_cus, hipStream_t st
   static const uint32_t per_cu = dev::resident_blocks_per_cu(rstream_kernel<U, OP, STAMP, PRIO, FLAV>);
   const uint32_t cap = (a.blocks_per_cu && a.blocks_per_cu < per_cu) ? a.blocks_per_cu : per_cu;
   const uint64_t resident = static_cast<uint64_t>(cap) * num_cus;
-  uint64_t blocks = resident * dev::oversub_for(a.oversub, a.count * a.stride, resident * kWavesPerBlock, 32);
+  // runs of >= 4 KiB, up to 128 x the resident grid (C2: 32, C5: 128)
+  uint64_t blocks = resident * dev::oversub_for(a.oversub, a.count * a.stride, resident * kWavesPerBlock, 128);
   const uint64_t need = (a.count + kWavesPerBlock - 1) / kWavesPerBlock;  // >= 1 image per wave
   if (blocks > need) blocks = need;
   if (blocks == 0) return hipSuccess;
@@ -243,6 +256,11 @@ hipError_t launch_rstream(int op, int variant, const FixedStreamArgs &a, uint32_
     case 11: return dispatch<4, false, 0, 2>(op, a, num_cus, stream);
     case 12: return dispatch<2, false, 0, 3>(op, a, num_cus, stream);
     case 13: return dispatch<8, false, 0, 3>(op, a, num_cus, stream);
+    case 20: case 21: {  // 18 / 14 with the first step read with the default policy (FLAV bit 2)
+      FixedStreamArgs b = a;
+      b.order = variant == 20 ? 4u : dev::kOrderXcd;
+      return dispatch<4, false, 0, 7>(op, b, num_cus, stream);
+    }
     case 14: case 15: case 16: case 17: case 18: case 19: {
       // 10 (14, 16-19) or 13 (15) with an XCD order: whole regions (14, 15) or
       // interleaved groups of 2, 4, 16, 64 blocks (16-19)
