@@ -32,7 +32,9 @@ extern "C" {
                                   with buffer loads; 14/15: 10/13 with each XCD
                                   taking one contiguous region of runs; 16-19: 10
                                   with each XCD taking groups of 2/4/16/64
-                                  consecutive runs, 18 = the policy's)
+                                  consecutive runs; 20/21: 18/14 with the run's
+                                  first step read with the default cache policy,
+                                  20 = the policy's)
                                   | (blocks per CU cap << 8)
                                   | (grid oversubscription << 16: 0 = by batch
                                   size, 1 = none, M = M x the resident grid)    */
@@ -44,8 +46,9 @@ extern "C" {
                                    flight, byte-balanced runs, 1: 8; 2/3: same
                                    with equal-count runs -- fixed layouts are
                                    always equal-count; 4: policy; + 8: each XCD
-                                   takes groups of 16 consecutive runs, 12 = the
-                                   policy's)
+                                   takes groups of 16 consecutive runs; + 16: the
+                                   run's first step read with the default cache
+                                   policy; 28 = the policy's)
                                    | (grid oversubscription << 16: 0 = by batch
                                    size, 1 = none, M = M x the resident grid)   */
 

@@ -59,6 +59,8 @@ for s in ${STEPS:-tests smoke bench prof}; do
     fillpol) step fillpol 300 python scripts/fill_write_probe.py --store-policy ;;
     pmc_rs) step pmc_rs 120 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d gpurun_out/pmc_rs -o run --output-format csv -- python3 scripts/pmc_probe.py --rs ;;
     os_c5x) step os_c5x 600 python scripts/oversub.py --what c5,c2 --variants 18,20,21 --ms 16,32,64,128 ;;
+    pmc_vv) step pmc_vv 120 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d gpurun_out/pmc_vv -o run --output-format csv -- python3 scripts/pmc_probe.py --vv ;;
+    xcd23) step xcd_c2 300 python scripts/xcd_probe.py --what c2 && step xcd_c3 300 python scripts/xcd_probe.py --what c3 ;;
     iso) step iso 300 python scripts/xcd_probe.py --what iso ;;
     os_c3x) step os_c3x 600 python scripts/oversub.py --what c3 --variants 3,11 --ms 8,16,32,64 ;;
     xccmap) step xccmap 300 python scripts/xcc_map.py ;;

@@ -41,6 +41,19 @@ def main():
             run(lambda: ctx.batch_fixed_ex(K.OP_CHECKSUM, a, L, L, n, out, K.KERNEL_RSTREAM, v | (32 << 16)))
         print("ok", flush=True)
         return
+    if "--vv" in sys.argv:  # C3 vvstream policy without / with the L2-kept first step
+        from synth_np import mixed_layout
+        off, ln, total = mixed_layout(4 << 20, seed=42)
+        n = ln.size
+        a = torch.empty(total, dtype=torch.uint8, device="cuda")
+        d_off, d_ln = torch.from_numpy(off).cuda(), torch.from_numpy(ln).cuda()
+        K.synth_var(a, d_off, d_ln, 1492, n, seed=42)
+        out = torch.empty(n, dtype=torch.int16, device="cuda")
+        for v in (12, 28):
+            run(lambda: ctx.batch_var_ex(K.OP_CHECKSUM, a, d_off, d_ln, n, out, K.KERNEL_VVSTREAM, v, packed=True,
+                                         total_bytes=total))
+        print("ok", flush=True)
+        return
     a = torch.empty(n * L, dtype=torch.uint8, device="cuda")
     K.synth_fixed(a, L, L, n, seed=42)
     out = torch.empty(n, dtype=torch.int16, device="cuda")

@@ -89,7 +89,8 @@ def main():
         runs = [(f"rstream v{v} x{m}", K.KERNEL_RSTREAM, v | (m << 16))
                 for v, m in ((10, 32), (14, 32), (18, 32), (20, 32), (21, 32), (19, 32), (18, 8))]
         runs += [("vvstream fixed x32", K.KERNEL_VVSTREAM, 3 | (32 << 16)),
-                 ("vvstream fixed x32 xcd16", K.KERNEL_VVSTREAM, 11 | (32 << 16))]
+                 ("vvstream fixed x32 xcd16", K.KERNEL_VVSTREAM, 11 | (32 << 16)),
+                 ("vvstream fixed x32 xcd16 first-step", K.KERNEL_VVSTREAM, 27 | (32 << 16))]
         fixed_case(ctx, s, what, n, 1492, runs, 20 if what == "c2" else 4)
     elif what == "c4":
         runs = [(f"seg G64U4 x{m}{' xcd16' if x else ''}", K.KERNEL_SEG, 3 | (m << 16) | (x << 24))
@@ -107,7 +108,7 @@ def main():
         ref = torch.empty(n, dtype=torch.int16, device="cuda")
         ctx.batch_var_ex(K.OP_CHECKSUM, a, d_off, d_ln, n, ref, K.KERNEL_SEG, 0)
         out = torch.empty(n, dtype=torch.int16, device="cuda")
-        for p in (12, 4, 3 | (32 << 16), 11 | (32 << 16), 2 | (32 << 16), 10 | (32 << 16), 12):
+        for p in (12, 28, 11 | (32 << 16), 27 | (32 << 16), 10 | (32 << 16), 26 | (32 << 16), 12, 28):
             ctx.batch_var_ex(K.OP_CHECKSUM, a, d_off, d_ln, n, out, K.KERNEL_VVSTREAM, p, packed=True,
                              total_bytes=total)
             torch.cuda.synchronize()

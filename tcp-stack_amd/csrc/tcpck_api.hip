@@ -167,11 +167,12 @@ constexpr uint64_t kRunMaxLen = 16384;  // above: seg (one wave per jumbo image 
 // 84.1%, C4 85.5 -> 87.4%, profiles/r01/xcd_*.log; the HBM bytes do not
 // change, PMC).  rstream also reads each run's first step with the default
 // cache policy: that line is the previous run's last line, and the
-// neighbour's last step then finds it in L2 (PMC bytes x1.015 -> x1.000);
-// with up to 128 x the resident grid for large batches (C5 84.7 -> 88.3%,
-// profiles/r01/oversub_c5_first_step.log).
+// neighbour's last step then finds it in L2 (PMC bytes x1.015 -> x1.000;
+// C2 90.9 -> 93.1%), with up to 128 x the resident grid for large batches
+// (C5 84.7 -> 88.3%, profiles/r01/oversub_c5_first_step.log); vvstream the
+// same (C3 86.3 -> 89.5%, profiles/r01/xcd_first_step_probe.log).
 constexpr int kRstreamPolicy = 20;       // v_dot2 sums, buffer loads, XCD-chunked order, L2-kept first step
-constexpr int kVvPolicy = 4 | 8;         // size policy, XCD-chunked order
+constexpr int kVvPolicy = 4 | 8 | 16;    // size policy, XCD-chunked order, L2-kept first step
 constexpr int kSegXcdOrder = 1 << 24;    // seg: XCD-chunked order
 
 hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t stride, uint32_t len,

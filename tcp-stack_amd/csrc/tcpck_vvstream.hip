@@ -64,6 +64,7 @@ struct VVArgs {
   uint32_t stride;          // fixed layouts: image k at k * stride
   uint32_t len;             // fixed layouts: image length (<= stride)
   uint32_t order;           // block order (dev::ordered_block)
+  uint32_t keep_first;      // 1: the run's first step read with the default cache policy (L2-kept edge line)
 };
 
 // Word wi (0..7) of a 16-byte chunk set to zero.
@@ -163,7 +164,16 @@ __global__ void __launch_bounds__(kBlock) vvstream_kernel(VVArgs a) {
     uint32_t e_last = lead;  // end of image jn - 1 (= start of image jn), run-relative
     u32x4 ring[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) ring[u] = load_step(static_cast<uint32_t>(u));
+    for (int u = 0; u < U; ++u) {
+      if (u == 0 && a.keep_first) {
+        // the first line is the previous run's last: kept in L2 for its last step
+        typedef unsigned v4u __attribute__((ext_vector_type(4)));
+        const v4u v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, static_cast<int>(lane << 4), 0, 0);
+        ring[0] = u32x4{v.x, v.y, v.z, v.w};
+      } else {
+        ring[u] = load_step(static_cast<uint32_t>(u));
+      }
+    }
 
     // descriptor rounds (variable layouts): lengths of run images [256 r, 256 r + 256), 4 per lane
     const uint32_t *lens = FIXED ? nullptr : a.lengths + kb;
@@ -386,7 +396,7 @@ __global__ void __launch_bounds__(kBlock) vvstream_kernel(VVArgs a) {
 }
 
 template <int U, int OP, int SPLIT, int LAYOUT>
-hipError_t launch_one(const RunArgs &s, uint32_t oversub, bool xcd, uint32_t num_cus, hipStream_t stream) {
+hipError_t launch_one(const RunArgs &s, uint32_t oversub, int flags, uint32_t num_cus, hipStream_t stream) {
   static const uint32_t per_cu = dev::resident_blocks_per_cu(vvstream_kernel<U, OP, SPLIT, LAYOUT>);
   const uint64_t resident = static_cast<uint64_t>(per_cu) * num_cus;
   uint64_t blocks = resident * (oversub ? oversub : 1);
@@ -404,18 +414,19 @@ hipError_t launch_one(const RunArgs &s, uint32_t oversub, bool xcd, uint32_t num
   a.rem = s.count % (blocks * kWavesPerBlock);
   a.stride = static_cast<uint32_t>(s.stride);
   a.len = s.len;
-  a.order = xcd ? 4u : dev::kOrderDefault;  // groups of 16 blocks per XCD
+  a.order = (flags & 8) ? 4u : dev::kOrderDefault;  // groups of 16 blocks per XCD
+  a.keep_first = (flags & 16) ? 1u : 0u;
   hipLaunchKernelGGL((vvstream_kernel<U, OP, SPLIT, LAYOUT>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0,
                      stream, a);
   return hipGetLastError();
 }
 
 template <int U, int SPLIT, int LAYOUT>
-hipError_t dispatch(int op, const RunArgs &a, uint32_t oversub, bool xcd, uint32_t num_cus, hipStream_t s) {
+hipError_t dispatch(int op, const RunArgs &a, uint32_t oversub, int flags, uint32_t num_cus, hipStream_t s) {
   switch (op) {
-    case kChecksum: return launch_one<U, kChecksum, SPLIT, LAYOUT>(a, oversub, xcd, num_cus, s);
-    case kVerify: return launch_one<U, kVerify, SPLIT, LAYOUT>(a, oversub, xcd, num_cus, s);
-    case kFill: return launch_one<U, kFill, SPLIT, LAYOUT>(a, oversub, xcd, num_cus, s);
+    case kChecksum: return launch_one<U, kChecksum, SPLIT, LAYOUT>(a, oversub, flags, num_cus, s);
+    case kVerify: return launch_one<U, kVerify, SPLIT, LAYOUT>(a, oversub, flags, num_cus, s);
+    case kFill: return launch_one<U, kFill, SPLIT, LAYOUT>(a, oversub, flags, num_cus, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -429,7 +440,7 @@ hipError_t launch_vvstream(int op, int variant, bool fixed, const RunArgs &a, ui
   const bool gap = fixed && a.stride != a.len;
   const uint64_t bytes = fixed ? a.count * a.stride : a.total_bytes;
   uint32_t m = a.oversub ? a.oversub : 1;
-  const bool xcd = (variant & 8) != 0;  // XCD-chunked run order
+  const int flags = variant & 24;  // 8: XCD-chunked run order; 16: L2-kept first step
   variant &= 7;
   int u8 = (variant & 1);
   int split = variant >= 2 ? 1 : 0;
@@ -445,10 +456,10 @@ hipError_t launch_vvstream(int op, int variant, bool fixed, const RunArgs &a, ui
   } else if (variant > 4 || variant < 0) {
     return hipErrorInvalidValue;
   }
-  if (gap) return u8 ? dispatch<8, 1, 2>(op, a, m, xcd, num_cus, stream) : dispatch<4, 1, 2>(op, a, m, xcd, num_cus, stream);
-  if (fixed) return u8 ? dispatch<8, 1, 1>(op, a, m, xcd, num_cus, stream) : dispatch<4, 1, 1>(op, a, m, xcd, num_cus, stream);
-  if (split) return u8 ? dispatch<8, 1, 0>(op, a, m, xcd, num_cus, stream) : dispatch<4, 1, 0>(op, a, m, xcd, num_cus, stream);
-  return u8 ? dispatch<8, 0, 0>(op, a, m, xcd, num_cus, stream) : dispatch<4, 0, 0>(op, a, m, xcd, num_cus, stream);
+  if (gap) return u8 ? dispatch<8, 1, 2>(op, a, m, flags, num_cus, stream) : dispatch<4, 1, 2>(op, a, m, flags, num_cus, stream);
+  if (fixed) return u8 ? dispatch<8, 1, 1>(op, a, m, flags, num_cus, stream) : dispatch<4, 1, 1>(op, a, m, flags, num_cus, stream);
+  if (split) return u8 ? dispatch<8, 1, 0>(op, a, m, flags, num_cus, stream) : dispatch<4, 1, 0>(op, a, m, flags, num_cus, stream);
+  return u8 ? dispatch<8, 0, 0>(op, a, m, flags, num_cus, stream) : dispatch<4, 0, 0>(op, a, m, flags, num_cus, stream);
 }
 
 }  // namespace tcpck
