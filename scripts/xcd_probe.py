@@ -96,7 +96,7 @@ def main():
         runs = [(f"seg G64U4 x{m}{' xcd16' if x else ''}", K.KERNEL_SEG, 3 | (m << 16) | (x << 24))
                 for m in (1, 8) for x in (0, 1)]
         runs += [(f"rstream v{v} x{m}", K.KERNEL_RSTREAM, v | (m << 16))
-                 for v, m in ((10, 8), (14, 8), (18, 8), (18, 32))]
+                 for v, m in ((10, 8), (14, 8), (18, 8), (18, 32), (20, 8), (20, 32), (20, 0))]
         fixed_case(ctx, s, "c4", 256 << 10, 65536, runs, 4)
     elif what == "c3":
         from synth_np import mixed_layout

@@ -152,15 +152,17 @@ void free_stage(tcpck_ctx *ctx) {
 
 // ---- kernel selection (AUTO; measurements in DESIGN.md section 4) ------------
 // reference mode:
-//   fixed, stride == len   < 512 B vvstream (prefix table), 512 B..16 KiB
+//   fixed, stride == len   < 512 B vvstream (prefix table), 512 B..64 KiB
 //                          rstream (scalar boundary walk), larger seg
 //   fixed, stride > len    small gaps vvstream (gaps streamed as virtual
 //                          images), larger gaps seg with 8 lanes per image
 //   packed variable        CHECKSUM / VERIFY vvstream, FILL span
 // everything else -- unordered offsets, gaps in variable layouts, RFC 1071
-// mode, jumbo images (where one wave per image already streams whole 1 KiB
-// steps) -- seg.
-constexpr uint64_t kRunMaxLen = 16384;  // above: seg (one wave per jumbo image already streams whole steps)
+// mode, variable or gapped layouts of images above 16 KiB (where one wave per
+// image already streams whole 1 KiB steps) -- seg.
+constexpr uint64_t kRunMaxLen = 16384;       // variable / gapped layouts: above, seg
+constexpr uint64_t kFixedRunMaxLen = 65536;  // packed fixed: rstream up to here (C4 88.5% vs seg 87.5%,
+                                             // profiles/r01/xcd_c4_first_step.log), above seg
 // Policy parameters.  Every kernel takes its runs in the XCD-chunked block
 // order (dev::ordered_block, groups of 16 blocks per XCD): each XCD streams
 // compact regions instead of every eighth run (C2 86.3% -> 90.6%, C3 82.7 ->
@@ -179,7 +181,8 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
                      uint64_t count, void *out, int kernel, int param, hipStream_t s) {
   const uint32_t num_cus = static_cast<uint32_t>(ctx->num_cus);
   if (kernel == TCPCK_KERNEL_AUTO) {
-    if (mode != TCPCK_MODE_REF || len < 2 || len > kRunMaxLen || stride > (1u << 24)) {
+    if (mode != TCPCK_MODE_REF || len < 2 || len > kFixedRunMaxLen || stride > (1u << 24) ||
+        (stride > len && len > kRunMaxLen)) {
       kernel = TCPCK_KERNEL_SEG;
       param = kSegXcdOrder;  // shape by length
     } else if (stride > len) {
