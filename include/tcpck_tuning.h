@@ -34,7 +34,8 @@ extern "C" {
                                   with each XCD taking groups of 2/4/16/64
                                   consecutive runs; 20/21: 18/14 with the run's
                                   first step read with the default cache policy,
-                                  20 = the policy's)
+                                  20 = the policy's; 22: 18 with every step read
+                                  with the default policy)
                                   | (blocks per CU cap << 8)
                                   | (grid oversubscription << 16: 0 = by batch
                                   size, 1 = none, M = M x the resident grid)    */

@@ -68,8 +68,10 @@ def main():
 
         def chk():
             assert torch.equal(out, ref)
-        for label, kern, p in (("rstream", K.KERNEL_RSTREAM, 10), ("vvstream fixed", K.KERNEL_VVSTREAM, 4),
-                               ("auto", None, 0)):
+        runs = [("rstream", K.KERNEL_RSTREAM, 10), ("vvstream fixed", K.KERNEL_VVSTREAM, 4), ("auto", None, 0)]
+        if L == 1492:  # rstream policy (20) vs every step read with the default cache policy (22)
+            runs += [("rstream v20", K.KERNEL_RSTREAM, 20), ("rstream v22", K.KERNEL_RSTREAM, 22)]
+        for label, kern, p in runs:
             for op in (K.OP_FILL, K.OP_CHECKSUM):
                 if kern is None:
                     fn = (lambda op=op: ctx.batch_fixed(op, a, L, L, n, out, stream=s))

@@ -44,6 +44,7 @@ using dev::u32x4;
 // FLAV bit 0: chunk sums with v_dot2_u32_u16; bit 1: buffer (SRSRC) loads with
 // the step offset in an SGPR instead of per-lane 64-bit clamped addresses;
 // bit 2 (with bit 1): the run's first step read with the default cache policy;
+// bit 3 (with bit 1): every step read with the default cache policy;
 // a.order (runtime): the block order, dev::ordered_block -- the XCD orders let
 // neighbouring runs share an XCD, so the results of neighbouring blocks that
 // share a 128-B line of out[] leave one L2 as whole lines instead of partial
@@ -91,7 +92,13 @@ __global__ void __launch_bounds__(kBlock) rstream_kernel(FixedStreamArgs a) {
   const auto rsrc = dev::make_rsrc(base, (last_chunk + 1) << 4);
   auto load_step = [&](uint32_t st) -> u32x4 {
     if constexpr (FLAV & 2) {
-      return dev::load16_buf_nt(rsrc, lane << 4, st << 10);
+      if constexpr (FLAV & 8) {  // default cache policy for every step (FILL: the field's line stays in L2)
+        typedef unsigned v4u __attribute__((ext_vector_type(4)));
+        const v4u v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, static_cast<int>(lane << 4), static_cast<int>(st << 10), 0);
+        return u32x4{v.x, v.y, v.z, v.w};
+      } else {
+        return dev::load16_buf_nt(rsrc, lane << 4, st << 10);
+      }
     } else {
       const uint32_t ci = min((st << 6) + lane, last_chunk);  // clamp: always a legal address
       return dev::load16_nt(base + 16 * static_cast<uint64_t>(ci));
@@ -260,6 +267,11 @@ hipError_t launch_rstream(int op, int variant, const FixedStreamArgs &a, uint32_
       FixedStreamArgs b = a;
       b.order = variant == 20 ? 4u : dev::kOrderXcd;
       return dispatch<4, false, 0, 7>(op, b, num_cus, stream);
+    }
+    case 22: {  // 18 with every step read with the default policy (FLAV bit 3)
+      FixedStreamArgs b = a;
+      b.order = 4u;
+      return dispatch<4, false, 0, 11>(op, b, num_cus, stream);
     }
     case 14: case 15: case 16: case 17: case 18: case 19: {
       // 10 (14, 16-19) or 13 (15) with an XCD order: whole regions (14, 15) or
