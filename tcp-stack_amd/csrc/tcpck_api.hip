@@ -156,7 +156,7 @@ void free_stage(tcpck_ctx *ctx) {
 //                          rstream (scalar boundary walk), larger seg
 //   fixed, stride > len    small gaps vvstream (gaps streamed as virtual
 //                          images), larger gaps seg with 8 lanes per image
-//   packed variable        CHECKSUM / VERIFY vvstream, FILL span
+//   packed variable        vvstream, every op
 // everything else -- unordered offsets, gaps in variable layouts, RFC 1071
 // mode, variable or gapped layouts of images above 16 KiB (where one wave per
 // image already streams whole 1 KiB steps) -- seg.
@@ -203,9 +203,9 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
     } else if (len < 512) {
       // packed, by image length (scripts/policy_sweep.py, profiles/r01/policy_small.log):
       // below 512 B boundaries are dense enough that resolving all of a step's
-      // ends in parallel from the prefix table wins (vvstream FIXED, 73-81% at
-      // 32-256 B); from 512 B the scalar boundary walk (rstream: ~87% of the
-      // HBM roof on C2 at 32x oversubscription)
+      // ends in parallel from the prefix table wins (vvstream FIXED, 80-81% at
+      // 96-256 B, profiles/r01/fill_probe.log); from 512 B the scalar boundary
+      // walk (rstream: 92-93% of the HBM roof on C2)
       kernel = (op == TCPCK_OP_FILL && len < 30) ? TCPCK_KERNEL_SEG : TCPCK_KERNEL_VVSTREAM;
       param = kernel == TCPCK_KERNEL_SEG ? kSegXcdOrder : kVvPolicy;
     } else {
@@ -256,8 +256,8 @@ hipError_t run_var(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const uint6
                    hipStream_t s) {
   const uint64_t typical = (layout && layout->total_bytes) ? layout->total_bytes / count : 1500;
   const bool packed = mode == TCPCK_MODE_REF && layout && (layout->flags & TCPCK_LAYOUT_PACKED);
-  // packed, reference mode: vvstream for every op (any image lengths; C3 85.9%
-  // at 32x oversubscription, profiles/r01/c3_bench_vv_u8x32_settle.log); a
+  // packed, reference mode: vvstream for every op (any image lengths; C3 89.1%
+  // at 32x oversubscription, profiles/r01/c3_bench_r01_final.log); a
   // wrong packed hint costs speed, never correctness (waves re-check)
   if (kernel == TCPCK_KERNEL_AUTO) {
     if (!packed || typical > kRunMaxLen || (op == TCPCK_OP_FILL && layout->min_len != 0 && layout->min_len < 30)) {
