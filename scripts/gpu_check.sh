@@ -61,6 +61,9 @@ for s in ${STEPS:-tests smoke bench prof}; do
     os_c5x) step os_c5x 600 python scripts/oversub.py --what c5,c2 --variants 18,20,21 --ms 16,32,64,128 ;;
     pmc_vv) step pmc_vv 120 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d gpurun_out/pmc_vv -o run --output-format csv -- python3 scripts/pmc_probe.py --vv ;;
     xcd23) step xcd_c2 300 python scripts/xcd_probe.py --what c2 && step xcd_c3 300 python scripts/xcd_probe.py --what c3 ;;
+    reuse) step reuse 300 python scripts/reuse_probe.py ;;
+    split) step split 300 python scripts/split_probe.py ;;
+    c3big) step c3big 300 python scripts/xcd_probe.py --what c3big ;;
     iso) step iso 300 python scripts/xcd_probe.py --what iso ;;
     os_c3x) step os_c3x 600 python scripts/oversub.py --what c3 --variants 3,11 --ms 8,16,32,64 ;;
     xccmap) step xccmap 300 python scripts/xcc_map.py ;;

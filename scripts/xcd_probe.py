@@ -98,9 +98,9 @@ def main():
         runs += [(f"rstream v{v} x{m}", K.KERNEL_RSTREAM, v | (m << 16))
                  for v, m in ((10, 8), (14, 8), (18, 8), (18, 32), (20, 8), (20, 32), (20, 0))]
         fixed_case(ctx, s, "c4", 256 << 10, 65536, runs, 4)
-    elif what == "c3":
+    elif what in ("c3", "c3big"):
         from synth_np import mixed_layout
-        off, ln, total = mixed_layout(4 << 20, seed=42)
+        off, ln, total = mixed_layout((4 if what == "c3" else 16) << 20, seed=42)
         n = ln.size
         a = torch.empty(total, dtype=torch.uint8, device="cuda")
         d_off, d_ln = torch.from_numpy(off).cuda(), torch.from_numpy(ln).cuda()
@@ -108,14 +108,17 @@ def main():
         ref = torch.empty(n, dtype=torch.int16, device="cuda")
         ctx.batch_var_ex(K.OP_CHECKSUM, a, d_off, d_ln, n, ref, K.KERNEL_SEG, 0)
         out = torch.empty(n, dtype=torch.int16, device="cuda")
-        for p in (12, 28, 11 | (32 << 16), 27 | (32 << 16), 10 | (32 << 16), 26 | (32 << 16), 12, 28):
+        params = (12, 28, 11 | (32 << 16), 27 | (32 << 16), 10 | (32 << 16), 26 | (32 << 16), 12, 28)
+        if what == "c3big":  # 16M images, ~12 GB: the policy's M (128) vs 32 and 64
+            params = (28, 27 | (32 << 16), 27 | (64 << 16), 27 | (128 << 16), 28)
+        for p in params:
             ctx.batch_var_ex(K.OP_CHECKSUM, a, d_off, d_ln, n, out, K.KERNEL_VVSTREAM, p, packed=True,
                              total_bytes=total)
             torch.cuda.synchronize()
             assert torch.equal(out, ref), p
             ms = b2b(lambda: ctx.batch_var_ex(K.OP_CHECKSUM, a, d_off, d_ln, n, out, K.KERNEL_VVSTREAM, p,
                                               packed=True, total_bytes=total, stream=s), s)
-            print(f"c3 vvstream variant {p & 0xFF} x{p >> 16}: {ms:.4f} ms ({(total + 2 * n) / ms / 1e6 / 80:.1f}%)",
+            print(f"{what} vvstream variant {p & 0xFF} x{p >> 16}: {ms:.4f} ms ({(total + 2 * n) / ms / 1e6 / 80:.1f}%)",
                   flush=True)
     elif what == "iso":
         # what separates C3 from the fixed layouts on vvstream: the descriptors

@@ -170,9 +170,10 @@ constexpr uint64_t kFixedRunMaxLen = 65536;  // packed fixed: rstream up to here
 // change, PMC).  rstream also reads each run's first step with the default
 // cache policy: that line is the previous run's last line, and the
 // neighbour's last step then finds it in L2 (PMC bytes x1.015 -> x1.000;
-// C2 90.9 -> 93.1%), with up to 128 x the resident grid for large batches
-// (C5 84.7 -> 88.3%, profiles/r01/oversub_c5_first_step.log); vvstream the
-// same (C3 86.3 -> 89.5%, profiles/r01/xcd_first_step_probe.log).
+// C2 90.9 -> 93.1%), and large batches keep runs of 4-8 KiB with up to
+// 1024 x the resident grid (C5: 256x, 84.7% at 32x -> 92.5%,
+// profiles/r01/oversub_c5_first_step.log, split_probe.log); vvstream the
+// same with runs >= 8 KiB (C3 86.3 -> 89.5%, profiles/r01/xcd_first_step_probe.log).
 constexpr int kRstreamPolicy = 20;       // v_dot2 sums, buffer loads, XCD-chunked order, L2-kept first step
 constexpr int kVvPolicy = 4 | 8 | 16;    // size policy, XCD-chunked order, L2-kept first step
 constexpr int kSegXcdOrder = 1 << 24;    // seg: XCD-chunked order

@@ -218,8 +218,8 @@ hipError_t launch_one(const FixedStreamArgs &a, uint32_t num_cus, hipStream_t st
   static const uint32_t per_cu = dev::resident_blocks_per_cu(rstream_kernel<U, OP, STAMP, PRIO, FLAV>);
   const uint32_t cap = (a.blocks_per_cu && a.blocks_per_cu < per_cu) ? a.blocks_per_cu : per_cu;
   const uint64_t resident = static_cast<uint64_t>(cap) * num_cus;
-  // runs of >= 4 KiB, up to 128 x the resident grid (C2: 32, C5: 128)
-  uint64_t blocks = resident * dev::oversub_for(a.oversub, a.count * a.stride, resident * kWavesPerBlock, 128);
+  // runs of >= 4 KiB (4-8 KiB: C2 1M x 1492 B at 32x, C5 8M at 256x), up to 1024 x the resident grid
+  uint64_t blocks = resident * dev::oversub_for(a.oversub, a.count * a.stride, resident * kWavesPerBlock, 1024);
   const uint64_t need = (a.count + kWavesPerBlock - 1) / kWavesPerBlock;  // >= 1 image per wave
   if (blocks > need) blocks = need;
   if (blocks == 0) return hipSuccess;

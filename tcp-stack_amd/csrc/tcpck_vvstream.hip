@@ -446,11 +446,12 @@ hipError_t launch_vvstream(int op, int variant, bool fixed, const RunArgs &a, ui
   int split = variant >= 2 ? 1 : 0;
   if (variant == 4) {
     // library policy: oversubscribe by size, runs of >= 8 KiB, M a power of two
-    // <= 32 (M = 16/24/40 measured 2-4% below 32 on the run kernels,
-    // profiles/r01/oversub_c2c3.log).  At M = 32, U8 (C3 85.0-86.3% vs U4
-    // 82.7-84.2%); once M >= 4 the dispatcher balances the runs and
-    // equal-count runs (no offset searches) win.
-    m = dev::oversub_for(a.oversub, bytes, static_cast<uint64_t>(num_cus) * 32, 32, 8u << 10);
+    // (M = 16/24/40 measured 2-4% below 32 on the run kernels,
+    // profiles/r01/oversub_c2c3.log; C3: 32).  From M = 32, U8 (C3 85.0-86.3%
+    // vs U4 82.7-84.2%); once M >= 4 the dispatcher balances the runs and
+    // equal-count runs (no offset searches) win.  Larger batches keep the
+    // runs short with larger M, as rstream does (C5: profiles/r01/split_probe.log).
+    m = dev::oversub_for(a.oversub, bytes, static_cast<uint64_t>(num_cus) * 32, 1024, 8u << 10);
     u8 = m >= 32;
     split = m >= 4;
   } else if (variant > 4 || variant < 0) {
