@@ -64,6 +64,9 @@ for s in ${STEPS:-tests smoke bench prof}; do
     reuse) step reuse 300 python scripts/reuse_probe.py ;;
     split) step split 300 python scripts/split_probe.py ;;
     c3big) step c3big 300 python scripts/xcd_probe.py --what c3big ;;
+    segtests) step segtests 600 python -u -m pytest tests/test_gpu_kernels.py -x -q --timeout 300 --timeout-method thread ;;
+    c4x) step xcd_c4 300 python scripts/xcd_probe.py --what c4 ;;
+    jumbo) step jumbo 600 python scripts/xcd_probe.py --what jumbo ;;
     iso) step iso 300 python scripts/xcd_probe.py --what iso ;;
     os_c3x) step os_c3x 600 python scripts/oversub.py --what c3 --variants 3,11 --ms 8,16,32,64 ;;
     xccmap) step xccmap 300 python scripts/xcc_map.py ;;

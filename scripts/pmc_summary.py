@@ -21,7 +21,7 @@ import statistics
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = ("rstream_kernel", "vvstream_kernel", "seg_kernel")
+KERNELS = ("rstream_kernel", "vvstream_kernel", "seg_kernel", "jumbo_kernel")
 
 
 def per_launch(path: str, counter: str):

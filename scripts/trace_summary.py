@@ -10,7 +10,7 @@ import argparse
 import csv
 import statistics
 
-KERNELS = ("rstream_kernel", "vvstream_kernel", "vstream_kernel", "seg_kernel", "span_kernel")
+KERNELS = ("rstream_kernel", "vvstream_kernel", "seg_kernel", "jumbo_kernel")
 
 
 def main():

@@ -96,8 +96,20 @@ def main():
         runs = [(f"seg G64U4 x{m}{' xcd16' if x else ''}", K.KERNEL_SEG, 3 | (m << 16) | (x << 24))
                 for m in (1, 8) for x in (0, 1)]
         runs += [(f"rstream v{v} x{m}", K.KERNEL_RSTREAM, v | (m << 16))
-                 for v, m in ((10, 8), (14, 8), (18, 8), (18, 32), (20, 8), (20, 32), (20, 0))]
+                 for v, m in ((18, 32), (20, 0))]
+        runs += [(f"seg {n} x{m} xcd16", K.KERNEL_SEG, sh | (m << 16) | (1 << 24))
+                 for n, sh in (("W4/U4", 7), ("W16/U2", 9)) for m in (32, 64, 128, 255, 0)]
         fixed_case(ctx, s, "c4", 256 << 10, 65536, runs, 4)
+    elif what == "jumbo":
+        # jumbo lengths: rstream (whole images per wave) vs W waves per image
+        for L in (4096, 6144, 8192, 12288, 16384, 32768, 65536, 131072):
+            n = (4 << 30) // L
+            runs = [("AUTO", K.KERNEL_AUTO, 0)]
+            runs += [("rstream v20", K.KERNEL_RSTREAM, 20)] if L <= 65536 else []
+            runs += [(f"seg {nm} xcd16", K.KERNEL_SEG, sh | (1 << 24))
+                     for nm, sh in (("G64/U4", 3), ("W2/U4", 11), ("W4/U4", 7), ("W8/U4", 8), ("W16/U2", 9))]
+            fixed_case(ctx, s, f"jumbo L={L}", n, L, runs, 8)
+            torch.cuda.empty_cache()
     elif what in ("c3", "c3big"):
         from synth_np import mixed_layout
         off, ln, total = mixed_layout((4 if what == "c3" else 16) << 20, seed=42)

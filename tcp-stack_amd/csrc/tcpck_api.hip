@@ -152,8 +152,9 @@ void free_stage(tcpck_ctx *ctx) {
 
 // ---- kernel selection (AUTO; measurements in DESIGN.md section 4) ------------
 // reference mode:
-//   fixed, stride == len   < 512 B vvstream (prefix table), 512 B..64 KiB
-//                          rstream (scalar boundary walk), larger seg
+//   fixed, stride == len   < 512 B vvstream (prefix table), 512 B..4 KiB
+//                          rstream (scalar boundary walk), larger seg with
+//                          W waves per image (~4 KiB per wave)
 //   fixed, stride > len    small gaps vvstream (gaps streamed as virtual
 //                          images), larger gaps seg with 8 lanes per image
 //   packed variable        vvstream, every op
@@ -161,8 +162,9 @@ void free_stage(tcpck_ctx *ctx) {
 // mode, variable or gapped layouts of images above 16 KiB (where one wave per
 // image already streams whole 1 KiB steps) -- seg.
 constexpr uint64_t kRunMaxLen = 16384;       // variable / gapped layouts: above, seg
-constexpr uint64_t kFixedRunMaxLen = 65536;  // packed fixed: rstream up to here (C4 88.5% vs seg 87.5%,
-                                             // profiles/r01/xcd_c4_first_step.log), above seg
+constexpr uint64_t kFixedRunMaxLen = 4096;   // packed fixed: rstream up to here; above, seg with W waves
+                                             // per image (C4 64 KiB: W16 91% vs rstream 85-88%,
+                                             // 6 KiB: W2 90.6% vs 87.0%, profiles/r01/jumbo_probe.log)
 // Policy parameters.  Every kernel takes its runs in the XCD-chunked block
 // order (dev::ordered_block, groups of 16 blocks per XCD): each XCD streams
 // compact regions instead of every eighth run (C2 86.3% -> 90.6%, C3 82.7 ->

@@ -15,11 +15,16 @@ enum Mode : int { kRef = 0, kRfc1071 = 1 };
 enum SegShape : int {
   kShapeSmall = 0,   // G = 8,  U = 2  : images up to ~256 B
   kShapeMss = 1,     // G = 16, U = 6  : images up to ~4 KiB (Ethernet MSS)
-  kShapeJumbo = 2,   // G = 64, U = 4  : larger images (64 KiB jumbo)
+  kShapeJumbo = 2,   // G = 64, U = 4  : 4-6 KiB images
   kShapeWave2 = 3,   // G = 64, U = 2  : tuning
   kShapeG32 = 4,     // G = 32, U = 3  : tuning
   kShapeG4 = 5,      // G = 4,  U = 8  : tuning
-  kNumShapes = 6
+  kShapeW4 = 6,      // 4 waves per image, U = 4  : jumbo images
+  kShapeW8 = 7,      // 8 waves per image, U = 4  : jumbo images
+  kShapeW16 = 8,     // 16 waves per image, U = 2 : jumbo images
+  kShapeW16U4 = 9,   // 16 waves per image, U = 4 : tuning
+  kShapeW2 = 10,     // 2 waves per image, U = 4  : jumbo images
+  kNumShapes = 11
 };
 
 struct SegArgs {
