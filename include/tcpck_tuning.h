@@ -16,7 +16,9 @@ extern "C" {
 #define TCPCK_KERNEL_AUTO 0 /* library policy (what tcpck_batch_* use)              */
 #define TCPCK_KERNEL_SEG 1  /* G lanes per image, any layout; param = shape + 1
                                (1: G8/U2, 2: G16/U6, 3: G64/U4, 4: G64/U2,
-                                5: G32/U3, 6: G4/U8), 0 = by length
+                                5: G32/U3, 6: G4/U8; W waves per image:
+                                7: W4/U4, 8: W8/U4, 9: W16/U2, 10: W16/U4,
+                                11: W2/U4), 0 = by length
                                | (grid oversubscription << 16)
                                | (1 << 24: each XCD takes groups of 16 blocks)  */
 /* 2, 3, 4, 6, 7: span, stream, fstream, rvstream and vstream, measured in
