@@ -69,6 +69,7 @@ def fixed_case(ctx, s, label, n, L, runs, reps):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--what", default="c2")
+    ap.add_argument("--m-sweep", action="store_true")
     what = ap.parse_args().what
     ctx = tcpck.Context(0)
     s = torch.cuda.current_stream()
@@ -123,6 +124,8 @@ def main():
         params = (12, 28, 11 | (32 << 16), 27 | (32 << 16), 10 | (32 << 16), 26 | (32 << 16), 12, 28)
         if what == "c3big":  # 16M images, ~12 GB: the policy's M (128) vs 32 and 64
             params = (28, 27 | (32 << 16), 27 | (64 << 16), 27 | (128 << 16), 28)
+        if "--m-sweep" in sys.argv:  # grid multiple with the policy's flags, U8 and U4
+            params = tuple(v | (m << 16) for v in (27, 26) for m in (8, 16, 32, 48)) + (28,)
         for p in params:
             ctx.batch_var_ex(K.OP_CHECKSUM, a, d_off, d_ln, n, out, K.KERNEL_VVSTREAM, p, packed=True,
                              total_bytes=total)
