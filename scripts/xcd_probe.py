@@ -88,7 +88,7 @@ def main():
     elif what in ("c2", "c5"):
         n = (1 << 20) if what == "c2" else (8 << 20)
         runs = [(f"rstream v{v} x{m}", K.KERNEL_RSTREAM, v | (m << 16))
-                for v, m in ((10, 32), (14, 32), (18, 32), (20, 32), (21, 32), (19, 32), (18, 8))]
+                for v, m in ((18, 32), (20, 32), (23, 32), (24, 32), (20, 0), (23, 0), (24, 0))]
         runs += [("vvstream fixed x32", K.KERNEL_VVSTREAM, 3 | (32 << 16)),
                  ("vvstream fixed x32 xcd16", K.KERNEL_VVSTREAM, 11 | (32 << 16)),
                  ("vvstream fixed x32 xcd16 first-step", K.KERNEL_VVSTREAM, 27 | (32 << 16))]

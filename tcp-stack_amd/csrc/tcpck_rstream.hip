@@ -45,10 +45,10 @@ using dev::u32x4;
 // the step offset in an SGPR instead of per-lane 64-bit clamped addresses;
 // bit 2 (with bit 1): the run's first step read with the default cache policy;
 // bit 3 (with bit 1): every step read with the default cache policy;
-// a.order (runtime): the block order, dev::ordered_block -- the XCD orders let
-// neighbouring runs share an XCD, so the results of neighbouring blocks that
-// share a 128-B line of out[] leave one L2 as whole lines instead of partial
-// lines from up to four XCDs.
+// a.order (runtime): the block order, dev::ordered_block -- with the XCD
+// orders each XCD streams compact regions instead of every eighth run
+// (measured +4% at C2; the HBM bytes do not change), and
+// neighbouring runs share an XCD's L2 for the run-edge line (FLAV bit 2).
 template <int U, int OP, bool STAMP, int PRIO = 0, int FLAV = 0>
 __global__ void __launch_bounds__(kBlock) rstream_kernel(FixedStreamArgs a) {
   const uint32_t lane = threadIdx.x & 63;
@@ -272,6 +272,12 @@ hipError_t launch_rstream(int op, int variant, const FixedStreamArgs &a, uint32_
       FixedStreamArgs b = a;
       b.order = 4u;
       return dispatch<4, false, 0, 11>(op, b, num_cus, stream);
+    }
+    case 23: case 24: {  // 20 with 8 (23) or 2 (24) steps in flight
+      FixedStreamArgs b = a;
+      b.order = 4u;
+      return variant == 23 ? dispatch<8, false, 0, 7>(op, b, num_cus, stream)
+                           : dispatch<2, false, 0, 7>(op, b, num_cus, stream);
     }
     case 14: case 15: case 16: case 17: case 18: case 19: {
       // 10 (14, 16-19) or 13 (15) with an XCD order: whole regions (14, 15) or
