@@ -363,3 +363,53 @@ def test_set_ack_argument_errors(ctx):
     with pytest.raises(tcpck.TcpckError):
         ctx.batch_set_ack(a, 4, stride=64, mode=5)
     ctx.batch_set_ack(a, 0, stride=64)       # empty batch is a no-op
+
+
+# ---- AUTO policy boundaries: rstream / jumbo W-shapes / vvstream hand-overs ----------
+
+@pytest.mark.parametrize("length", [510, 512, 4094, 4096, 4098, 6144, 8192, 8194, 16384, 16386, 32768,
+                                    32770, 98304])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_auto_policy_boundaries_fixed(ctx, oracle_c, length, mode):
+    """Packed fixed batches at every length where the AUTO policy changes kernel or
+    waves per image: CHECKSUM, FILL (arena and results) and VERIFY against the oracle."""
+    import tcpck
+    from oracle import ref16 as R
+    rng = np.random.default_rng(length + 7 * mode)
+    count = max(8, min(4000, (48 << 20) // length))
+    arena_np = rng.integers(0, 256, count * length, dtype=np.uint8)
+    arena = dev(arena_np)
+    out = torch.empty(count, dtype=torch.int16, device="cuda")
+    ctx.batch_fixed(tcpck.OP_CHECKSUM, arena, length, length, count, out, mode=mode)
+    exp = oracle_c.batch(arena_np, stride=length, length=length, count=count, mode=mode, threads=8)
+    np.testing.assert_array_equal(host(out).view(np.uint16), exp)
+    ctx.batch_fixed(tcpck.OP_FILL, arena, length, length, count, out, mode=mode)
+    filled = host(arena)
+    exp_arena = arena_np.copy()
+    exp_fill = np.array([R.fill_np(exp_arena[k * length:(k + 1) * length], mode) for k in range(count)],
+                        np.uint16)
+    np.testing.assert_array_equal(host(out).view(np.uint16), exp_fill)
+    np.testing.assert_array_equal(filled, exp_arena)
+    ok = torch.empty(count, dtype=torch.uint8, device="cuda")
+    ctx.batch_fixed(tcpck.OP_VERIFY, arena, length, length, count, ok, mode=mode)
+    assert bool(host(ok).all())
+
+
+@pytest.mark.parametrize("typical", [6000, 12000, 24000, 60000])
+def test_auto_policy_jumbo_var(ctx, oracle_c, typical):
+    """Variable layouts whose typical length selects a W-waves-per-image shape, with
+    lengths spread around it (some far shorter, some zero), packed and with gaps."""
+    import tcpck
+    rng = np.random.default_rng(typical)
+    count = 1500
+    ln = (rng.integers(0, 2 * typical, count) // 2 * 2).astype(np.uint32)
+    ln[::97] = 0
+    for gaps in (False, True):
+        g = (rng.integers(0, 3, count) * 2) if gaps else np.zeros(count, np.int64)
+        off = (np.concatenate([[0], np.cumsum(ln[:-1].astype(np.int64) + g[:-1])])).astype(np.uint64)
+        total = int(off[-1] + ln[-1])
+        arena_np = rng.integers(0, 256, total + 16, dtype=np.uint8)
+        out = torch.empty(count, dtype=torch.int16, device="cuda")
+        ctx.batch_var(tcpck.OP_CHECKSUM, dev(arena_np), dev(off), dev(ln), count, out,
+                      total_bytes=int(ln.sum()), packed=not gaps)
+        np.testing.assert_array_equal(host(out).view(np.uint16), oracle_c.batch(arena_np, off, ln, threads=8))
