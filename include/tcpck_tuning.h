@@ -52,6 +52,7 @@ extern "C" {
                                    takes groups of 16 consecutive runs; + 16: the
                                    run's first step read with the default cache
                                    policy; 28 = the policy's)
+                                   | (blocks per CU cap << 8: LDS padding)
                                    | (grid oversubscription << 16: 0 = by batch
                                    size, 1 = none, M = M x the resident grid)   */
 

@@ -57,8 +57,8 @@ def main():
     a = torch.empty(n * L, dtype=torch.uint8, device="cuda")
     K.synth_fixed(a, L, L, n, seed=42)
     out = torch.empty(n, dtype=torch.int16, device="cuda")
-    run(lambda: ctx.batch_fixed_ex(K.OP_CHECKSUM, a, L, L, n, out, K.KERNEL_RSTREAM, 18 | (32 << 16)))
-    run(lambda: ctx.batch_fixed_ex(K.OP_CHECKSUM, a, L, L, n, out, K.KERNEL_VVSTREAM, 11 | (32 << 16)))
+    run(lambda: ctx.batch_fixed_ex(K.OP_CHECKSUM, a, L, L, n, out, K.KERNEL_RSTREAM, 20 | (32 << 16)))
+    run(lambda: ctx.batch_fixed_ex(K.OP_CHECKSUM, a, L, L, n, out, K.KERNEL_VVSTREAM, 27 | (32 << 16)))
     del a, out
     from synth_np import mixed_layout
     off, ln, total = mixed_layout(4 << 20, seed=42)
@@ -67,7 +67,7 @@ def main():
     d_off, d_ln = torch.from_numpy(off).cuda(), torch.from_numpy(ln).cuda()
     K.synth_var(a, d_off, d_ln, 1492, n, seed=42)
     out = torch.empty(n, dtype=torch.int16, device="cuda")
-    run(lambda: ctx.batch_var_ex(K.OP_CHECKSUM, a, d_off, d_ln, n, out, K.KERNEL_VVSTREAM, 12, packed=True,
+    run(lambda: ctx.batch_var_ex(K.OP_CHECKSUM, a, d_off, d_ln, n, out, K.KERNEL_VVSTREAM, 28, packed=True,
                                  total_bytes=total))
     print("ok", flush=True)
 

@@ -70,6 +70,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--what", default="c2")
     ap.add_argument("--m-sweep", action="store_true")
+    ap.add_argument("--cap-sweep", action="store_true")
     what = ap.parse_args().what
     ctx = tcpck.Context(0)
     s = torch.cuda.current_stream()
@@ -111,9 +112,11 @@ def main():
                      for nm, sh in (("G64/U4", 3), ("W2/U4", 11), ("W4/U4", 7), ("W8/U4", 8), ("W16/U2", 9))]
             fixed_case(ctx, s, f"jumbo L={L}", n, L, runs, 8)
             torch.cuda.empty_cache()
-    elif what in ("c3", "c3big"):
+    elif what in ("c3", "c3big", "c3u"):
         from synth_np import mixed_layout
-        off, ln, total = mixed_layout((4 if what == "c3" else 16) << 20, seed=42)
+        # c3u: the C3 mix with payloads of 66/578/1462 B (images 2 mod 4: the unaligned table path)
+        pay = (66, 578, 1462) if what == "c3u" else (64, 576, 1460)
+        off, ln, total = mixed_layout((16 if what == "c3big" else 4) << 20, seed=42, payloads=pay)
         n = ln.size
         a = torch.empty(total, dtype=torch.uint8, device="cuda")
         d_off, d_ln = torch.from_numpy(off).cuda(), torch.from_numpy(ln).cuda()
@@ -126,6 +129,12 @@ def main():
             params = (28, 27 | (32 << 16), 27 | (64 << 16), 27 | (128 << 16), 28)
         if "--m-sweep" in sys.argv:  # grid multiple with the policy's flags, U8 and U4
             params = tuple(v | (m << 16) for v in (27, 26) for m in (8, 16, 32, 48)) + (28,)
+        if what == "c3u":
+            params = (28, 27 | (32 << 16), 27 | (6 << 8) | (24 << 16), 26 | (8 << 8) | (24 << 16), 28)
+        if "--cap-sweep" in sys.argv:  # blocks per CU (LDS padding) x grid multiple, U8 + flags
+            params = tuple(27 | (c << 8) | (m << 16) for c, m in ((8, 16), (8, 20), (8, 24), (7, 24), (6, 24),
+                                                                  (6, 28), (5, 32)))
+            params += tuple(26 | (c << 8) | (m << 16) for c, m in ((8, 16), (8, 20), (8, 24), (8, 32))) + (28,)
         for p in params:
             ctx.batch_var_ex(K.OP_CHECKSUM, a, d_off, d_ln, n, out, K.KERNEL_VVSTREAM, p, packed=True,
                              total_bytes=total)
@@ -133,7 +142,7 @@ def main():
             assert torch.equal(out, ref), p
             ms = b2b(lambda: ctx.batch_var_ex(K.OP_CHECKSUM, a, d_off, d_ln, n, out, K.KERNEL_VVSTREAM, p,
                                               packed=True, total_bytes=total, stream=s), s)
-            print(f"{what} vvstream variant {p & 0xFF} x{p >> 16}: {ms:.4f} ms ({(total + 2 * n) / ms / 1e6 / 80:.1f}%)",
+            print(f"{what} vvstream variant {p & 0xFF} cap {(p >> 8) & 0xFF} x{p >> 16}: {ms:.4f} ms ({(total + 2 * n) / ms / 1e6 / 80:.1f}%)",
                   flush=True)
     elif what == "iso":
         # what separates C3 from the fixed layouts on vvstream: the descriptors

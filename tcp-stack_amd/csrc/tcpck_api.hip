@@ -239,6 +239,7 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
     a.count = count;
     a.out = out;
     a.oversub = static_cast<uint32_t>(param >> 16) & 0xFFu;
+    a.blocks_per_cu = static_cast<uint32_t>(param >> 8) & 0xFFu;
     return tcpck::launch_vvstream(op, param & 0xFF, true, a, num_cus, s);
   }
   if (kernel != TCPCK_KERNEL_SEG) return hipErrorInvalidValue;
@@ -282,6 +283,7 @@ hipError_t run_var(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const uint6
     a.out = out;
     a.oversub = static_cast<uint32_t>(param >> 16) & 0xFFu;
     a.total_bytes = layout ? layout->total_bytes : 0;
+    a.blocks_per_cu = static_cast<uint32_t>(param >> 8) & 0xFFu;
     return tcpck::launch_vvstream(op, param & 0xFF, false, a, static_cast<uint32_t>(ctx->num_cus), s);
   }
   if (kernel != TCPCK_KERNEL_SEG) return hipErrorInvalidValue;

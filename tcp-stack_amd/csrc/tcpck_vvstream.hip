@@ -184,17 +184,21 @@ __global__ void __launch_bounds__(kBlock) vvstream_kernel(VVArgs a) {
         d[i] = j < nimg ? lens[j] : 0u;
       }
     };
-    uint32_t dnext[4] = {0, 0, 0, 0};
     uint32_t loaded = FIXED ? nv : 0;  // ends available (run-relative image count)
     uint32_t pos = lead;                 // end of the last written image
     bool short_fill = false;             // kFill: an image < 30 B (two fields per chunk possible)
     // every end so far 4-B aligned: the step's prefix table then holds u32 P
     // at dword positions (no packing), else packed u16 P at word positions
     bool al4 = (lead & 3u) == 0 && (!FIXED || ((S & 3u) == 0 && (!GAP || (L & 3u) == 0)));
-    auto fill_round = [&]() {            // write round (loaded / 256) from dnext, prefetch the next
-      uint32_t d[4] = {dnext[0], dnext[1], dnext[2], dnext[3]};
+    // Round r's lengths are loaded when the round is written, not prefetched a
+    // round ahead: a prefetch kept in registers across the step loop made the
+    // compiler copy them on every step, behind a vmcnt(0) that drained the
+    // data ring.  Runs of <= 256 images (C3 at 32x: ~16-25) write their one
+    // round before the loop.
+    auto fill_round = [&]() {            // load and write round (loaded / 256)
       const uint32_t r = loaded / kRound;
-      load_round(r + 1, dnext);
+      uint32_t d[4];
+      load_round(r, d);
       al4 = al4 && __ballot(((d[0] | d[1] | d[2] | d[3]) & 3u) != 0) == 0;  // lengths past nimg are 0
       const uint32_t e1 = d[0], e2 = e1 + d[1], e3 = e2 + d[2], e4 = e3 + d[3];
       const uint32_t incl = dev::wave_inclusive_scan(e4);
@@ -233,7 +237,6 @@ __global__ void __launch_bounds__(kBlock) vvstream_kernel(VVArgs a) {
       __builtin_amdgcn_wave_barrier();  // ends are read by other lanes
     };
     if constexpr (!FIXED) {
-      load_round(0, dnext);
       fill_round();
       if constexpr (OP == kFill) {
         // nothing may be written into the arena before the layout is known to
