@@ -56,6 +56,20 @@ extern "C" {
                                    | (grid oversubscription << 16: 0 = by batch
                                    size, 1 = none, M = M x the resident grid)   */
 
+#define TCPCK_KERNEL_GSTREAM 9 /* MODE_REF, all ops: fixed stride == len, len a
+                                  power of two in [32, 1024], 16-B aligned
+                                  arena; G = len / 16 lanes per image, DPP group
+                                  sums, no boundary resolution; param = variant
+                                  (0: 4 steps in flight, 1: 8, 2: 2; + 4: default
+                                  block order, else XCD-chunked; 0x80: 4 in
+                                  flight with default-policy loads, AUTO's FILL
+                                  choice up to 256 B; tuning: 0x10/0x20/0x40
+                                  results stored with the default/nt/sc1
+                                  policy, 0x100: 0x80 + 0x10, 0x200-0x202:
+                                  FILL field lines with default-policy loads,
+                                  U4/U8/U2)
+                                  | (grid oversubscription << 16: 0 = by batch
+                                  size, 1 = none, M = M x the resident grid)    */
 int tcpck_batch_fixed_ex(tcpck_ctx *ctx, int op, int mode, void *d_arena,
                          uint64_t stride, uint32_t len, uint64_t count, void *d_out,
                          int kernel, int param, tcpck_stream stream);

@@ -54,6 +54,12 @@ for s in ${STEPS:-tests smoke bench prof}; do
       timeout -s KILL 60 rocprofv3 -L > gpurun_out/counters.txt 2>&1 || true
       step sq1 120 rocprofv3 --kernel-trace --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS -d gpurun_out/sq1 -o run --output-format csv -- python3 scripts/pmc_probe.py &&
       step sq2 120 rocprofv3 --kernel-trace --pmc SQ_BUSY_CYCLES SQ_WAVES SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_WAIT_INST_LDS SQ_INST_CYCLES_VMEM_RD -d gpurun_out/sq2 -o run --output-format csv -- python3 scripts/pmc_probe.py ;;
+    gstests) step gstests 600 python -u -m pytest tests/test_gpu_kernels.py -x -q --timeout 120 --timeout-method thread -k gstream ;;
+    gssweep) step gssweep 600 python scripts/gstream_probe.py --ops checksum --lengths 32,64,128,256 --gs 0x80000,0x100000,0x200000,0x400000,0x80002,0x100002,0x200002,0x400002 ;;
+    gspol) step gspol 600 python scripts/gstream_probe.py --ops checksum,fill --lengths 32,128,512 --gs 0,2,0x10,0x20,0x40,0x80,0x100,0x22 ;;
+    gsfill) step gsfill 600 python scripts/gstream_probe.py --ops fill --lengths 32,64,128,256,512,1024 --gs 0,0x80,0x200,0x201,0x202 ;;
+    gsorder) step gsorder 600 python scripts/gstream_probe.py --ops fill --lengths 32,256,512,1024 --gs 0,0x80,0x100,0x200,0x201,0x202 ;;
+    gsprobe) step gsprobe 600 python scripts/gstream_probe.py ;;
     resend) step resend_tests 300 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread -k set_ack &&
       step resend 300 python scripts/resend_probe.py ;;
     fillpol) step fillpol 300 python scripts/fill_write_probe.py --store-policy ;;

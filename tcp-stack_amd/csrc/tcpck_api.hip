@@ -203,6 +203,15 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
         kernel = TCPCK_KERNEL_SEG;
         param = (tcpck::kShapeSmall + 1) | kSegXcdOrder;
       }
+    } else if (op == TCPCK_OP_FILL && tcpck::gstream_applies(arena, stride, len)) {
+      // send-path FILL of power-of-two images, 32 B (pure ACKs) .. 1 KiB:
+      // gstream; up to 256 B every line holds a checksum field, and reading
+      // the lines with the default cache policy keeps them in L2 until the
+      // field store lands, so they leave as whole lines rather than masked
+      // partial writes (scripts/gstream_probe.py, profiles/r01/gstream_fill.log:
+      // 32 B 21.4 -> 32 % of the roof, 256 B 33 -> 43 %, 512 B 46 -> 57 %)
+      kernel = TCPCK_KERNEL_GSTREAM;
+      param = len <= 256 ? tcpck::kGstreamDefaultLoads : 0;
     } else if (len < 512) {
       // packed, by image length (scripts/policy_sweep.py, profiles/r01/policy_small.log):
       // below 512 B boundaries are dense enough that resolving all of a step's
@@ -228,6 +237,16 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
     a.blocks_per_cu = static_cast<uint32_t>(param >> 8) & 0xFFu;
     a.oversub = static_cast<uint32_t>(param >> 16) & 0xFFu;
     return tcpck::launch_rstream(op, param & 0xFF, a, num_cus, s);
+  }
+  if (kernel == TCPCK_KERNEL_GSTREAM) {  // stride == len, a power of two in [32, 1024], 16-B aligned arena
+    if (mode != TCPCK_MODE_REF || !tcpck::gstream_applies(arena, stride, len)) return hipErrorInvalidValue;
+    tcpck::GroupStreamArgs a{};
+    a.arena = arena;
+    a.len = len;
+    a.count = count;
+    a.out = out;
+    a.oversub = static_cast<uint32_t>(param >> 16) & 0xFFu;
+    return tcpck::launch_gstream(op, param & 0xFFFF, a, num_cus, s);
   }
   if (kernel == TCPCK_KERNEL_VVSTREAM) {  // any even length: the prefix table takes any number of ends per step
     if (mode != TCPCK_MODE_REF || len == 0 || stride > (1u << 24) || (op == TCPCK_OP_FILL && len < 30))

@@ -74,6 +74,28 @@ struct FixedStreamArgs {
   uint32_t order;          // block order (dev::ordered_block; 0xFF default)
 };
 
+// Fixed stride == len == S, S a power of two in [32, 1024], 16-B aligned arena
+// (tcpck_gstream.hip): G = S / 16 lanes per image.
+struct GroupStreamArgs {
+  uint8_t *arena;
+  uint32_t len;      // == stride
+  uint64_t count;
+  void *out;
+  uint32_t oversub;  // grid = resident blocks x this (0 = by size)
+  uint32_t order;    // block order, set by launch_gstream
+  uint64_t per_wave; // step split, set by the launcher: steps = per_wave * waves + rem
+  uint64_t rem;
+};
+bool gstream_applies(const uint8_t *arena, uint64_t stride, uint32_t len);
+// variant: 0 = 4 steps in flight, 1 = 8, 2 = 2; + 4: default block order
+// (else XCD-chunked, groups of 16 blocks); kGstreamDefaultLoads: 4 in flight,
+// loads with the default cache policy instead of nt (AUTO for FILL <= 256 B);
+// tuning: 0x10 / 0x20 / 0x40 results through a buffer resource with the
+// default / nt / sc1 policy, 0x100 default-policy loads + 0x10, 0x200-0x202
+// FILL with default-policy loads for the field lines only (U4 / U8 / U2)
+constexpr int kGstreamDefaultLoads = 0x80;
+hipError_t launch_gstream(int op, int variant, const GroupStreamArgs &a, uint32_t num_cus, hipStream_t stream);
+
 // ---- rstream (fixed stride == len): one run per wave, scalar boundary walk.
 // variant: 0 = 4 loads in flight, 1 = 2, 2 = 8, 3 = 4 with per-wave time stamps,
 // 4-8 issue-priority experiments, 9-13 v_dot2 sums and/or buffer loads (10 = policy)

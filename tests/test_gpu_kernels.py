@@ -431,3 +431,87 @@ def test_oversubscribed_vvstream(ctx, oracle_c, variant, oversub):
     ctx.batch_var_ex(tcpck.OP_CHECKSUM, dev(arena_np), dev(off), dev(ln), count, out, tcpck.KERNEL_VVSTREAM,
                      variant | (oversub << 16), packed=True, total_bytes=total)
     np.testing.assert_array_equal(host(out).view(np.uint16), oracle_c.batch(arena_np, off, ln, threads=8))
+
+
+# ---- group stream (KERNEL_GSTREAM = 9: fixed stride == len, len a power of two in [32, 1024]) ----
+
+GSTREAM = [0, 1, 2, 4, 0x10, 0x20, 0x22, 0x40, 0x80, 0x100, 0x200, 0x201, 0x202]  # include/tcpck_tuning.h
+GS_LENGTHS = [32, 64, 128, 256, 512, 1024]
+
+
+@pytest.mark.parametrize("variant", GSTREAM)
+@pytest.mark.parametrize("length", GS_LENGTHS)
+@pytest.mark.parametrize("count", [1, 2, 31, 33, 64, 65, 3001, 70001])
+def test_gstream_fixed_vs_oracle(ctx, oracle_c, variant, length, count):
+    """Every length and ragged counts (partial last step, fewer images than one step),
+    the arena at 16-B (not 128-B) alignment too, and grid oversubscription."""
+    import tcpck
+    rng = np.random.default_rng(length * 11 + count + variant)
+    arena_np = rng.integers(0, 256, count * length + 128, dtype=np.uint8)
+    arena_np[:length] = 0xFF
+    arena_np[length:2 * length] = 0
+    buf = dev(arena_np)
+    for mis, oversub in ((0, 0), (16, 0), (112, 1), (0, 8)):
+        out = torch.full((count + 1,), -1, dtype=torch.int16, device="cuda")
+        ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, buf.data_ptr() + mis, length, length, count, out,
+                           tcpck.KERNEL_GSTREAM, variant | (oversub << 16))
+        exp = oracle_c.batch(arena_np[mis:], stride=length, length=length, count=count, threads=8)
+        got = host(out).view(np.uint16)
+        np.testing.assert_array_equal(got[:count], exp)
+        assert got[count] == 0xFFFF  # nothing written past the batch
+
+
+@pytest.mark.parametrize("variant", GSTREAM)
+@pytest.mark.parametrize("length", GS_LENGTHS)
+def test_gstream_fill_verify(ctx, variant, length):
+    import tcpck
+    from oracle import ref16 as R
+    rng = np.random.default_rng(length + 13 * variant)
+    count = 9001
+    arena_np = rng.integers(0, 256, count * length, dtype=np.uint8)
+    arena = dev(arena_np)
+    out = torch.empty(count, dtype=torch.int16, device="cuda")
+    ctx.batch_fixed_ex(tcpck.OP_FILL, arena, length, length, count, out, tcpck.KERNEL_GSTREAM, variant)
+    exp_arena = arena_np.copy()
+    exp = np.array([R.fill_np(exp_arena[k * length:(k + 1) * length]) for k in range(count)], np.uint16)
+    np.testing.assert_array_equal(host(out).view(np.uint16), exp)
+    got = host(arena)
+    np.testing.assert_array_equal(got, exp_arena)
+    # FILL without an output array writes the fields only
+    arena2 = dev(arena_np)
+    ctx.batch_fixed_ex(tcpck.OP_FILL, arena2, length, length, count, None, tcpck.KERNEL_GSTREAM, variant)
+    np.testing.assert_array_equal(host(arena2), exp_arena)
+    bad = rng.choice(count, 64, replace=False)
+    for k in bad:
+        got[k * length + int(rng.integers(0, length))] ^= 0x24
+    ok = torch.empty(count, dtype=torch.uint8, device="cuda")
+    ctx.batch_fixed_ex(tcpck.OP_VERIFY, dev(got), length, length, count, ok, tcpck.KERNEL_GSTREAM, variant)
+    np.testing.assert_array_equal(np.nonzero(host(ok) == 0)[0], np.sort(bad))
+
+
+def test_gstream_golden_header_only(ctx, golden):
+    """Header-only images (MakeTcpPacket(0), 32 B) from the golden fixtures, packed at stride 32."""
+    import tcpck
+    cases = [c for c in golden.by_kind("checksum") if c["len"] == 32]
+    assert cases
+    arena_np = np.concatenate([golden.image(c) for c in cases])
+    out = torch.empty(len(cases), dtype=torch.int16, device="cuda")
+    ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, dev(arena_np), 32, 32, len(cases), out, tcpck.KERNEL_GSTREAM, 0)
+    np.testing.assert_array_equal(host(out).view(np.uint16), np.array([c["expected"] for c in cases], np.uint16))
+
+
+def test_gstream_reject(ctx):
+    import tcpck
+    a = torch.zeros(1 << 20, dtype=torch.uint8, device="cuda")
+    o = torch.zeros(4096, dtype=torch.int16, device="cuda")
+    for stride, length in ((96, 96), (16, 16), (2048, 2048), (64, 32), (1492, 1492)):
+        with pytest.raises(tcpck.TcpckError):
+            ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, a, stride, length, 100, o, tcpck.KERNEL_GSTREAM, 0)
+    with pytest.raises(tcpck.TcpckError):  # arena not 16-B aligned
+        ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, a.data_ptr() + 2, 64, 64, 100, o, tcpck.KERNEL_GSTREAM, 0)
+    with pytest.raises(tcpck.TcpckError):  # RFC 1071 mode: seg only
+        ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, a, 64, 64, 100, o, tcpck.KERNEL_GSTREAM, 0, mode=1)
+    for v in (3, 8, 0x30, 0x400):  # no such variant
+        with pytest.raises(tcpck.TcpckError):
+            ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, a, 64, 64, 100, o, tcpck.KERNEL_GSTREAM, v)
+    ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, a, 64, 64, 0, o, tcpck.KERNEL_GSTREAM, 0)  # empty batch: no-op

@@ -365,10 +365,30 @@ def test_set_ack_argument_errors(ctx):
     ctx.batch_set_ack(a, 0, stride=64)       # empty batch is a no-op
 
 
-# ---- AUTO policy boundaries: rstream / jumbo W-shapes / vvstream hand-overs ----------
+# ---- AUTO policy boundaries: rstream / jumbo W-shapes / vvstream / gstream hand-overs ----------
 
-@pytest.mark.parametrize("length", [510, 512, 4094, 4096, 4098, 6144, 8192, 8194, 16384, 16386, 32768,
-                                    32770, 98304])
+
+@pytest.mark.parametrize("length", [32, 64, 256, 1024])
+@pytest.mark.parametrize("mis", [0, 2, 16])
+def test_auto_fill_small_pow2_alignment(ctx, length, mis):
+    """AUTO FILL of power-of-two images takes gstream only for a 16-B aligned arena;
+    any other pointer goes to the general kernels -- same arena bytes and results."""
+    import tcpck
+    from oracle import ref16 as R
+    rng = np.random.default_rng(length * 3 + mis)
+    count = 5000
+    arena_np = rng.integers(0, 256, count * length + 64, dtype=np.uint8)
+    buf = dev(arena_np)
+    out = torch.empty(count, dtype=torch.int16, device="cuda")
+    ctx.batch_fixed(tcpck.OP_FILL, buf.data_ptr() + mis, length, length, count, out)
+    exp_arena = arena_np.copy()
+    img = exp_arena[mis:]
+    exp = np.array([R.fill_np(img[k * length:(k + 1) * length]) for k in range(count)], np.uint16)
+    np.testing.assert_array_equal(host(out).view(np.uint16), exp)
+    np.testing.assert_array_equal(host(buf), exp_arena)
+
+@pytest.mark.parametrize("length", [30, 32, 34, 64, 96, 128, 256, 258, 510, 512, 1024, 1026, 4094, 4096,
+                                    4098, 6144, 8192, 8194, 16384, 16386, 32768, 32770, 98304])
 @pytest.mark.parametrize("mode", [0, 1])
 def test_auto_policy_boundaries_fixed(ctx, oracle_c, length, mode):
     """Packed fixed batches at every length where the AUTO policy changes kernel or
