@@ -51,7 +51,9 @@ extern "C" {
                                    always equal-count; 4: policy; + 8: each XCD
                                    takes groups of 16 consecutive runs; + 16: the
                                    run's first step read with the default cache
-                                   policy; 28 = the policy's)
+                                   policy; 28 = the policy's; + 32: FILL reads
+                                   every step with the default policy, AUTO's
+                                   choice for images up to 448 B)
                                    | (blocks per CU cap << 8: LDS padding)
                                    | (grid oversubscription << 16: 0 = by batch
                                    size, 1 = none, M = M x the resident grid)   */

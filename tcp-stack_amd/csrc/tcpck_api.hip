@@ -179,6 +179,14 @@ constexpr uint64_t kFixedRunMaxLen = 4096;   // packed fixed: rstream up to here
 constexpr int kRstreamPolicy = 20;       // v_dot2 sums, buffer loads, XCD-chunked order, L2-kept first step
 constexpr int kVvPolicy = 4 | 8 | 16;    // size policy, XCD-chunked order, L2-kept first step
 constexpr int kSegXcdOrder = 1 << 24;    // seg: XCD-chunked order
+// FILL of small images: nearly every line holds a checksum field, so the
+// run kernels read every step with the default cache policy; the line is then
+// still in L2 when the field store lands and leaves as a whole line instead of
+// a masked partial write (scripts/keep_probe.py, profiles/r01/keep_probe.log:
+// 96 B 20.4 -> 29.9 % of the roof, 192 B 28.6 -> 38.1 %, 320 B 38.0 -> 44.1 %,
+// 480 B +0.6 %, the C3 mix -3.7 %: bytes per image up to 448)
+constexpr uint64_t kFillKeepMaxLen = 448;
+constexpr int kVvKeep = 32;              // vvstream: kFill reads with the default policy
 
 hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t stride, uint32_t len,
                      uint64_t count, void *out, int kernel, int param, hipStream_t s) {
@@ -198,7 +206,7 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
       const bool hull = len < 512 ? stride <= 2 * l : (len < 1024 ? 4 * stride <= 5 * l : 16 * stride <= 17 * l);
       if (hull && (op != TCPCK_OP_FILL || len >= 30)) {
         kernel = TCPCK_KERNEL_VVSTREAM;
-        param = kVvPolicy;
+        param = kVvPolicy | (op == TCPCK_OP_FILL && stride <= kFillKeepMaxLen ? kVvKeep : 0);
       } else {
         kernel = TCPCK_KERNEL_SEG;
         param = (tcpck::kShapeSmall + 1) | kSegXcdOrder;
@@ -219,7 +227,8 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
       // 96-256 B, profiles/r01/fill_probe.log); from 512 B the scalar boundary
       // walk (rstream: 92-93% of the HBM roof on C2)
       kernel = (op == TCPCK_OP_FILL && len < 30) ? TCPCK_KERNEL_SEG : TCPCK_KERNEL_VVSTREAM;
-      param = kernel == TCPCK_KERNEL_SEG ? kSegXcdOrder : kVvPolicy;
+      param = kernel == TCPCK_KERNEL_SEG ? kSegXcdOrder
+                                         : kVvPolicy | (op == TCPCK_OP_FILL && len <= kFillKeepMaxLen ? kVvKeep : 0);
     } else {
       kernel = TCPCK_KERNEL_RSTREAM;
       param = kRstreamPolicy;
@@ -280,15 +289,17 @@ hipError_t run_var(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const uint6
   const uint64_t typical = (layout && layout->total_bytes) ? layout->total_bytes / count : 1500;
   const bool packed = mode == TCPCK_MODE_REF && layout && (layout->flags & TCPCK_LAYOUT_PACKED);
   // packed, reference mode: vvstream for every op (any image lengths; C3 89.1%
-  // at 32x oversubscription, profiles/r01/c3_bench_r01_final.log); a
-  // wrong packed hint costs speed, never correctness (waves re-check)
+  // at 32x oversubscription, profiles/r01/c3_bench_r01_final.log).  The
+  // packed flag must be true when set (tcpck.h); a wave whose lengths do not
+  // add up to its span falls back to per-image sums, but that check cannot see
+  // a gap that an overlap elsewhere in the run cancels
   if (kernel == TCPCK_KERNEL_AUTO) {
     if (!packed || typical > kRunMaxLen || (op == TCPCK_OP_FILL && layout->min_len != 0 && layout->min_len < 30)) {
       kernel = TCPCK_KERNEL_SEG;
       param = kSegXcdOrder;
     } else {
       kernel = TCPCK_KERNEL_VVSTREAM;
-      param = kVvPolicy;
+      param = kVvPolicy | (op == TCPCK_OP_FILL && typical <= kFillKeepMaxLen ? kVvKeep : 0);
     }
   }
   if (kernel == TCPCK_KERNEL_VVSTREAM) {

@@ -79,7 +79,7 @@ __device__ __forceinline__ u32x4 zero_word(u32x4 w, uint32_t wi) {
 }
 
 // LAYOUT: 0 packed variable, 1 fixed packed (stride == len), 2 fixed gapped
-template <int U, int OP, int SPLIT, int LAYOUT>
+template <int U, int OP, int SPLIT, int LAYOUT, bool KEEP = false>
 __global__ void __launch_bounds__(kBlock) vvstream_kernel(VVArgs a) {
   constexpr bool FIXED = LAYOUT != 0;
   constexpr bool GAP = LAYOUT == 2;
@@ -149,7 +149,19 @@ __global__ void __launch_bounds__(kBlock) vvstream_kernel(VVArgs a) {
     const uint32_t nsteps = (span + 1023) >> 10;
     const uint32_t last_chunk = span > 0 ? (span - 1) >> 4 : 0;
     const auto rsrc = dev::make_rsrc(arena + A0, (last_chunk + 1) << 4);
-    auto load_step = [&](uint32_t st) -> u32x4 { return dev::load16_buf_nt(rsrc, lane << 4, st << 10); };
+    // KEEP (kFill, small images): every line holds a checksum field, so read
+    // it with the default policy -- still in L2 when the field store lands, it
+    // leaves as a whole line instead of a masked partial write (gstream's
+    // measurement)
+    auto load_step = [&](uint32_t st) -> u32x4 {
+      if constexpr (KEEP) {
+        typedef unsigned v4u __attribute__((ext_vector_type(4)));
+        const v4u v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, static_cast<int>(lane << 4), static_cast<int>(st << 10), 0);
+        return u32x4{v.x, v.y, v.z, v.w};
+      } else {
+        return dev::load16_buf_nt(rsrc, lane << 4, st << 10);
+      }
+    };
     uint32_t *ring_end = s_end[wv];
     u32x4 *pre4 = reinterpret_cast<u32x4 *>(s_pre[wv]);
     const uint16_t *pre16 = reinterpret_cast<const uint16_t *>(s_pre[wv]);
@@ -398,9 +410,9 @@ __global__ void __launch_bounds__(kBlock) vvstream_kernel(VVArgs a) {
   }
 }
 
-template <int U, int OP, int SPLIT, int LAYOUT>
+template <int U, int OP, int SPLIT, int LAYOUT, bool KEEP = false>
 hipError_t launch_one(const RunArgs &s, uint32_t oversub, int flags, uint32_t num_cus, hipStream_t stream) {
-  static const uint32_t per_cu = dev::resident_blocks_per_cu(vvstream_kernel<U, OP, SPLIT, LAYOUT>);
+  static const uint32_t per_cu = dev::resident_blocks_per_cu(vvstream_kernel<U, OP, SPLIT, LAYOUT, KEEP>);
   const uint64_t resident = static_cast<uint64_t>(per_cu) * num_cus;
   uint64_t blocks = resident * (oversub ? oversub : 1);
   const uint64_t need = (s.count + kWavesPerBlock - 1) / kWavesPerBlock;
@@ -419,7 +431,7 @@ hipError_t launch_one(const RunArgs &s, uint32_t oversub, int flags, uint32_t nu
   a.len = s.len;
   a.order = (flags & 8) ? 4u : dev::kOrderDefault;  // groups of 16 blocks per XCD
   a.keep_first = (flags & 16) ? 1u : 0u;
-  hipLaunchKernelGGL((vvstream_kernel<U, OP, SPLIT, LAYOUT>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0,
+  hipLaunchKernelGGL((vvstream_kernel<U, OP, SPLIT, LAYOUT, KEEP>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0,
                      stream, a);
   return hipGetLastError();
 }
@@ -429,7 +441,9 @@ hipError_t dispatch(int op, const RunArgs &a, uint32_t oversub, int flags, uint3
   switch (op) {
     case kChecksum: return launch_one<U, kChecksum, SPLIT, LAYOUT>(a, oversub, flags, num_cus, s);
     case kVerify: return launch_one<U, kVerify, SPLIT, LAYOUT>(a, oversub, flags, num_cus, s);
-    case kFill: return launch_one<U, kFill, SPLIT, LAYOUT>(a, oversub, flags, num_cus, s);
+    case kFill:
+      return (flags & 32) ? launch_one<U, kFill, SPLIT, LAYOUT, true>(a, oversub, flags, num_cus, s)
+                          : launch_one<U, kFill, SPLIT, LAYOUT>(a, oversub, flags, num_cus, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -443,7 +457,9 @@ hipError_t launch_vvstream(int op, int variant, bool fixed, const RunArgs &a, ui
   const bool gap = fixed && a.stride != a.len;
   const uint64_t bytes = fixed ? a.count * a.stride : a.total_bytes;
   uint32_t m = a.oversub ? a.oversub : 1;
-  const int flags = variant & 24;  // 8: XCD-chunked run order; 16: L2-kept first step
+  // 8: XCD-chunked run order; 16: L2-kept first step; 32: kFill reads every
+  // step with the default cache policy (small images)
+  const int flags = variant & 56;
   variant &= 7;
   int u8 = (variant & 1);
   int split = variant >= 2 ? 1 : 0;

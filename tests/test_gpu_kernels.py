@@ -12,7 +12,7 @@ torch = pytest.importorskip("torch")
 
 SEG = [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11]  # 7-11: 4, 8, 16, 16, 2 waves per image
 RSTREAM = [0, 1, 2, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24]  # 9-13: v_dot2 sums and/or buffer loads; 14-21 XCD orders (20, 21: default-policy first step)
-VVSTREAM = [0, 1, 2, 3, 4, 28]  # 0/1 byte split U4/U8, 2/3 count split, 4 policy; +8 XCD order, +16 L2-kept first step
+VVSTREAM = [0, 1, 2, 3, 4, 28, 36, 60]  # 0/1 byte split U4/U8, 2/3 count split, 4 policy; +8 XCD order, +16 L2-kept first step, +32 FILL default-policy reads
 
 
 @pytest.fixture(scope="module")
