@@ -224,6 +224,37 @@ def test_c3_full_4m_mixed_vs_oracle(ctx, oracle_c):
     np.testing.assert_array_equal(host(out).view(np.uint16), exp)
 
 
+@pytest.mark.parametrize("L", [32, 256])
+def test_small_pow2_above_4gib_sampled(ctx, oracle_c, L):
+    """Pure-ACK-sized images in a 4.5 GiB arena (byte offsets past 2^32): gstream
+    CHECKSUM against the oracle on a sample (both sides of the 4 GiB line, the
+    batch end), then the AUTO send path (FILL, gstream) -> VERIFY over every image,
+    and CHECKSUM of the filled batch is 0 everywhere except the corrupted images."""
+    import tcpck
+    count = (9 << 29) // L
+    a = _synth_fixed_dev(count, L, L, seed=11)
+    out = torch.empty(count, dtype=torch.int16, device="cuda")
+    ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, a, L, L, count, out, tcpck.KERNEL_GSTREAM, 0)
+    got = host(out).view(np.uint16)
+    edge = (1 << 32) // L
+    idx = np.unique(np.concatenate([np.arange(0, count, 100003), np.arange(edge - 40, edge + 40),
+                                    np.arange(count - 70, count)]))
+    sample = host(a.view(count, L)[torch.from_numpy(idx).cuda()]).reshape(-1)
+    exp = oracle_c.batch(sample, stride=L, length=L, count=idx.size)
+    np.testing.assert_array_equal(got[idx], exp)
+    ctx.batch_fixed(tcpck.OP_FILL, a, L, L, count, None)
+    ok = torch.empty(count, dtype=torch.uint8, device="cuda")
+    ctx.batch_fixed(tcpck.OP_VERIFY, a, L, L, count, ok)
+    assert int(ok.sum(dtype=torch.int64).item()) == count
+    rng = np.random.default_rng(5)
+    bad = np.unique(np.concatenate([rng.integers(0, count, 500), [edge, count - 1]]))
+    pos = torch.from_numpy(bad.astype(np.int64) * L + rng.integers(0, L, bad.size)).cuda()
+    a[pos] ^= 0x11
+    ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, a, L, L, count, out, tcpck.KERNEL_GSTREAM, 2)
+    np.testing.assert_array_equal(np.nonzero(host(out) != 0)[0], bad)
+    del a
+
+
 def test_c4_jumbo_256k_x_64k_sampled(ctx, oracle_c):
     import tcpck
     count, L = 256 << 10, 65536
