@@ -61,6 +61,7 @@ for s in ${STEPS:-tests smoke bench prof}; do
     gsorder) step gsorder 600 python scripts/gstream_probe.py --ops fill --lengths 32,256,512,1024 --gs 0,0x80,0x100,0x200,0x201,0x202 ;;
     keep) step keep 600 python scripts/keep_probe.py ;;
     vvkeep) step vvkeep 900 python -u -m pytest tests/test_gpu_kernels.py -x -q --timeout 300 --timeout-method thread -k "vvstream" ;;
+    gsstage) step gsstage 600 python scripts/gstream_probe.py --ops checksum,fill --lengths 32,64,128,256,1024 --gs 0,2,0x800,0x802,0x80,0x880 ;;
     gsprobe) step gsprobe 600 python scripts/gstream_probe.py ;;
     resend) step resend_tests 300 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread -k set_ack &&
       step resend 300 python scripts/resend_probe.py ;;
