@@ -69,7 +69,10 @@ extern "C" {
                                   results stored with the default/nt/sc1
                                   policy, 0x100: 0x80 + 0x10, 0x200-0x202:
                                   FILL field lines with default-policy loads,
-                                  U4/U8/U2)
+                                  U4/U8/U2; FILL only: 0x400/0x800/0xC00 every
+                                  16-B chunk written back whole with the
+                                  nt/default/sc1 store policy, U4; 0x401: nt,
+                                  U8, AUTO's FILL choice up to 128 B)
                                   | (grid oversubscription << 16: 0 = by batch
                                   size, 1 = none, M = M x the resident grid)    */
 int tcpck_batch_fixed_ex(tcpck_ctx *ctx, int op, int mode, void *d_arena,

@@ -59,6 +59,8 @@ for s in ${STEPS:-tests smoke bench prof}; do
     gspol) step gspol 600 python scripts/gstream_probe.py --ops checksum,fill --lengths 32,128,512 --gs 0,2,0x10,0x20,0x40,0x80,0x100,0x22 ;;
     gsfill) step gsfill 600 python scripts/gstream_probe.py --ops fill --lengths 32,64,128,256,512,1024 --gs 0,0x80,0x200,0x201,0x202 ;;
     gsorder) step gsorder 600 python scripts/gstream_probe.py --ops fill --lengths 32,256,512,1024 --gs 0,0x80,0x100,0x200,0x201,0x202 ;;
+    gswb) step gswb_tests 600 python -u -m pytest tests/test_gpu_kernels.py -x -q --timeout 120 --timeout-method thread -k "gstream_fill" &&
+      step gswb 600 python scripts/gstream_probe.py --ops fill --lengths 32,64,128,256,512,1024 --gs 0x200,0x400,0x800,0xC00,0x401 ;;
     keep) step keep 600 python scripts/keep_probe.py ;;
     vvkeep) step vvkeep 900 python -u -m pytest tests/test_gpu_kernels.py -x -q --timeout 300 --timeout-method thread -k "vvstream" ;;
     gsstage) step gsstage 600 python scripts/gstream_probe.py --ops checksum,fill --lengths 32,64,128,256,1024 --gs 0,2,0x800,0x802,0x80,0x880 ;;

@@ -217,9 +217,13 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
       // the lines with the default cache policy keeps them in L2 until the
       // field store lands, so they leave as whole lines rather than masked
       // partial writes (scripts/gstream_probe.py, profiles/r01/gstream_fill.log:
-      // 32 B 21.4 -> 32 % of the roof, 256 B 33 -> 43 %, 512 B 46 -> 57 %)
+      // 32 B 21.4 -> 32 % of the roof, 256 B 33 -> 43 %, 512 B 46 -> 57 %).
+      // Up to 128 B, writing every chunk back whole (twice the bytes, all of
+      // them full-line writes) beats even that (profiles/r01/gstream_writeback.log:
+      // 32 B 33.9 -> 41.3 %, 64 B 32.5 -> 40.2 %, 128 B 36.3 -> 40.3 %; 256 B
+      // 44.7 vs 39.9 % keeps the default-policy loads)
       kernel = TCPCK_KERNEL_GSTREAM;
-      param = len <= 256 ? tcpck::kGstreamDefaultLoads : 0;
+      param = len <= 128 ? tcpck::kGstreamWriteBack : (len <= 256 ? tcpck::kGstreamDefaultLoads : 0);
     } else if (len < 512) {
       // packed, by image length (scripts/policy_sweep.py, profiles/r01/policy_small.log):
       // below 512 B boundaries are dense enough that resolving all of a step's

@@ -48,7 +48,10 @@ __device__ __forceinline__ uint32_t lane_group_sum(uint32_t x) {
 // SPOL: results stored through a buffer resource over the run's out[] slice
 // with these cache-policy bits (-1: plain global stores); LPOL: load policy
 // bits (2 = nt).  Tuning (variant bits 8-11, 12, scripts/gstream_probe.py).
-template <int U, int G, int OP, int SPOL = -1, int LPOL = 2, bool FLINE = false>
+// WB >= 0 (kFill): every lane writes its whole 16-B chunk back, the field
+// patched, with store policy WB: the image's lines leave as full-line writes
+// instead of one masked partial write per image (twice the traffic).
+template <int U, int G, int OP, int SPOL = -1, int LPOL = 2, bool FLINE = false, int WB = -1>
 __global__ void __launch_bounds__(kBlock) gstream_kernel(GroupStreamArgs a) {
   constexpr uint32_t S = 16 * G;     // image bytes
   constexpr uint32_t P = 1024 / S;   // images per step
@@ -113,6 +116,13 @@ __global__ void __launch_bounds__(kBlock) gstream_kernel(GroupStreamArgs a) {
             if (leader) __builtin_amdgcn_raw_buffer_store_b16(c, orsrc, static_cast<int>(vo), 0, SPOL);
             if (OP == kFill && field_lane && k < a.count) dev::store16_field(rsrc, (st << 10) + (lane << 4) + 12, c);
           }
+        } else if (OP == kFill && WB >= 0) {
+          if (leader && a.out && k < a.count) static_cast<uint16_t *>(a.out)[k] = c;
+          if (field_lane) w.w |= c;  // the field was zeroed above
+          typedef unsigned v4u __attribute__((ext_vector_type(4)));
+          // range-checked: chunks past the batch drop
+          __builtin_amdgcn_raw_buffer_store_b128(v4u{w.x, w.y, w.z, w.w}, rsrc, static_cast<int>((st << 10) + (lane << 4)), 0,
+                                                 WB < 0 ? 0 : WB);
         } else if (k < a.count) {
           if constexpr (OP == kVerify) {
             if (leader) static_cast<uint8_t *>(a.out)[k] = (c == 0) ? 1 : 0;
@@ -129,9 +139,9 @@ __global__ void __launch_bounds__(kBlock) gstream_kernel(GroupStreamArgs a) {
   }
 }
 
-template <int U, int G, int OP, int SPOL, int LPOL, bool FLINE>
+template <int U, int G, int OP, int SPOL, int LPOL, bool FLINE, int WB = -1>
 hipError_t launch_one(const GroupStreamArgs &a, uint32_t num_cus, hipStream_t stream) {
-  static const uint32_t per_cu = dev::resident_blocks_per_cu(gstream_kernel<U, G, OP, SPOL, LPOL, FLINE>);
+  static const uint32_t per_cu = dev::resident_blocks_per_cu(gstream_kernel<U, G, OP, SPOL, LPOL, FLINE, WB>);
   const uint64_t resident = static_cast<uint64_t>(per_cu) * num_cus;
   const uint64_t bytes = a.count * (16u * G);
   const uint64_t steps = (bytes + 1023) >> 10;
@@ -144,29 +154,29 @@ hipError_t launch_one(const GroupStreamArgs &a, uint32_t num_cus, hipStream_t st
   b.per_wave = steps / (blocks * kWavesPerBlock);
   b.rem = steps % (blocks * kWavesPerBlock);
   if (((b.per_wave + 1 + U) << 10) >= (uint64_t{1} << 31)) return hipErrorInvalidValue;  // u32 run offsets
-  hipLaunchKernelGGL((gstream_kernel<U, G, OP, SPOL, LPOL, FLINE>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0, stream, b);
+  hipLaunchKernelGGL((gstream_kernel<U, G, OP, SPOL, LPOL, FLINE, WB>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0, stream, b);
   return hipGetLastError();
 }
 
-template <int U, int G, int SPOL, int LPOL, bool FLINE>
+template <int U, int G, int SPOL, int LPOL, bool FLINE, int WB>
 hipError_t by_op(int op, const GroupStreamArgs &a, uint32_t num_cus, hipStream_t s) {
   switch (op) {
     case kChecksum: return launch_one<U, G, kChecksum, SPOL, LPOL, false>(a, num_cus, s);
-    case kFill: return launch_one<U, G, kFill, SPOL, LPOL, FLINE>(a, num_cus, s);
+    case kFill: return launch_one<U, G, kFill, SPOL, LPOL, FLINE, WB>(a, num_cus, s);
     case kVerify: return launch_one<U, G, kVerify, SPOL, LPOL, false>(a, num_cus, s);
     default: return hipErrorInvalidValue;
   }
 }
 
-template <int U, int SPOL = -1, int LPOL = 2, bool FLINE = false>
+template <int U, int SPOL = -1, int LPOL = 2, bool FLINE = false, int WB = -1>
 hipError_t by_len(int op, const GroupStreamArgs &a, uint32_t num_cus, hipStream_t s) {
   switch (a.len) {
-    case 32: return by_op<U, 2, SPOL, LPOL, FLINE>(op, a, num_cus, s);
-    case 64: return by_op<U, 4, SPOL, LPOL, FLINE>(op, a, num_cus, s);
-    case 128: return by_op<U, 8, SPOL, LPOL, FLINE>(op, a, num_cus, s);
-    case 256: return by_op<U, 16, SPOL, LPOL, FLINE>(op, a, num_cus, s);
-    case 512: return by_op<U, 32, SPOL, LPOL, FLINE>(op, a, num_cus, s);
-    case 1024: return by_op<U, 64, SPOL, LPOL, FLINE>(op, a, num_cus, s);
+    case 32: return by_op<U, 2, SPOL, LPOL, FLINE, WB>(op, a, num_cus, s);
+    case 64: return by_op<U, 4, SPOL, LPOL, FLINE, WB>(op, a, num_cus, s);
+    case 128: return by_op<U, 8, SPOL, LPOL, FLINE, WB>(op, a, num_cus, s);
+    case 256: return by_op<U, 16, SPOL, LPOL, FLINE, WB>(op, a, num_cus, s);
+    case 512: return by_op<U, 32, SPOL, LPOL, FLINE, WB>(op, a, num_cus, s);
+    case 1024: return by_op<U, 64, SPOL, LPOL, FLINE, WB>(op, a, num_cus, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -183,7 +193,17 @@ hipError_t launch_gstream(int op, int variant, const GroupStreamArgs &a, uint32_
   if (a.count == 0) return hipSuccess;
   GroupStreamArgs b = a;
   b.order = (variant & 4) ? dev::kOrderDefault : 4u;  // XCD-chunked order, groups of 16 blocks
-  if (variant & ~0x3F7) return hipErrorInvalidValue;
+  if (variant & ~0xFF7) return hipErrorInvalidValue;
+  if (variant & 0xC00) {  // FILL: whole-chunk write-back (bit 10: nt stores, bit 11: default policy)
+    if (op != kFill) return hipErrorInvalidValue;
+    switch (variant & 0xDF3) {
+      case 0x400: return by_len<4, -1, 2, false, 2>(op, b, num_cus, stream);
+      case 0x800: return by_len<4, -1, 2, false, 0>(op, b, num_cus, stream);
+      case 0x401: return by_len<8, -1, 2, false, 2>(op, b, num_cus, stream);
+      case 0xC00: return by_len<4, -1, 2, false, 16>(op, b, num_cus, stream);  // sc1
+      default: return hipErrorInvalidValue;
+    }
+  }
   if (variant & 0x200) {  // FILL field lines with the default load policy
     switch (variant & 0x1F3) {
       case 0: return by_len<4, -1, 2, true>(op, b, num_cus, stream);

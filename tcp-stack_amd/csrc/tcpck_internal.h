@@ -92,8 +92,12 @@ bool gstream_applies(const uint8_t *arena, uint64_t stride, uint32_t len);
 // loads with the default cache policy instead of nt (AUTO for FILL <= 256 B);
 // tuning: 0x10 / 0x20 / 0x40 results through a buffer resource with the
 // default / nt / sc1 policy, 0x100 default-policy loads + 0x10, 0x200-0x202
-// FILL with default-policy loads for the field lines only (U4 / U8 / U2)
+// FILL with default-policy loads for the field lines only (U4 / U8 / U2);
+// FILL only: 0x400 / 0x800 / 0xC00 every chunk written back whole with the
+// nt / default / sc1 store policy (U4), kGstreamWriteBack: nt, U8 (AUTO for
+// FILL <= 128 B)
 constexpr int kGstreamDefaultLoads = 0x80;
+constexpr int kGstreamWriteBack = 0x401;
 hipError_t launch_gstream(int op, int variant, const GroupStreamArgs &a, uint32_t num_cus, hipStream_t stream);
 
 // ---- rstream (fixed stride == len): one run per wave, scalar boundary walk.

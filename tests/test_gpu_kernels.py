@@ -489,6 +489,34 @@ def test_gstream_fill_verify(ctx, variant, length):
     np.testing.assert_array_equal(np.nonzero(host(ok) == 0)[0], np.sort(bad))
 
 
+GS_WRITEBACK = [0x400, 0x800, 0x401, 0xC00]  # FILL only: whole-chunk write-back
+
+
+@pytest.mark.parametrize("variant", GS_WRITEBACK)
+@pytest.mark.parametrize("length", GS_LENGTHS)
+@pytest.mark.parametrize("count", [1, 33, 9001])
+def test_gstream_fill_writeback(ctx, variant, length, count):
+    """The write-back FILL rewrites every chunk of the batch: the images must come back
+    byte-exact except the field, and the guard bytes after the batch untouched."""
+    import tcpck
+    from oracle import ref16 as R
+    rng = np.random.default_rng(length * 7 + count + variant)
+    for mis in (0, 16):
+        arena_np = rng.integers(0, 256, count * length + 256 + mis, dtype=np.uint8)
+        arena = dev(arena_np)
+        out = torch.empty(count, dtype=torch.int16, device="cuda")
+        ctx.batch_fixed_ex(tcpck.OP_FILL, arena.data_ptr() + mis, length, length, count, out,
+                           tcpck.KERNEL_GSTREAM, variant)
+        exp_arena = arena_np.copy()
+        body = exp_arena[mis:mis + count * length]
+        exp = np.array([R.fill_np(body[k * length:(k + 1) * length]) for k in range(count)], np.uint16)
+        exp_arena[mis:mis + count * length] = body
+        np.testing.assert_array_equal(host(out).view(np.uint16), exp)
+        np.testing.assert_array_equal(host(arena), exp_arena)
+    with pytest.raises(tcpck.TcpckError):  # CHECKSUM / VERIFY have nothing to write back
+        ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, arena, length, length, count, out, tcpck.KERNEL_GSTREAM, variant)
+
+
 def test_gstream_golden_header_only(ctx, golden):
     """Header-only images (MakeTcpPacket(0), 32 B) from the golden fixtures, packed at stride 32."""
     import tcpck
@@ -511,7 +539,7 @@ def test_gstream_reject(ctx):
         ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, a.data_ptr() + 2, 64, 64, 100, o, tcpck.KERNEL_GSTREAM, 0)
     with pytest.raises(tcpck.TcpckError):  # RFC 1071 mode: seg only
         ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, a, 64, 64, 100, o, tcpck.KERNEL_GSTREAM, 0, mode=1)
-    for v in (3, 8, 0x30, 0x400):  # no such variant
+    for v in (3, 8, 0x30, 0x1000):  # no such variant
         with pytest.raises(tcpck.TcpckError):
             ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, a, 64, 64, 100, o, tcpck.KERNEL_GSTREAM, v)
     ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, a, 64, 64, 0, o, tcpck.KERNEL_GSTREAM, 0)  # empty batch: no-op
