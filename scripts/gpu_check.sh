@@ -61,6 +61,9 @@ for s in ${STEPS:-tests smoke bench prof}; do
     gsorder) step gsorder 600 python scripts/gstream_probe.py --ops fill --lengths 32,256,512,1024 --gs 0,0x80,0x100,0x200,0x201,0x202 ;;
     gswb) step gswb_tests 600 python -u -m pytest tests/test_gpu_kernels.py -x -q --timeout 120 --timeout-method thread -k "gstream_fill" &&
       step gswb 600 python scripts/gstream_probe.py --ops fill --lengths 32,64,128,256,512,1024 --gs 0x200,0x400,0x800,0xC00,0x401 ;;
+    gsnp) step gsnp_tests 600 python -u -m pytest tests/test_gpu_kernels.py -x -q --timeout 120 --timeout-method thread -k "gstream_np or gstream_reject or gstream_fill" &&
+      step gsnp_fill 600 python scripts/gstream_probe.py --ops fill --lengths 48,96,128,144,192,240 --gs 0,0x80,0x400,0x401 &&
+      step gsnp_ck 600 python scripts/gstream_probe.py --ops checksum --lengths 48,96,192,240 --gs 0,1,0x80 ;;
     keep) step keep 600 python scripts/keep_probe.py ;;
     vvkeep) step vvkeep 900 python -u -m pytest tests/test_gpu_kernels.py -x -q --timeout 300 --timeout-method thread -k "vvstream" ;;
     gsstage) step gsstage 600 python scripts/gstream_probe.py --ops checksum,fill --lengths 32,64,128,256,1024 --gs 0,2,0x800,0x802,0x80,0x880 ;;

@@ -212,7 +212,8 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
         param = (tcpck::kShapeSmall + 1) | kSegXcdOrder;
       }
     } else if (op == TCPCK_OP_FILL && tcpck::gstream_applies(arena, stride, len)) {
-      // send-path FILL of power-of-two images, 32 B (pure ACKs) .. 1 KiB:
+      // send-path FILL of power-of-two images, 32 B (pure ACKs) .. 1 KiB, and
+      // of the other multiples of 16 B up to 240 B:
       // gstream; up to 256 B every line holds a checksum field, and reading
       // the lines with the default cache policy keeps them in L2 until the
       // field store lands, so they leave as whole lines rather than masked
@@ -221,7 +222,10 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
       // Up to 128 B, writing every chunk back whole (twice the bytes, all of
       // them full-line writes) beats even that (profiles/r01/gstream_writeback.log:
       // 32 B 33.9 -> 41.3 %, 64 B 32.5 -> 40.2 %, 128 B 36.3 -> 40.3 %; 256 B
-      // 44.7 vs 39.9 % keeps the default-policy loads)
+      // 44.7 vs 39.9 % keeps the default-policy loads).  The other multiples of
+      // 16 B up to 240 B take the same rule (profiles/r01/gstream_np.log: 48 B
+      // 29.0 -> 36.1 %, 96 B 29.7 -> 37.0 %; 144-240 B default-policy loads
+      // 1-2 points ahead of vvstream FIXED)
       kernel = TCPCK_KERNEL_GSTREAM;
       param = len <= 128 ? tcpck::kGstreamWriteBack : (len <= 256 ? tcpck::kGstreamDefaultLoads : 0);
     } else if (len < 512) {

@@ -23,6 +23,13 @@
 //
 // Runs are contiguous ranges of whole steps (equal counts, split by the
 // launcher); with a 128-B aligned arena no line is shared by two runs.
+//
+// Other multiples of 16 B up to 240 B (48, 80, 96 (64-B payloads), ... B;
+// G = 3 .. 15 not a power of two): a step is the P = 64 / G whole images that
+// fit one wave, B = P * S bytes (96 B: 10 images, 960 B, 60 lanes); the idle
+// lanes load and store out of the buffer range (nothing moves).  Group sums
+// come from a wave-wide inclusive scan (6 shuffles) and two reads of it at the
+// group's edges.  Variants 0-2, 4, 0x80 and the FILL write-back 0x400 / 0x401.
 #include "tcpck_device.h"
 
 namespace tcpck {
@@ -51,10 +58,30 @@ __device__ __forceinline__ uint32_t lane_group_sum(uint32_t x) {
 // WB >= 0 (kFill): every lane writes its whole 16-B chunk back, the field
 // patched, with store policy WB: the image's lines leave as full-line writes
 // instead of one masked partial write per image (twice the traffic).
+// any G in [2, 64]: aligned groups of G lanes from lane 0 (the idle lanes past
+// the last whole group get garbage)
+template <int G>
+__device__ __forceinline__ uint32_t lane_group_sum_any(uint32_t x, uint32_t lane) {
+  if constexpr ((G & (G - 1)) == 0) {
+    return lane_group_sum<G>(x);
+  } else {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(x, d, 64);
+      if (lane >= static_cast<uint32_t>(d)) x += y;
+    }
+    const uint32_t base = (lane / G) * G;
+    const uint32_t hi = __shfl(x, static_cast<int>(base + G - 1) & 63, 64);
+    const uint32_t lo = __shfl(x, static_cast<int>(base + 63) & 63, 64);  // lane base - 1
+    return base ? hi - lo : hi;
+  }
+}
+
 template <int U, int G, int OP, int SPOL = -1, int LPOL = 2, bool FLINE = false, int WB = -1>
 __global__ void __launch_bounds__(kBlock) gstream_kernel(GroupStreamArgs a) {
   constexpr uint32_t S = 16 * G;     // image bytes
-  constexpr uint32_t P = 1024 / S;   // images per step
+  constexpr uint32_t P = 64 / G;     // images per step
+  constexpr uint32_t B = P * S;      // step bytes (1024 for a power-of-two G)
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t bid = dev::ordered_block(blockIdx.x, gridDim.x, a.order);
   const uint64_t wid = static_cast<uint64_t>(bid) * kWavesPerBlock +
@@ -62,15 +89,18 @@ __global__ void __launch_bounds__(kBlock) gstream_kernel(GroupStreamArgs a) {
   uint64_t sb, se;  // the wave's steps [sb, se)
   dev::count_split(wid, a.per_wave, a.rem, sb, se);
   if (sb >= se) return;
-  const uint64_t byte0 = sb << 10;
+  const uint64_t byte0 = sb * B;
   const uint64_t left = a.count * S - byte0;  // > 0: sb < steps
   const uint32_t nsteps = static_cast<uint32_t>(se - sb);
-  const uint64_t run = static_cast<uint64_t>(nsteps) << 10;
+  const uint64_t run = static_cast<uint64_t>(nsteps) * B;
   // records cover the run's image bytes; loads past them (the batch tail, the
   // ring's look-ahead past the run) read 0 without a memory access
   const auto rsrc = dev::make_rsrc(a.arena + byte0, static_cast<uint32_t>(run < left ? run : left));
   const uint64_t k0 = sb * P + lane / G;  // image of this lane's chunk in the run's first step
-  const bool leader = (lane % G) == 0;
+  // lanes past the step's last whole image: offsets past any buffer range
+  const bool live = lane < P * G;
+  const uint32_t loff = live ? lane << 4 : 0x80000000u;
+  const bool leader = live && (lane % G) == 0;
   constexpr uint32_t kOutBytes = OP == kVerify ? 1u : 2u;
   const uint64_t kend = (se * P < a.count) ? se * P : a.count;
   const auto orsrc = dev::make_rsrc(static_cast<uint8_t *>(a.out) + kOutBytes * sb * P,
@@ -90,11 +120,11 @@ __global__ void __launch_bounds__(kBlock) gstream_kernel(GroupStreamArgs a) {
     }
     return u32x4{v.x, v.y, v.z, v.w};
   };
-  const bool field_lane = (lane % G) == 1;
+  const bool field_lane = live && (lane % G) == 1;
 
   u32x4 ring[U];
 #pragma unroll
-  for (int u = 0; u < U; ++u) ring[u] = load((static_cast<uint32_t>(u) << 10) + (lane << 4));
+  for (int u = 0; u < U; ++u) ring[u] = load(static_cast<uint32_t>(u) * B + loff);
 
   for (uint32_t g = 0; g < nsteps; g += U) {
 #pragma unroll
@@ -105,7 +135,7 @@ __global__ void __launch_bounds__(kBlock) gstream_kernel(GroupStreamArgs a) {
         if constexpr (OP == kFill) {
           if (field_lane) w.w &= 0xFFFF0000u;  // bytes 28-29 of the image read as 0
         }
-        const uint32_t sum = lane_group_sum<G>(dev::ref_chunk_sum_dot(w));
+        const uint32_t sum = lane_group_sum_any<G>(dev::ref_chunk_sum_dot(w), lane);
         const uint16_t c = static_cast<uint16_t>(~sum);  // tcp-header.h:262
         const uint64_t k = k0 + static_cast<uint64_t>(st) * P;
         if constexpr (SPOL >= 0) {
@@ -114,27 +144,27 @@ __global__ void __launch_bounds__(kBlock) gstream_kernel(GroupStreamArgs a) {
             if (leader) __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(c == 0), orsrc, static_cast<int>(vo), 0, SPOL);
           } else {
             if (leader) __builtin_amdgcn_raw_buffer_store_b16(c, orsrc, static_cast<int>(vo), 0, SPOL);
-            if (OP == kFill && field_lane && k < a.count) dev::store16_field(rsrc, (st << 10) + (lane << 4) + 12, c);
+            if (OP == kFill && field_lane && k < a.count) dev::store16_field(rsrc, st * B + loff + 12, c);
           }
         } else if (OP == kFill && WB >= 0) {
           if (leader && a.out && k < a.count) static_cast<uint16_t *>(a.out)[k] = c;
           if (field_lane) w.w |= c;  // the field was zeroed above
           typedef unsigned v4u __attribute__((ext_vector_type(4)));
           // range-checked: chunks past the batch drop
-          __builtin_amdgcn_raw_buffer_store_b128(v4u{w.x, w.y, w.z, w.w}, rsrc, static_cast<int>((st << 10) + (lane << 4)), 0,
+          __builtin_amdgcn_raw_buffer_store_b128(v4u{w.x, w.y, w.z, w.w}, rsrc, static_cast<int>(st * B + loff), 0,
                                                  WB < 0 ? 0 : WB);
         } else if (k < a.count) {
           if constexpr (OP == kVerify) {
             if (leader) static_cast<uint8_t *>(a.out)[k] = (c == 0) ? 1 : 0;
           } else {
             if (leader && a.out) static_cast<uint16_t *>(a.out)[k] = c;
-            if (OP == kFill && field_lane) dev::store16_field(rsrc, (st << 10) + (lane << 4) + 12, c);
+            if (OP == kFill && field_lane) dev::store16_field(rsrc, st * B + loff + 12, c);
           }
         }
       }
       // the slot's data is dead: refill in place (the step offset in the VGPR
       // offset, which the range check always covers)
-      ring[u] = load(((st + U) << 10) + (lane << 4));
+      ring[u] = load((st + U) * B + loff);
     }
   }
 }
@@ -144,7 +174,8 @@ hipError_t launch_one(const GroupStreamArgs &a, uint32_t num_cus, hipStream_t st
   static const uint32_t per_cu = dev::resident_blocks_per_cu(gstream_kernel<U, G, OP, SPOL, LPOL, FLINE, WB>);
   const uint64_t resident = static_cast<uint64_t>(per_cu) * num_cus;
   const uint64_t bytes = a.count * (16u * G);
-  const uint64_t steps = (bytes + 1023) >> 10;
+  constexpr uint32_t B = (64 / G) * 16u * G;
+  const uint64_t steps = (bytes + B - 1) / B;
   // runs of >= 4 KiB, up to 1024 x the resident grid (the rstream rule)
   uint64_t blocks = resident * dev::oversub_for(a.oversub, bytes, resident * kWavesPerBlock, 1024);
   const uint64_t need = (steps + kWavesPerBlock - 1) / kWavesPerBlock;  // >= 1 step per wave
@@ -153,7 +184,7 @@ hipError_t launch_one(const GroupStreamArgs &a, uint32_t num_cus, hipStream_t st
   GroupStreamArgs b = a;
   b.per_wave = steps / (blocks * kWavesPerBlock);
   b.rem = steps % (blocks * kWavesPerBlock);
-  if (((b.per_wave + 1 + U) << 10) >= (uint64_t{1} << 31)) return hipErrorInvalidValue;  // u32 run offsets
+  if ((b.per_wave + 1 + U) * B >= (uint64_t{1} << 31)) return hipErrorInvalidValue;  // u32 run offsets
   hipLaunchKernelGGL((gstream_kernel<U, G, OP, SPOL, LPOL, FLINE, WB>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0, stream, b);
   return hipGetLastError();
 }
@@ -181,10 +212,42 @@ hipError_t by_len(int op, const GroupStreamArgs &a, uint32_t num_cus, hipStream_
   }
 }
 
+// the other multiples of 16 B up to 240 B (scan-based group sums)
+template <int U, int LPOL = 2, int WB = -1>
+hipError_t by_len_np(int op, const GroupStreamArgs &a, uint32_t num_cus, hipStream_t s) {
+  switch (a.len) {
+    case 48: return by_op<U, 3, -1, LPOL, false, WB>(op, a, num_cus, s);
+    case 80: return by_op<U, 5, -1, LPOL, false, WB>(op, a, num_cus, s);
+    case 96: return by_op<U, 6, -1, LPOL, false, WB>(op, a, num_cus, s);
+    case 112: return by_op<U, 7, -1, LPOL, false, WB>(op, a, num_cus, s);
+    case 144: return by_op<U, 9, -1, LPOL, false, WB>(op, a, num_cus, s);
+    case 160: return by_op<U, 10, -1, LPOL, false, WB>(op, a, num_cus, s);
+    case 176: return by_op<U, 11, -1, LPOL, false, WB>(op, a, num_cus, s);
+    case 192: return by_op<U, 12, -1, LPOL, false, WB>(op, a, num_cus, s);
+    case 208: return by_op<U, 13, -1, LPOL, false, WB>(op, a, num_cus, s);
+    case 224: return by_op<U, 14, -1, LPOL, false, WB>(op, a, num_cus, s);
+    case 240: return by_op<U, 15, -1, LPOL, false, WB>(op, a, num_cus, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t launch_np(int op, int variant, const GroupStreamArgs &b, uint32_t num_cus, hipStream_t stream) {
+  switch (variant & ~4) {
+    case 0: return by_len_np<4>(op, b, num_cus, stream);
+    case 1: return by_len_np<8>(op, b, num_cus, stream);
+    case 2: return by_len_np<2>(op, b, num_cus, stream);
+    case 0x80: return by_len_np<4, 0>(op, b, num_cus, stream);
+    case 0x400: return op == kFill ? by_len_np<4, 2, 2>(op, b, num_cus, stream) : hipErrorInvalidValue;
+    case 0x401: return op == kFill ? by_len_np<8, 2, 2>(op, b, num_cus, stream) : hipErrorInvalidValue;
+    default: return hipErrorInvalidValue;
+  }
+}
+
 }  // namespace
 
 bool gstream_applies(const uint8_t *arena, uint64_t stride, uint32_t len) {
-  return stride == len && len >= 32 && len <= 1024 && (len & (len - 1)) == 0 &&
+  const bool pow2 = (len & (len - 1)) == 0;
+  return stride == len && len >= 32 && len <= 1024 && (len & 15u) == 0 && (pow2 || len <= 240) &&
          (reinterpret_cast<uintptr_t>(arena) & 15u) == 0;
 }
 
@@ -194,6 +257,7 @@ hipError_t launch_gstream(int op, int variant, const GroupStreamArgs &a, uint32_
   GroupStreamArgs b = a;
   b.order = (variant & 4) ? dev::kOrderDefault : 4u;  // XCD-chunked order, groups of 16 blocks
   if (variant & ~0xFF7) return hipErrorInvalidValue;
+  if (a.len & (a.len - 1)) return launch_np(op, variant, b, num_cus, stream);
   if (variant & 0xC00) {  // FILL: whole-chunk write-back (bit 10: nt stores, bit 11: default policy)
     if (op != kFill) return hipErrorInvalidValue;
     switch (variant & 0xDF3) {

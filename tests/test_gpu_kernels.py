@@ -490,6 +490,55 @@ def test_gstream_fill_verify(ctx, variant, length):
 
 
 GS_WRITEBACK = [0x400, 0x800, 0x401, 0xC00]  # FILL only: whole-chunk write-back
+# multiples of 16 B up to 240 B that are not powers of two: P = 64 / G images per step
+GS_NP_LENGTHS = [48, 80, 96, 112, 144, 176, 192, 240]
+GS_NP = [0, 1, 2, 4, 0x80]
+
+
+@pytest.mark.parametrize("variant", GS_NP)
+@pytest.mark.parametrize("length", GS_NP_LENGTHS)
+@pytest.mark.parametrize("count", [1, 9, 11, 65, 3001])
+def test_gstream_np_vs_oracle(ctx, oracle_c, variant, length, count):
+    """Steps of P = 64 / G whole images (idle lanes at the top of the wave), ragged
+    counts, 16-B misaligned arenas, grid oversubscription."""
+    import tcpck
+    rng = np.random.default_rng(length * 13 + count + variant)
+    arena_np = rng.integers(0, 256, count * length + 128, dtype=np.uint8)
+    arena_np[:length] = 0xFF
+    buf = dev(arena_np)
+    for mis, oversub in ((0, 0), (16, 0), (48, 1), (0, 8)):
+        out = torch.full((count + 1,), -1, dtype=torch.int16, device="cuda")
+        ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, buf.data_ptr() + mis, length, length, count, out,
+                           tcpck.KERNEL_GSTREAM, variant | (oversub << 16))
+        exp = oracle_c.batch(arena_np[mis:], stride=length, length=length, count=count, threads=8)
+        got = host(out).view(np.uint16)
+        np.testing.assert_array_equal(got[:count], exp)
+        assert got[count] == 0xFFFF  # nothing written past the batch
+        ok = torch.full((count + 1,), 7, dtype=torch.uint8, device="cuda")
+        ctx.batch_fixed_ex(tcpck.OP_VERIFY, buf.data_ptr() + mis, length, length, count, ok,
+                           tcpck.KERNEL_GSTREAM, variant | (oversub << 16))
+        np.testing.assert_array_equal(host(ok)[:count], (exp == 0).astype(np.uint8))
+        assert host(ok)[count] == 7
+
+
+@pytest.mark.parametrize("variant", GS_NP + [0x400, 0x401])
+@pytest.mark.parametrize("length", GS_NP_LENGTHS)
+@pytest.mark.parametrize("count", [1, 11, 9001])
+def test_gstream_np_fill(ctx, variant, length, count):
+    import tcpck
+    from oracle import ref16 as R
+    rng = np.random.default_rng(length * 5 + count + variant)
+    for mis in (0, 16):
+        arena_np = rng.integers(0, 256, count * length + 256 + mis, dtype=np.uint8)
+        arena = dev(arena_np)
+        out = torch.empty(count, dtype=torch.int16, device="cuda")
+        ctx.batch_fixed_ex(tcpck.OP_FILL, arena.data_ptr() + mis, length, length, count, out,
+                           tcpck.KERNEL_GSTREAM, variant)
+        exp_arena = arena_np.copy()
+        body = exp_arena[mis:mis + count * length]  # a view: fill_np writes the fields in place
+        exp = np.array([R.fill_np(body[k * length:(k + 1) * length]) for k in range(count)], np.uint16)
+        np.testing.assert_array_equal(host(out).view(np.uint16), exp)
+        np.testing.assert_array_equal(host(arena), exp_arena)
 
 
 @pytest.mark.parametrize("variant", GS_WRITEBACK)
@@ -510,7 +559,6 @@ def test_gstream_fill_writeback(ctx, variant, length, count):
         exp_arena = arena_np.copy()
         body = exp_arena[mis:mis + count * length]
         exp = np.array([R.fill_np(body[k * length:(k + 1) * length]) for k in range(count)], np.uint16)
-        exp_arena[mis:mis + count * length] = body
         np.testing.assert_array_equal(host(out).view(np.uint16), exp)
         np.testing.assert_array_equal(host(arena), exp_arena)
     with pytest.raises(tcpck.TcpckError):  # CHECKSUM / VERIFY have nothing to write back
@@ -532,7 +580,7 @@ def test_gstream_reject(ctx):
     import tcpck
     a = torch.zeros(1 << 20, dtype=torch.uint8, device="cuda")
     o = torch.zeros(4096, dtype=torch.int16, device="cuda")
-    for stride, length in ((96, 96), (16, 16), (2048, 2048), (64, 32), (1492, 1492)):
+    for stride, length in ((272, 272), (100, 100), (16, 16), (2048, 2048), (64, 32), (1492, 1492)):
         with pytest.raises(tcpck.TcpckError):
             ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, a, stride, length, 100, o, tcpck.KERNEL_GSTREAM, 0)
     with pytest.raises(tcpck.TcpckError):  # arena not 16-B aligned

@@ -399,10 +399,10 @@ def test_set_ack_argument_errors(ctx):
 # ---- AUTO policy boundaries: rstream / jumbo W-shapes / vvstream / gstream hand-overs ----------
 
 
-@pytest.mark.parametrize("length", [32, 64, 256, 1024])
+@pytest.mark.parametrize("length", [32, 48, 64, 96, 240, 256, 1024])
 @pytest.mark.parametrize("mis", [0, 2, 16])
 def test_auto_fill_small_pow2_alignment(ctx, length, mis):
-    """AUTO FILL of power-of-two images takes gstream only for a 16-B aligned arena;
+    """AUTO FILL of power-of-two images (and multiples of 16 B up to 240 B) takes gstream only for a 16-B aligned arena;
     any other pointer goes to the general kernels -- same arena bytes and results."""
     import tcpck
     from oracle import ref16 as R
@@ -418,7 +418,7 @@ def test_auto_fill_small_pow2_alignment(ctx, length, mis):
     np.testing.assert_array_equal(host(out).view(np.uint16), exp)
     np.testing.assert_array_equal(host(buf), exp_arena)
 
-@pytest.mark.parametrize("length", [30, 32, 34, 64, 96, 128, 256, 258, 510, 512, 1024, 1026, 4094, 4096,
+@pytest.mark.parametrize("length", [30, 32, 34, 48, 64, 96, 128, 240, 256, 258, 272, 510, 512, 1024, 1026, 4094, 4096,
                                     4098, 6144, 8192, 8194, 16384, 16386, 32768, 32770, 98304])
 @pytest.mark.parametrize("mode", [0, 1])
 def test_auto_policy_boundaries_fixed(ctx, oracle_c, length, mode):
