@@ -64,6 +64,10 @@ for s in ${STEPS:-tests smoke bench prof}; do
     gsnp) step gsnp_tests 600 python -u -m pytest tests/test_gpu_kernels.py -x -q --timeout 120 --timeout-method thread -k "gstream_np or gstream_reject or gstream_fill" &&
       step gsnp_fill 600 python scripts/gstream_probe.py --ops fill --lengths 48,96,128,144,192,240 --gs 0,0x80,0x400,0x401 &&
       step gsnp_ck 600 python scripts/gstream_probe.py --ops checksum --lengths 48,96,192,240 --gs 0,1,0x80 ;;
+    fjumbo) step fjumbo 600 python scripts/fill_wb_probe.py --lengths 4096,4098,6144,8192,9000,12000,16384,24576,32768,49152,65536 ;;
+    fjumbo3) step fjumbo3_tests 600 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -k "auto" &&
+      step fjumbo3 600 python scripts/fill_wb_probe.py --ops checksum,fill --lengths 4098,5000,6144,9000,12000,16384,20000,24576,28000,40000,49152,60000,65536 ;;
+    fjumbo2) step fjumbo2 600 python scripts/fill_wb_probe.py --ops checksum,fill --lengths 5000,7000,9000,10000,14000,20000,28000,40000,49152,60000,65504 ;;
     keep) step keep 600 python scripts/keep_probe.py ;;
     vvkeep) step vvkeep 900 python -u -m pytest tests/test_gpu_kernels.py -x -q --timeout 300 --timeout-method thread -k "vvstream" ;;
     gsstage) step gsstage 600 python scripts/gstream_probe.py --ops checksum,fill --lengths 32,64,128,256,1024 --gs 0,2,0x800,0x802,0x80,0x880 ;;

@@ -154,7 +154,8 @@ void free_stage(tcpck_ctx *ctx) {
 // reference mode:
 //   fixed, stride == len   < 512 B vvstream (prefix table), 512 B..4 KiB
 //                          rstream (scalar boundary walk), larger seg with
-//                          W waves per image (~4 KiB per wave)
+//                          W waves per image (~4 KiB per wave) where the
+//                          image fills seg's steps, else rstream
 //   fixed, stride > len    small gaps vvstream (gaps streamed as virtual
 //                          images), larger gaps seg with 8 lanes per image
 //   packed variable        vvstream, every op
@@ -163,8 +164,9 @@ void free_stage(tcpck_ctx *ctx) {
 // image already streams whole 1 KiB steps) -- seg.
 constexpr uint64_t kRunMaxLen = 16384;       // variable / gapped layouts: above, seg
 constexpr uint64_t kFixedRunMaxLen = 4096;   // packed fixed: rstream up to here; above, seg with W waves
-                                             // per image (C4 64 KiB: W16 91% vs rstream 85-88%,
-                                             // 6 KiB: W2 90.6% vs 87.0%, profiles/r01/jumbo_probe.log)
+                                             // per image where the image fills its steps (jumbo_on_seg;
+                                             // C4 64 KiB: W16 91% vs rstream 85-88%, 6 KiB: W2 90.6% vs
+                                             // 87.0%, profiles/r01/jumbo_probe.log), else rstream
 // Policy parameters.  Every kernel takes its runs in the XCD-chunked block
 // order (dev::ordered_block, groups of 16 blocks per XCD): each XCD streams
 // compact regions instead of every eighth run (C2 86.3% -> 90.6%, C3 82.7 ->
@@ -188,11 +190,28 @@ constexpr int kSegXcdOrder = 1 << 24;    // seg: XCD-chunked order
 constexpr uint64_t kFillKeepMaxLen = 448;
 constexpr int kVvKeep = 32;              // vvstream: kFill reads with the default policy
 
+// Packed fixed images above 4 KiB: seg's W-wave shapes stream W KiB of an
+// image per step (shape_for_len: W = 2, 4, 8, 16 up to 8, 16, 32, 64 KiB), so
+// an image that ends early in its last step wastes the rest of that step --
+// 9000 B on W4 reads as 3 x 4 KiB: 72 % of the roof against rstream's 90 %
+// (profiles/r01/jumbo_fit_probe.log).  seg keeps the sizes it fills to >= 85 %
+// (W16: only in four steps);
+// FILL only from 24 KiB (below, rstream's batched field stores win even at a
+// perfect fit: 8-24 KiB 77-81 % vs 82-84 %).
+static bool jumbo_on_seg(int op, uint64_t len) {
+  if (len > 65536) return true;
+  const uint64_t step = len <= 8192 ? 2048 : (len <= 16384 ? 4096 : (len <= 32768 ? 8192 : 16384));
+  const uint64_t steps = (len + step - 1) / step;
+  const bool fits = 100 * len >= 85 * steps * step && (step < 16384 || steps == 4);  // W16: 48 KiB 81 vs 83 %
+  return op == TCPCK_OP_FILL ? fits && len > 24576 : fits;
+}
+
 hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t stride, uint32_t len,
                      uint64_t count, void *out, int kernel, int param, hipStream_t s) {
   const uint32_t num_cus = static_cast<uint32_t>(ctx->num_cus);
   if (kernel == TCPCK_KERNEL_AUTO) {
-    if (mode != TCPCK_MODE_REF || len < 2 || len > kFixedRunMaxLen || stride > (1u << 24) ||
+    if (mode != TCPCK_MODE_REF || len < 2 || (len > kFixedRunMaxLen && (stride > len || jumbo_on_seg(op, len))) ||
+        stride > (1u << 24) ||
         (stride > len && len > kRunMaxLen)) {
       kernel = TCPCK_KERNEL_SEG;
       param = kSegXcdOrder;  // shape by length

@@ -419,7 +419,8 @@ def test_auto_fill_small_pow2_alignment(ctx, length, mis):
     np.testing.assert_array_equal(host(buf), exp_arena)
 
 @pytest.mark.parametrize("length", [30, 32, 34, 48, 64, 96, 128, 240, 256, 258, 272, 510, 512, 1024, 1026, 4094, 4096,
-                                    4098, 6144, 8192, 8194, 16384, 16386, 32768, 32770, 98304])
+                                    4098, 5000, 6144, 8192, 8194, 9000, 16384, 16386, 24578, 28000, 32768, 32770,
+                                    49152, 60000, 98304])
 @pytest.mark.parametrize("mode", [0, 1])
 def test_auto_policy_boundaries_fixed(ctx, oracle_c, length, mode):
     """Packed fixed batches at every length where the AUTO policy changes kernel or
