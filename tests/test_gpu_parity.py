@@ -447,7 +447,32 @@ def test_auto_policy_boundaries_fixed(ctx, oracle_c, length, mode):
     assert bool(host(ok).all())
 
 
-@pytest.mark.parametrize("typical", [6000, 12000, 24000, 60000])
+@pytest.mark.parametrize("length,stride", [(4500, 4608), (9000, 9216), (9000, 9088), (20000, 20480),
+                                           (40000, 40960), (65536, 69632), (9000, 12000), (4098, 4100)])
+def test_auto_policy_jumbo_gapped(ctx, oracle_c, length, stride):
+    """Jumbo images in slots: small gaps go to vvstream (virtual gap images), larger
+    ones and FILL to seg.  CHECKSUM, FILL (results, fields, untouched gaps), VERIFY."""
+    import tcpck
+    from oracle import ref16 as R
+    rng = np.random.default_rng(length + stride)
+    count = max(8, min(1200, (48 << 20) // stride))
+    arena_np = rng.integers(0, 256, count * stride, dtype=np.uint8)
+    arena = dev(arena_np)
+    out = torch.empty(count, dtype=torch.int16, device="cuda")
+    ctx.batch_fixed(tcpck.OP_CHECKSUM, arena, stride, length, count, out)
+    np.testing.assert_array_equal(host(out).view(np.uint16),
+                                  oracle_c.batch(arena_np, stride=stride, length=length, count=count, threads=8))
+    ctx.batch_fixed(tcpck.OP_FILL, arena, stride, length, count, out)
+    exp_arena = arena_np.copy()
+    exp = np.array([R.fill_np(exp_arena[k * stride:k * stride + length]) for k in range(count)], np.uint16)
+    np.testing.assert_array_equal(host(out).view(np.uint16), exp)
+    np.testing.assert_array_equal(host(arena), exp_arena)
+    ok = torch.empty(count, dtype=torch.uint8, device="cuda")
+    ctx.batch_fixed(tcpck.OP_VERIFY, arena, stride, length, count, ok)
+    assert bool(host(ok).all())
+
+
+@pytest.mark.parametrize("typical", [6000, 12000, 20000, 24000, 40000, 60000])
 def test_auto_policy_jumbo_var(ctx, oracle_c, typical):
     """Variable layouts whose typical length selects a W-waves-per-image shape, with
     lengths spread around it (some far shorter, some zero), packed and with gaps."""
