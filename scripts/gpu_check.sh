@@ -68,6 +68,7 @@ for s in ${STEPS:-tests smoke bench prof}; do
     fjumbo3) step fjumbo3_tests 600 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -k "auto" &&
       step fjumbo3 600 python scripts/fill_wb_probe.py --ops checksum,fill --lengths 4098,5000,6144,9000,12000,16384,20000,24576,28000,40000,49152,60000,65536 ;;
     jlay) step jlay 600 python scripts/jumbo_layout_probe.py ;;
+    jlayf) step jlayf 600 python scripts/jumbo_layout_probe.py --fill ;;
     fjumbo2) step fjumbo2 600 python scripts/fill_wb_probe.py --ops checksum,fill --lengths 5000,7000,9000,10000,14000,20000,28000,40000,49152,60000,65504 ;;
     keep) step keep 600 python scripts/keep_probe.py ;;
     vvkeep) step vvkeep 900 python -u -m pytest tests/test_gpu_kernels.py -x -q --timeout 300 --timeout-method thread -k "vvstream" ;;

@@ -6,7 +6,7 @@ policy (variant 28: gapped slots streamed as virtual images, packed variable as
 one run).  CHECKSUM, back to back after a clock settle; every candidate checked
 against seg's results first.
 
-    python scripts/jumbo_layout_probe.py
+    python scripts/jumbo_layout_probe.py [--fill]
 """
 import os
 import sys
@@ -33,6 +33,7 @@ def report(label, fn, nbytes, s, chk):
 
 
 def main():
+    op = K.OP_FILL if "--fill" in sys.argv else K.OP_CHECKSUM  # FILL: idempotent on the filled arena
     ctx = K.Context(0)
     s = torch.cuda.current_stream()
     for L, S in ((4500, 4608), (9000, 9216), (9000, 9088), (20000, 20480), (40000, 40960)):
@@ -41,13 +42,15 @@ def main():
         K.synth_fixed(a, S, L, n, seed=42)
         ref = torch.empty(n, dtype=torch.int16, device="cuda")
         out = torch.empty(n, dtype=torch.int16, device="cuda")
-        ctx.batch_fixed_ex(K.OP_CHECKSUM, a, S, L, n, ref, K.KERNEL_SEG, 0)
+        ctx.batch_fixed_ex(op, a, S, L, n, ref, K.KERNEL_SEG, 0)
+        snap = a.clone()
 
         def chk():
-            assert torch.equal(out, ref)
-        report(f"gapped {L}/{S} auto", lambda: ctx.batch_fixed(K.OP_CHECKSUM, a, S, L, n, out, stream=s), n * L + 2 * n, s, chk)
-        report(f"gapped {L}/{S} vvstream 28", lambda: ctx.batch_fixed_ex(K.OP_CHECKSUM, a, S, L, n, out, K.KERNEL_VVSTREAM, 28,
+            assert torch.equal(out, ref) and torch.equal(a, snap)
+        report(f"gapped {L}/{S} auto", lambda: ctx.batch_fixed(op, a, S, L, n, out, stream=s), n * L + 2 * n, s, chk)
+        report(f"gapped {L}/{S} vvstream 28", lambda: ctx.batch_fixed_ex(op, a, S, L, n, out, K.KERNEL_VVSTREAM, 28,
                                                                        stream=s), n * L + 2 * n, s, chk)
+        del snap
         del a, ref, out
         torch.cuda.empty_cache()
     rng = np.random.default_rng(5)
@@ -62,18 +65,19 @@ def main():
         K.synth_var(a, d_off, d_ln, int(ln.max()), n, seed=42)
         ref = torch.empty(n, dtype=torch.int16, device="cuda")
         out = torch.empty(n, dtype=torch.int16, device="cuda")
-        ctx.batch_var_ex(K.OP_CHECKSUM, a, d_off, d_ln, n, ref, K.KERNEL_SEG, 0)
+        ctx.batch_var_ex(op, a, d_off, d_ln, n, ref, K.KERNEL_SEG, 0)
+        snap = a.clone()
         lay = dict(packed=True, total_bytes=total, min_len=int(ln.min()), max_len=int(ln.max()))
 
         def chk():
-            assert torch.equal(out, ref)
+            assert torch.equal(out, ref) and torch.equal(a, snap)
         lab = "/".join(str(p + 32) for p in pay)
-        report(f"packed var {lab} auto", lambda: ctx.batch_var(K.OP_CHECKSUM, a, d_off, d_ln, n, out, stream=s, **lay),
+        report(f"packed var {lab} auto", lambda: ctx.batch_var(op, a, d_off, d_ln, n, out, stream=s, **lay),
                total + 2 * n, s, chk)
-        report(f"packed var {lab} vvstream 28", lambda: ctx.batch_var_ex(K.OP_CHECKSUM, a, d_off, d_ln, n, out,
+        report(f"packed var {lab} vvstream 28", lambda: ctx.batch_var_ex(op, a, d_off, d_ln, n, out,
                                                                          K.KERNEL_VVSTREAM, 28, stream=s, **lay),
                total + 2 * n, s, chk)
-        del a, ref, out, d_off, d_ln
+        del a, ref, out, d_off, d_ln, snap
         torch.cuda.empty_cache()
 
 

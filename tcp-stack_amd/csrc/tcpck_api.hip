@@ -162,7 +162,7 @@ void free_stage(tcpck_ctx *ctx) {
 // everything else -- unordered offsets, gaps in variable layouts, RFC 1071
 // mode, variable or gapped layouts of images above 16 KiB (where one wave per
 // image already streams whole 1 KiB steps) -- seg.
-constexpr uint64_t kRunMaxLen = 16384;       // FILL of packed variable layouts: above, seg
+constexpr uint64_t kRunMaxLen = 32768;       // packed variable layouts, typical image: above, seg
 constexpr uint64_t kFixedRunMaxLen = 4096;   // packed fixed: rstream up to here; above, seg with W waves
                                              // per image where the image fills its steps (jumbo_on_seg;
                                              // C4 64 KiB: W16 91% vs rstream 85-88%, 6 KiB: W2 90.6% vs
@@ -211,10 +211,9 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
   const uint32_t num_cus = static_cast<uint32_t>(ctx->num_cus);
   if (kernel == TCPCK_KERNEL_AUTO) {
     // jumbo images in slots with small gaps (9000 B in 9216-B slots): vvstream
-    // streams the gaps as virtual images, 86 % against seg's 70 %
-    // (profiles/r01/jumbo_layout_probe.log); FILL there is unmeasured: seg
-    const bool jumbo_hull = stride > len && op != TCPCK_OP_FILL && len <= 65536 &&
-                            16 * stride <= 17 * static_cast<uint64_t>(len);
+    // streams the gaps as virtual images, 86 % against seg's 70 % (FILL 78 vs
+    // 64 %; profiles/r01/jumbo_layout_probe.log, jumbo_layout_fill_probe.log)
+    const bool jumbo_hull = stride > len && len <= 65536 && 16 * stride <= 17 * static_cast<uint64_t>(len);
     if (mode != TCPCK_MODE_REF || len < 2 ||
         (len > kFixedRunMaxLen && (stride > len ? !jumbo_hull : jumbo_on_seg(op, len))) ||
         stride > (1u << 24)) {
@@ -326,12 +325,11 @@ hipError_t run_var(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const uint6
   // add up to its span falls back to per-image sums, but that check cannot see
   // a gap that an overlap elsewhere in the run cancels
   if (kernel == TCPCK_KERNEL_AUTO) {
-    // packed jumbo batches stay on vvstream up to the reference's 64-KiB
-    // images for CHECKSUM / VERIFY (20000 B 86 % vs seg 76 %, a 9000/20000/
-    // 40000 mix 83 vs 72 %, 40000/60032 82 vs 83.5 %:
-    // profiles/r01/jumbo_layout_probe.log); FILL above 16 KiB is unmeasured: seg
-    const uint64_t run_max = op == TCPCK_OP_FILL ? kRunMaxLen : 65536;
-    if (!packed || typical > run_max || (op == TCPCK_OP_FILL && layout->min_len != 0 && layout->min_len < 30)) {
+    // packed jumbo batches stay on vvstream up to a typical image of 32 KiB
+    // (20000 B 86 % vs seg 76 %, FILL 82 vs 71 %; a 9000/20000/40000 mix 83
+    // vs 72 %, FILL 79 vs 66 %), seg above (a 40000/60032 mix: 83.5 vs 82 %,
+    // FILL 83 vs 79 %; profiles/r01/jumbo_layout_probe.log, jumbo_layout_fill_probe.log)
+    if (!packed || typical > kRunMaxLen || (op == TCPCK_OP_FILL && layout->min_len != 0 && layout->min_len < 30)) {
       kernel = TCPCK_KERNEL_SEG;
       param = kSegXcdOrder;
     } else {
