@@ -67,6 +67,7 @@ for s in ${STEPS:-tests smoke bench prof}; do
     fjumbo) step fjumbo 600 python scripts/fill_wb_probe.py --lengths 4096,4098,6144,8192,9000,12000,16384,24576,32768,49152,65536 ;;
     fjumbo3) step fjumbo3_tests 600 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -k "auto" &&
       step fjumbo3 600 python scripts/fill_wb_probe.py --ops checksum,fill --lengths 4098,5000,6144,9000,12000,16384,20000,24576,28000,40000,49152,60000,65536 ;;
+    c2fill) step c2fill 600 python scripts/c2_fill_sweep.py ;;
     c3fill) step c3fill 600 python scripts/c3_fill_sweep.py ;;
     jlay) step jlay 600 python scripts/jumbo_layout_probe.py ;;
     jlayf) step jlayf 600 python scripts/jumbo_layout_probe.py --fill ;;
