@@ -106,6 +106,10 @@ uint16_t finish_host(uint64_t total, int mode) {
   return static_cast<uint16_t>(~total);
 }
 
+// Grows the host-batch staging buffers.  New buffers are allocated into
+// temporaries and swapped in only when every allocation succeeded, so a failed
+// (ENOMEM) request leaves the context's previous buffers and sizes intact and a
+// later smaller request still runs on them.
 int ensure_stage(tcpck_ctx *ctx, uint64_t bytes, uint64_t images) {
   if (!ctx->s[0]) {
     for (int i = 0; i < 2; ++i) {
@@ -114,26 +118,44 @@ int ensure_stage(tcpck_ctx *ctx, uint64_t bytes, uint64_t images) {
     }
   }
   if (bytes > ctx->stage_bytes) {
+    if (bytes > UINT64_MAX - 16) return TCPCK_ENOMEM;
+    uint8_t *fresh[2] = {nullptr, nullptr};
+    for (int i = 0; i < 2; ++i) {
+      if (hipMalloc(&fresh[i], bytes + 16) != hipSuccess) {
+        for (int j = 0; j < 2; ++j)
+          if (fresh[j]) (void)hipFree(fresh[j]);
+        (void)hipGetLastError();  // clear the allocation error so the caller's next launch check is clean
+        return TCPCK_ENOMEM;
+      }
+    }
     for (int i = 0; i < 2; ++i) {
       if (ctx->stage[i]) (void)hipFree(ctx->stage[i]);
-      ctx->stage[i] = nullptr;
-      hipError_t e = hipMalloc(&ctx->stage[i], bytes + 16);
-      if (e != hipSuccess) return TCPCK_ENOMEM;
+      ctx->stage[i] = fresh[i];
     }
     ctx->stage_bytes = bytes;
   }
   if (images > ctx->stage_images) {
+    if (images > UINT64_MAX / 8) return TCPCK_ENOMEM;
+    void *fresh[2][3] = {{nullptr, nullptr, nullptr}, {nullptr, nullptr, nullptr}};
+    const uint64_t size[3] = {images * 2, images * 8, images * 4};
+    for (int i = 0; i < 2; ++i) {
+      for (int k = 0; k < 3; ++k) {
+        if (hipMalloc(&fresh[i][k], size[k]) != hipSuccess) {
+          for (int a = 0; a < 2; ++a)
+            for (int b = 0; b < 3; ++b)
+              if (fresh[a][b]) (void)hipFree(fresh[a][b]);
+          (void)hipGetLastError();
+          return TCPCK_ENOMEM;
+        }
+      }
+    }
     for (int i = 0; i < 2; ++i) {
       if (ctx->stage_out[i]) (void)hipFree(ctx->stage_out[i]);
       if (ctx->stage_off[i]) (void)hipFree(ctx->stage_off[i]);
       if (ctx->stage_len[i]) (void)hipFree(ctx->stage_len[i]);
-      ctx->stage_out[i] = nullptr;
-      ctx->stage_off[i] = nullptr;
-      ctx->stage_len[i] = nullptr;
-      if (hipMalloc(&ctx->stage_out[i], images * 2) != hipSuccess ||
-          hipMalloc(&ctx->stage_off[i], images * 8) != hipSuccess ||
-          hipMalloc(&ctx->stage_len[i], images * 4) != hipSuccess)
-        return TCPCK_ENOMEM;
+      ctx->stage_out[i] = static_cast<uint8_t *>(fresh[i][0]);
+      ctx->stage_off[i] = static_cast<uint64_t *>(fresh[i][1]);
+      ctx->stage_len[i] = static_cast<uint32_t *>(fresh[i][2]);
     }
     ctx->stage_images = images;
   }
@@ -442,7 +464,9 @@ int tcpck_checksum16(const void *image, size_t len, int mode, uint16_t *out) {
 }
 
 int tcpck_fill16(void *image, size_t len, int mode, uint16_t *out) {
-  if (!image || len < 30 || (len & 1)) return TCPCK_EINVAL;
+  // validate everything before the image is touched: a rejected call leaves bytes 28-29 as they were
+  if (!image || len < 30 || (len & 1) || (mode != TCPCK_MODE_REF && mode != TCPCK_MODE_RFC1071))
+    return TCPCK_EINVAL;
   auto *b = static_cast<uint8_t *>(image);
   b[28] = 0;  // socket-manager.cc:9
   b[29] = 0;
@@ -506,6 +530,7 @@ int tcpck_batch_fixed_ex(tcpck_ctx *ctx, int op, int mode, void *d_arena, uint64
   if (!d_out && op != TCPCK_OP_FILL) return TCPCK_EINVAL;
   if (op == TCPCK_OP_FILL && len < 30) return TCPCK_EINVAL;
   if (count > 1 && stride > (UINT64_MAX - len) / (count - 1)) return TCPCK_EINVAL;
+  if (count == 1) stride = len;  // one image: its stride is never read; the run kernels assume stride >= len
   DeviceGuard g(ctx->device);
   if (g.status() != hipSuccess) return hip_status(g.status());
   return hip_status(run_fixed(ctx, op, mode, static_cast<uint8_t *>(d_arena), stride, len, count, d_out,
@@ -558,6 +583,8 @@ int tcpck_host_batch_fixed(tcpck_ctx *ctx, int op, int mode, void *h_arena, uint
   if (!h_arena || (len & 1) || (stride & 1) || (count > 1 && stride < len)) return TCPCK_EINVAL;
   if (!h_out && op != TCPCK_OP_FILL) return TCPCK_EINVAL;
   if (op == TCPCK_OP_FILL && len < 30) return TCPCK_EINVAL;
+  if (count > 1 && stride > (UINT64_MAX - len) / (count - 1)) return TCPCK_EINVAL;
+  if (count == 1) stride = len;
   std::lock_guard<std::mutex> lk(ctx->mu);
   DeviceGuard g(ctx->device);
   if (g.status() != hipSuccess) return hip_status(g.status());

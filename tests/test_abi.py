@@ -79,6 +79,17 @@ def test_host_rejects_odd_and_null(built_lib):
         tcpck.fill16(np.zeros(28, np.uint8))  # no room for the checksum field
 
 
+def test_fill_with_bad_mode_leaves_image_untouched(built_lib):
+    """a rejected fill16 must not have zeroed bytes 28-29."""
+    import tcpck
+    img = np.arange(64, dtype=np.uint8)
+    before = img.copy()
+    with pytest.raises(tcpck.TcpckError) as e:
+        tcpck.fill16(img, mode=7)
+    assert e.value.status == tcpck.EINVAL
+    np.testing.assert_array_equal(img, before)
+
+
 @pytest.mark.parametrize("mode", [0, 1])
 def test_incremental_update_matches_recompute(built_lib, oracle_c, mode):
     """Retransmit ACK rewrite (socket-internal.h:376-377) without a full pass."""

@@ -316,6 +316,80 @@ def test_host_batch_var_vs_oracle(ctx, oracle_c):
     np.testing.assert_array_equal(out, oracle_c.batch(arena, off, ln, threads=8))
 
 
+
+def test_host_batch_recovers_after_failed_stage_growth(ctx, oracle_c):
+    """a staging-buffer growth that fails with ENOMEM must
+    leave the context usable.  A 30-TiB chunk request fails inside ensure_stage
+    before the host arena is touched; the next normal-size batch must run on the
+    previous buffers and be bit-exact."""
+    import tcpck
+    rng = np.random.default_rng(310)
+    stride = length = 1492
+    count = 20000
+    arena = rng.integers(0, 256, stride * count, dtype=np.uint8)
+    out = np.zeros(count, np.uint16)
+    ctx.set_chunk_bytes(8 << 20)
+    ctx.host_batch_fixed(tcpck.OP_CHECKSUM, arena, stride, length, count, out)
+    exp = oracle_c.batch(arena, stride=stride, length=length, count=count)
+    np.testing.assert_array_equal(out, exp)
+    ctx.set_chunk_bytes(1 << 45)
+    with pytest.raises(tcpck.TcpckError) as e:
+        # 32 images per chunk at a 1-TiB stride: ~31 TiB of staging, far above HBM
+        ctx.host_batch_fixed(tcpck.OP_CHECKSUM, arena, 1 << 40, length, 64, out)
+    assert e.value.status == tcpck.ENOMEM
+    ctx.set_chunk_bytes(8 << 20)
+    out[:] = 0
+    ctx.host_batch_fixed(tcpck.OP_CHECKSUM, arena, stride, length, count, out)
+    np.testing.assert_array_equal(out, exp)
+    torch.cuda.synchronize()
+    t = torch.ones(1 << 20, device="cuda") * 2  # torch's own launch checks see no stale error
+    assert float(t.sum().item()) == 2.0 * (1 << 20)
+
+
+@pytest.mark.parametrize("length", [96, 1492, 9000])
+@pytest.mark.parametrize("op", [0, 1, 2])
+def test_single_image_any_stride(ctx, oracle_c, length, op):
+    """count == 1 with stride < len (e.g. 0) is a valid batch of
+    one image, on the device and the host path alike."""
+    import tcpck
+    from oracle import ref16 as R
+    rng = np.random.default_rng(320 + length + op)
+    img = rng.integers(0, 256, length, dtype=np.uint8)
+    if op == tcpck.OP_VERIFY:
+        R.fill_np(img)
+    exp_img = img.copy()
+    exp = R.fill_np(exp_img) if op == tcpck.OP_FILL else oracle_c.one(img)
+    want = np.uint8(exp == 0) if op == tcpck.OP_VERIFY else np.uint16(exp)
+    dt = torch.uint8 if op == tcpck.OP_VERIFY else torch.int16
+    for stride in (0, 2, length):
+        a = dev(img)
+        o = torch.zeros(1, dtype=dt, device="cuda")
+        ctx.batch_fixed(op, a, stride, length, 1, o)
+        got = host(o).view(np.uint8 if op == tcpck.OP_VERIFY else np.uint16)[0]
+        assert got == want, (stride, got, want)
+        if op == tcpck.OP_FILL:
+            np.testing.assert_array_equal(host(a), exp_img)
+        h = img.copy()
+        ho = np.zeros(1, np.uint8 if op == tcpck.OP_VERIFY else np.uint16)
+        ctx.host_batch_fixed(op, h, stride, length, 1, ho)
+        assert ho[0] == want, (stride, ho[0], want)
+        if op == tcpck.OP_FILL:
+            np.testing.assert_array_equal(h, exp_img)
+
+
+def test_host_batch_fixed_rejects_wrapping_stride(ctx):
+    """the host fixed path has the device path's overflow guard."""
+    import tcpck
+    arena = np.zeros(4096, np.uint8)
+    out = np.zeros(4, np.uint16)
+    with pytest.raises(tcpck.TcpckError) as e:
+        ctx.host_batch_fixed(tcpck.OP_CHECKSUM, arena, (1 << 63), 1492, 4, out)
+    assert e.value.status == tcpck.EINVAL
+    with pytest.raises(tcpck.TcpckError) as e:
+        ctx.batch_fixed(tcpck.OP_CHECKSUM, dev(arena), (1 << 63), 1492, 4,
+                        torch.zeros(4, dtype=torch.int16, device="cuda"))
+    assert e.value.status == tcpck.EINVAL
+
 # ---- retransmit: batched ACK rewrite + incremental update (SURVEY.md 8f rank 3) ----
 
 @pytest.mark.parametrize("mode", [0, 1])
