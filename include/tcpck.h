@@ -63,6 +63,10 @@ extern "C" {
 /* ---- layout hints (tcpck_layout.flags) ---------------------------------- */
 #define TCPCK_LAYOUT_PACKED 1u /* images are back to back in index order:
                                   offsets[k+1] == offsets[k] + lengths[k]      */
+#define TCPCK_LAYOUT_SORTED 2u /* images in index order, apart: offsets[k+1] >=
+                                  offsets[k] + lengths[k] (receive slots, rings);
+                                  a wrong SORTED hint costs speed, never
+                                  correctness                                  */
 
 /* Optional description of a variable-length batch.  Zero fields = unknown.
  * Used only to choose a kernel; a wrong hint never changes results, except

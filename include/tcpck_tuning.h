@@ -75,6 +75,15 @@ extern "C" {
                                   U8, AUTO's FILL choice up to 128 B)
                                   | (grid oversubscription << 16: 0 = by batch
                                   size, 1 = none, M = M x the resident grid)    */
+#define TCPCK_KERNEL_SSTREAM 10 /* MODE_REF, all ops: slotted layouts -- fixed
+                                   slots (stride % 16 == 0) or any offset list --
+                                   read as one compacted stream per wave (lines
+                                   wholly in a gap are never read; runs of <= 256
+                                   images for offset lists); param = variant (0:
+                                   policy, 1: 4 steps in flight, 2: 8; + 4:
+                                   default block order, else XCD-chunked)
+                                   | (grid oversubscription << 16: 0 = by batch
+                                   size, M = M x the resident grid)             */
 int tcpck_batch_fixed_ex(tcpck_ctx *ctx, int op, int mode, void *d_arena,
                          uint64_t stride, uint32_t len, uint64_t count, void *d_out,
                          int kernel, int param, tcpck_stream stream);

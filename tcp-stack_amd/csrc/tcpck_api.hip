@@ -179,8 +179,12 @@ void free_stage(tcpck_ctx *ctx) {
 //                          W waves per image (~4 KiB per wave) where the
 //                          image fills seg's steps, else rstream
 //   fixed, stride > len    small gaps vvstream (gaps streamed as virtual
-//                          images), larger gaps seg with 8 lanes per image
+//                          images), larger gaps sstream (compacted slot
+//                          stream) in slots of a multiple of 16 B, else seg
+//                          with 8 lanes per image
 //   packed variable        vvstream, every op
+//   sorted variable        (TCPCK_LAYOUT_SORTED: receive slots) sstream for
+//                          CHECKSUM / VERIFY
 // everything else -- unordered offsets, gaps in variable layouts, RFC 1071
 // mode, variable or gapped layouts of images above 16 KiB (where one wave per
 // image already streams whole 1 KiB steps) -- seg.
@@ -252,6 +256,15 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
       if (hull && (op != TCPCK_OP_FILL || len >= 30)) {
         kernel = TCPCK_KERNEL_VVSTREAM;
         param = kVvPolicy | (op == TCPCK_OP_FILL && stride <= kFillKeepMaxLen ? kVvKeep : 0);
+      } else if (tcpck::sstream_fixed_applies(stride, len) && (op != TCPCK_OP_FILL || len >= 30)) {
+        // larger gaps in slots of a multiple of 16 B: the compacted slot stream
+        // reads only the images' chunks (scripts/slot_probe.py,
+        // profiles/r02/slot_probe_ss2.log, % of the roof in image bytes, seg ->
+        // sstream): 1492 B in 2048-B slots 77.0 -> 83.2 % (FILL 57.7 -> 64.1),
+        // 96 in 256 B 39.8 -> 55.0 %, 9000 in 16 KiB 75.0 -> 81.7 %, 1492 in
+        // 4 KiB 64.9 -> 67.6 %
+        kernel = TCPCK_KERNEL_SSTREAM;
+        param = 0;
       } else {
         kernel = TCPCK_KERNEL_SEG;
         param = (tcpck::kShapeSmall + 1) | kSegXcdOrder;
@@ -310,6 +323,19 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
     a.oversub = static_cast<uint32_t>(param >> 16) & 0xFFu;
     return tcpck::launch_gstream(op, param & 0xFFFF, a, num_cus, s);
   }
+  if (kernel == TCPCK_KERNEL_SSTREAM) {  // fixed slots: stride % 16 == 0, stride >= len
+    if (count == 1) stride = (static_cast<uint64_t>(len) + 15) & ~uint64_t{15};  // one image: never read
+    if (mode != TCPCK_MODE_REF || !tcpck::sstream_fixed_applies(stride, len) || (op == TCPCK_OP_FILL && len < 30))
+      return hipErrorInvalidValue;
+    tcpck::RunArgs a{};
+    a.arena = arena;
+    a.stride = stride;
+    a.len = len;
+    a.count = count;
+    a.out = out;
+    a.oversub = static_cast<uint32_t>(param >> 16) & 0xFFu;
+    return tcpck::launch_sstream(op, param & 0xFF, true, a, num_cus, s);
+  }
   if (kernel == TCPCK_KERNEL_VVSTREAM) {  // any even length: the prefix table takes any number of ends per step
     if (mode != TCPCK_MODE_REF || len == 0 || stride > (1u << 24) || (op == TCPCK_OP_FILL && len < 30))
       return hipErrorInvalidValue;
@@ -351,7 +377,17 @@ hipError_t run_var(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const uint6
     // (20000 B 86 % vs seg 76 %, FILL 82 vs 71 %; a 9000/20000/40000 mix 83
     // vs 72 %, FILL 79 vs 66 %), seg above (a 40000/60032 mix: 83.5 vs 82 %,
     // FILL 83 vs 79 %; profiles/r01/jumbo_layout_probe.log, jumbo_layout_fill_probe.log)
-    if (!packed || typical > kRunMaxLen || (op == TCPCK_OP_FILL && layout->min_len != 0 && layout->min_len < 30)) {
+    const bool sorted = mode == TCPCK_MODE_REF && layout && (layout->flags & TCPCK_LAYOUT_SORTED);
+    if (!packed && sorted && typical <= kRunMaxLen && op != TCPCK_OP_FILL) {
+      // images in order with gaps (receive slots): the compacted slot stream
+      // (profiles/r02/slot_probe_ss2.log, seg -> sstream, CHECKSUM): a
+      // 96/608/1492 mix in 2048-B slots 58.8 -> 66.3 %, in 1536-B slots 57.4
+      // -> 68.9 %, 1492 B in 2048-B slots 73.4 -> 78.1 %; FILL stays on seg
+      // (42-56 % either way: the scattered field writes bound it)
+      kernel = TCPCK_KERNEL_SSTREAM;
+      param = 0;
+    } else if (!packed || typical > kRunMaxLen ||
+               (op == TCPCK_OP_FILL && layout->min_len != 0 && layout->min_len < 30)) {
       kernel = TCPCK_KERNEL_SEG;
       param = kSegXcdOrder;
     } else {
@@ -372,6 +408,19 @@ hipError_t run_var(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const uint6
     a.total_bytes = layout ? layout->total_bytes : 0;
     a.blocks_per_cu = static_cast<uint32_t>(param >> 8) & 0xFFu;
     return tcpck::launch_vvstream(op, param & 0xFF, false, a, static_cast<uint32_t>(ctx->num_cus), s);
+  }
+  if (kernel == TCPCK_KERNEL_SSTREAM) {  // any offset list (runs of <= 256 images)
+    if (mode != TCPCK_MODE_REF) return hipErrorInvalidValue;
+    tcpck::RunArgs a{};
+    a.arena = arena;
+    a.offsets = off;
+    a.lengths = len;
+    a.base = base;
+    a.count = count;
+    a.out = out;
+    a.oversub = static_cast<uint32_t>(param >> 16) & 0xFFu;
+    a.total_bytes = layout ? layout->total_bytes : 0;
+    return tcpck::launch_sstream(op, param & 0xFF, false, a, static_cast<uint32_t>(ctx->num_cus), s);
   }
   if (kernel != TCPCK_KERNEL_SEG) return hipErrorInvalidValue;
   SegArgs a{};
@@ -630,13 +679,14 @@ int tcpck_host_batch_var(tcpck_ctx *ctx, int op, int mode, void *h_arena, const 
   if (!h_arena || !h_offsets || !h_lengths) return TCPCK_EINVAL;
   if (!h_out && op != TCPCK_OP_FILL) return TCPCK_EINVAL;
   uint64_t max_len = 0, min_len = UINT64_MAX;
-  bool packed = true;
+  bool packed = true, sorted = true;
   for (uint64_t k = 0; k < count; ++k) {
     if ((h_offsets[k] | h_lengths[k]) & 1) return TCPCK_EINVAL;
     if (op == TCPCK_OP_FILL && h_lengths[k] < 30) return TCPCK_EINVAL;
     max_len = std::max<uint64_t>(max_len, h_lengths[k]);
     min_len = std::min<uint64_t>(min_len, h_lengths[k]);
     if (k + 1 < count && h_offsets[k] + h_lengths[k] != h_offsets[k + 1]) packed = false;
+    if (k + 1 < count && h_offsets[k] + h_lengths[k] > h_offsets[k + 1]) sorted = false;
   }
   std::lock_guard<std::mutex> lk(ctx->mu);
   DeviceGuard g(ctx->device);
@@ -653,7 +703,7 @@ int tcpck_host_batch_var(tcpck_ctx *ctx, int op, int mode, void *h_arena, const 
   tcpck_layout lay{};
   lay.min_len = static_cast<uint32_t>(std::min<uint64_t>(min_len, UINT32_MAX));
   lay.max_len = static_cast<uint32_t>(std::min<uint64_t>(max_len, UINT32_MAX));
-  lay.flags = packed ? TCPCK_LAYOUT_PACKED : 0u;
+  lay.flags = (packed ? TCPCK_LAYOUT_PACKED : 0u) | (sorted ? TCPCK_LAYOUT_SORTED : 0u);
   hipError_t e = hipSuccess;
   uint64_t c = 0;
   for (uint64_t k0 = 0; k0 < count && e == hipSuccess; ++c) {

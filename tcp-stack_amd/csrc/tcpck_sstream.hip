@@ -1,0 +1,467 @@
+// tcpck_sstream.hip -- slotted layouts: images anywhere in the arena (fixed
+// slots with large gaps, variable-length images in fixed receive slots, any
+// offset list), streamed as one COMPACTED run per wave.  CHECKSUM, VERIFY, FILL.
+//
+// Reference semantics: CalculateChecksum, include/tcp-header.h:252-263:
+// ~(sum of the image's LE u16 words mod 2^16).  The receive arena this serves
+// is the batched form of NetworkService::Run's recvfrom buffer
+// (src/network-service.cc:39,49-56) feeding ReceivePacket's verify
+// (include/socket-manager.h:182): datagrams land in fixed slots, each image
+// shorter than its slot.
+//
+// The run's images are read as one stream with the gaps left out: image i
+// (run-relative) owns n_i = chunks of 16 B from its 16-B aligned start to its
+// rounded-up end (at least 1), at compacted chunks [C_i, C_i + n_i), C the
+// prefix sum of n.  Lane l of step t loads compacted chunk q = 64 t + l from
+// the arena address of image i(q): d_i + 16 q, d_i = (16-B start of image i) -
+// 16 C_i.  In compacted byte coordinates image i is [16 C_i + h_i, + len_i)
+// (h_i its offset inside its first chunk), and the bytes between two images
+// (the rest of the previous image's last chunk, the start of this one's
+// first chunk) form a virtual gap image.  So the compacted run is a packed
+// sequence of 2 n virtual images -- gap i ending at 16 C_i + h_i, image i at
+// + len_i -- and every image sum is a prefix difference P(end) - P(start),
+// resolved per step from an LDS prefix table exactly as tcpck_vvstream.hip's
+// gapped mode does; only the odd (image) differences are stored.  Lines that
+// lie wholly in a gap are never read.
+//
+//   * fixed slots (stride % 16 == 0): n and h are the same for every image,
+//     i(q) = q / n by a multiply-high with a launcher-computed magic number,
+//     the ends are arithmetic -- no descriptors at all;
+//   * variable (offsets + lengths): runs of <= 256 images, so every descriptor
+//     of the run is read once, 4 per lane, before the stream: C and d per
+//     image and the 2 n virtual ends go to per-wave LDS tables.  The step's
+//     chunk -> image map: the images that start inside the step post a flag at
+//     their first chunk, and lane l's image is the run's current image + the
+//     number of flags at or below l (ballot + mbcnt) -- one LDS write, one
+//     read and a table lookup per step, done when the step's loads are issued
+//     (U steps ahead of its sums);
+//   * images need not be in order or apart: an image that starts before the
+//     run's first image, or a run whose compacted bytes or buffer range pass
+//     2^31, is recomputed image by image (exact, slow);
+//   * kFill zeroes each field (compacted 16 C_i + h_i + 28) in the stream and
+//     stores the result at the image's arena address (d_i + 16 C_i + h_i +
+//     28); images < 30 B send the run to the per-image pass, which skips
+//     them (the C ABI rejects them).
+#include <algorithm>
+#include <type_traits>
+
+#include "tcpck_device.h"
+#include "tcpck_internal.h"
+
+namespace tcpck {
+
+namespace {
+
+using dev::kBlock;
+using dev::kWavesPerBlock;
+using dev::u32x4;
+
+constexpr uint32_t kMaxRun = 256;             // images per run, variable layouts
+constexpr uint32_t kEnds = 2 * kMaxRun + 64;  // virtual ends (gap, image) + 64 read past the run
+
+struct SSArgs {
+  uint8_t *arena;
+  const uint64_t *offsets;  // variable layouts
+  const uint32_t *lengths;
+  uint64_t base;
+  uint64_t count;
+  void *out;                // u16 (CHECKSUM, FILL; may be null for FILL) or u8 (VERIFY)
+  uint64_t per_wave, rem;   // equal-count split: count = per_wave * waves + rem
+  uint32_t stride;          // fixed slots: image k at k * stride, stride % 16 == 0
+  uint32_t len;
+  uint32_t nchunk;          // fixed: 16-B chunks per image (the same for all: stride % 16 == 0)
+  uint32_t lead;            // fixed: offset of every image inside its first chunk
+  uint32_t magic, shift;    // fixed: q / nchunk == mulhi(q, magic) >> shift (magic 0: q >> shift)
+  uint32_t order;           // block order (dev::ordered_block)
+};
+
+__device__ __forceinline__ u32x4 zero_word(u32x4 w, uint32_t wi) {
+  const uint32_t keep = (wi & 1u) ? 0x0000FFFFu : 0xFFFF0000u;
+  const uint32_t di = wi >> 1;
+  w.x &= di == 0 ? keep : 0xFFFFFFFFu;
+  w.y &= di == 1 ? keep : 0xFFFFFFFFu;
+  w.z &= di == 2 ? keep : 0xFFFFFFFFu;
+  w.w &= di == 3 ? keep : 0xFFFFFFFFu;
+  return w;
+}
+
+__device__ __forceinline__ uint32_t wave_max(uint32_t x) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) x = max(x, static_cast<uint32_t>(__shfl_xor(static_cast<int>(x), m, 64)));
+  return x;
+}
+
+template <int U, int OP, bool FIXED>
+__global__ void __launch_bounds__(kBlock) sstream_kernel(SSArgs a) {
+  __shared__ uint32_t s_end[kWavesPerBlock][FIXED ? 1 : kEnds];         // virtual ends, compacted bytes
+  __shared__ uint32_t s_c[kWavesPerBlock][FIXED ? 1 : kMaxRun + 64];    // first compacted chunk, ~0 past the run
+  __shared__ uint32_t s_d[kWavesPerBlock][FIXED ? 1 : kMaxRun];         // chunk q of image i at d_i + 16 q
+  __shared__ uint32_t s_flag[kWavesPerBlock][FIXED ? 1 : 64];           // images starting at chunk q0 + l
+  __shared__ __attribute__((aligned(16))) uint32_t s_pre[kWavesPerBlock][256];  // the step's prefix table
+  __shared__ uint32_t s_fld[kWavesPerBlock][OP == kFill ? 64 : 1];      // kFill: field word + 1 per chunk
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wv = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6)));
+  const uint32_t bid = dev::ordered_block(blockIdx.x, gridDim.x, a.order);
+  const uint64_t wid = static_cast<uint64_t>(bid) * kWavesPerBlock + wv;
+  uint64_t kb, ke;
+  dev::count_split(wid, a.per_wave, a.rem, kb, ke);
+  if (kb >= ke) return;
+  const uint32_t nimg = static_cast<uint32_t>(ke - kb);
+  uint8_t *const arena = a.arena;
+
+  auto store = [&](uint64_t k, uint32_t sum, uint64_t start) {
+    const uint16_t c = static_cast<uint16_t>(~sum);  // tcp-header.h:262
+    if constexpr (OP == kVerify) {
+      static_cast<uint8_t *>(a.out)[k] = (c == 0) ? 1 : 0;
+    } else {
+      if (a.out) static_cast<uint16_t *>(a.out)[k] = c;
+      if (OP == kFill) *reinterpret_cast<uint16_t *>(arena + start + 28) = c;  // raw, as the reference
+    }
+  };
+
+  // ---- the run's base, its compacted size and the descriptor tables --------
+  bool bad = false;
+  uint64_t B;        // run base (relative to arena; arena + B is 16-B aligned)
+  uint32_t T = 0;    // compacted chunks of the run
+  uint32_t R = 0;    // buffer range from B (bytes, whole chunks)
+  bool al4;          // every virtual end 4-B aligned: u32 prefix table
+  const uint32_t S = a.stride;
+  const uint32_t L = FIXED ? a.len : 0u;
+  const uint32_t n16 = FIXED ? a.nchunk << 4 : 0u;  // fixed: compacted bytes per image
+  const uint32_t h = FIXED ? a.lead : 0u;
+  if constexpr (FIXED) {
+    B = dev::align16_rel(arena, kb * S);
+    T = nimg * a.nchunk;  // the launcher keeps runs below 2^27 chunks and 2^31 bytes
+    R = ((nimg - 1) * S + h + L + 15) & ~15u;
+    al4 = ((h | L) & 3u) == 0;
+    if (OP == kFill) bad = L < 30;
+  } else {
+    uint64_t o[4];
+    uint32_t l[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {  // image 4 lane + i
+      const uint32_t j = 4 * lane + i;
+      o[i] = j < nimg ? a.offsets[kb + j] - a.base : 0;
+      l[i] = j < nimg ? a.lengths[kb + j] : 0u;
+    }
+    B = dev::align16_rel(arena, dev::read_lane64(o[0], 0));
+    uint32_t n[4], hh[4], r16[4], hi = 0;
+    bool ok = true, odd = false, shrt = false;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t j = 4 * lane + i;
+      const uint64_t r = o[i] - B;  // from the run base; an image before it wraps high
+      const bool in = j < nimg;
+      ok = ok && (!in || (r < (uint64_t{1} << 30) && l[i] <= (1u << 23)));
+      const uint32_t rr = static_cast<uint32_t>(r);
+      hh[i] = in ? rr & 15u : 0u;
+      r16[i] = rr & ~15u;
+      n[i] = in ? max((hh[i] + l[i] + 15u) >> 4, 1u) : 0u;
+      hi = in ? max(hi, rr + l[i]) : hi;
+      odd = odd || (in && ((hh[i] | l[i]) & 3u) != 0);
+      shrt = shrt || (in && l[i] < 30);
+    }
+    bad = __ballot(!ok) != 0;
+    al4 = __ballot(odd) == 0;
+    if (OP == kFill) bad = bad || __ballot(shrt) != 0;
+    const uint32_t e1 = n[0], e2 = e1 + n[1], e3 = e2 + n[2], e4 = e3 + n[3];
+    const uint32_t incl = dev::wave_inclusive_scan(e4);  // <= 256 x (2^19 + 1): no wrap
+    const uint32_t ex = incl - e4;
+    T = dev::read_lane(incl, 63);
+    R = (wave_max(hi) + 15u) & ~15u;
+    bad = bad || T >= (1u << 27);
+    const uint32_t c[4] = {ex, ex + e1, ex + e2, ex + e3};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t j = 4 * lane + i;
+      const bool in = j < nimg;
+      const uint32_t eg = 16u * c[i] + hh[i];
+      s_c[wv][j] = in ? c[i] : ~0u;
+      s_d[wv][j] = r16[i] - 16u * c[i];  // u32 wrap: d_i + 16 q lands in image i for its chunks
+      s_end[wv][2 * j] = in ? eg : ~0u;
+      s_end[wv][2 * j + 1] = in ? eg + l[i] : ~0u;
+    }
+    s_c[wv][kMaxRun + lane] = ~0u;
+    s_end[wv][2 * kMaxRun + lane] = ~0u;
+    s_flag[wv][lane] = 0u;
+    __builtin_amdgcn_wave_barrier();
+  }
+
+  if (!bad) {
+    const uint32_t span = T << 4;  // compacted bytes; every end <= span
+    const uint32_t nsteps = (T + 63) >> 6;
+    const uint32_t nv = 2 * nimg;
+    const auto rsrc = dev::make_rsrc(arena + B, R);
+    const uint16_t *pre16 = reinterpret_cast<const uint16_t *>(s_pre[wv]);
+    u32x4 *pre4 = reinterpret_cast<u32x4 *>(s_pre[wv]);
+    uint32_t *fld = s_fld[wv];
+    if constexpr (OP == kFill) {
+      fld[lane] = 0;
+      __builtin_amdgcn_wave_barrier();
+    }
+
+    // chunk -> arena offset (from B) of the lane's chunk of step t; steps are
+    // mapped in order, U ahead of their sums
+    uint32_t il = 0;  // variable: the image holding the first chunk of the next step mapped
+    auto map_step = [&](uint32_t t) -> uint32_t {
+      const uint32_t q0 = t << 6;
+      const uint32_t q = q0 + lane;
+      if constexpr (FIXED) {
+        const uint32_t i = a.magic ? (__umulhi(q, a.magic) >> a.shift) : (q >> a.shift);
+        return i * S + ((q - i * a.nchunk) << 4);
+      } else {
+        const uint32_t cj = s_c[wv][il + lane];  // image il + lane starts at chunk cj
+        const uint32_t p = cj - q0;              // il itself may start before q0: wraps high
+        if (p < 64u) s_flag[wv][p] = 1u;
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t f = s_flag[wv][lane];
+        s_flag[wv][lane] = 0u;
+        const uint64_t M = __ballot(f != 0u);
+        const uint32_t below = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(M >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(M), 0u));
+        // flags at or below l, less il's own flag when il starts at q0
+        const uint32_t idx = il + below + f - static_cast<uint32_t>(M & 1u);
+        const uint32_t d = s_d[wv][idx];
+        // the image holding chunk q0 + 64: one that starts there, else lane 63's
+        const uint64_t b64 = __ballot(p == 64u);
+        const uint32_t i63 = dev::read_lane(idx, 63);
+        if (b64) {
+          il += static_cast<uint32_t>(__builtin_ctzll(b64));
+        } else if (i63 - il == 63u) {
+          il = s_c[wv][il + 64] == q0 + 64 ? il + 64 : i63;
+        } else {
+          il = i63;
+        }
+        return d + (q << 4);
+      }
+    };
+    auto load_step = [&](uint32_t t) -> u32x4 { return dev::load16_buf_nt(rsrc, map_step(t), 0); };
+    // arena offset (from B) of image i's checksum field
+    auto field_at = [&](uint32_t i, uint32_t start) -> uint32_t {
+      if constexpr (FIXED)
+        return i * S + h + 28;
+      else
+        return s_d[wv][i] + start + 28;  // start = 16 C_i + h_i
+    };
+    // virtual end v (0 .. 2 nimg - 1), compacted bytes
+    auto end_of = [&](uint32_t v) -> uint32_t {
+      if constexpr (FIXED)
+        return h + (v >> 1) * n16 + (v & 1u) * L;
+      else
+        return s_end[wv][v];
+    };
+    auto ends_at = [&](uint32_t jn0) -> uint32_t {  // end of virtual jn0 + lane, ~0 past the run
+      if constexpr (FIXED) {
+        const uint32_t v = jn0 + lane;
+        return v < nv ? end_of(v) : ~0u;
+      } else {
+        return s_end[wv][jn0 + lane];  // jn0 <= 2 nimg: inside the table
+      }
+    };
+
+    u32x4 ring[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) ring[u] = load_step(static_cast<uint32_t>(u));
+
+    uint32_t carry = 0, p_last = 0, jn = 0, fj = 0;
+    uint32_t e_last = 0;  // end of virtual jn - 1 (the stream start for jn = 0)
+    auto stream_run = [&](auto al4_tag) {
+      constexpr bool AL4 = decltype(al4_tag)::value;
+      for (uint32_t g = 0; g < nsteps; g += U) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const uint32_t st = g + u;
+          const uint32_t sb = st << 10;
+          u32x4 w = ring[u];
+          if (sb + 1024 > span && sb + (lane << 4) >= span) w = u32x4{0u, 0u, 0u, 0u};  // past the run
+          const uint32_t j = jn + lane;
+          uint32_t e = ends_at(jn);
+          if constexpr (OP == kFill) {  // zero the checksum fields that lie in this step
+            const uint32_t i = fj + lane;
+            const uint32_t f = i < nimg ? end_of(2 * i) + 28 : ~0u;
+            const bool inf = f < sb + 1024;
+            const uint64_t bf = __ballot(inf);
+            if (bf) {
+              if (inf) fld[(f - sb) >> 4] = ((f & 15u) >> 1) + 1u;  // post the word to the chunk's lane
+              __builtin_amdgcn_wave_barrier();
+              const uint32_t qf = fld[lane];
+              if (qf) {
+                fld[lane] = 0u;
+                w = zero_word(w, qf - 1u);
+              }
+              __builtin_amdgcn_wave_barrier();
+              fj += static_cast<uint32_t>(__popcll(bf));
+            }
+          }
+          const uint32_t q1 = dev::dot2_u16(w.x, 0u);
+          const uint32_t q2 = dev::dot2_u16(w.y, q1);
+          const uint32_t q3 = dev::dot2_u16(w.z, q2);
+          const uint32_t tot = dev::dot2_u16(w.w, q3);
+          const uint32_t incl = dev::wave_inclusive_scan(tot);
+          bool table = false;
+          uint32_t jj = j;
+          for (;;) {  // once per step unless it holds more than 64 ends
+            const bool inb = e < sb + 1024;
+            const uint64_t bal = __ballot(inb);
+            if (!bal) break;
+            if (!table) {
+              const uint32_t p0 = carry + incl - tot;
+              const uint32_t b1 = p0 + q1, b2 = p0 + q2, b3 = p0 + q3;
+              if constexpr (AL4)
+                pre4[lane] = u32x4{p0, b1, b2, b3};
+              else
+                pre4[lane] = u32x4{__builtin_amdgcn_perm(p0 + w.x, p0, 0x05040100u),
+                                   __builtin_amdgcn_perm(b1 + w.y, b1, 0x05040100u),
+                                   __builtin_amdgcn_perm(b2 + w.z, b2, 0x05040100u),
+                                   __builtin_amdgcn_perm(b3 + w.w, b3, 0x05040100u)};
+              __builtin_amdgcn_wave_barrier();
+              table = true;
+            }
+            const uint32_t cnt = static_cast<uint32_t>(__popcll(bal));  // lanes 0..cnt-1 (ends ascend)
+            const uint32_t off = min(e - sb, 1022u);
+            const uint32_t P = AL4 ? s_pre[wv][off >> 2] : static_cast<uint32_t>(pre16[off >> 1]);
+            const uint32_t pprev = static_cast<uint32_t>(
+                __builtin_amdgcn_update_dpp(static_cast<int>(p_last), static_cast<int>(P), 0x138, 0xF, 0xF, false));
+            // the previous virtual end (= this image's start), read by DPP with
+            // every lane active: a DPP source lane masked off by a branch reads
+            // as the old value
+            uint32_t el = 0;
+            if constexpr (OP == kFill)
+              el = static_cast<uint32_t>(
+                  __builtin_amdgcn_update_dpp(static_cast<int>(e_last), static_cast<int>(e), 0x138, 0xF, 0xF, false));
+            if (inb && (jj & 1u)) {  // an image end (odd virtual index)
+              const uint32_t i = jj >> 1;
+              if constexpr (OP == kFill) {
+                const uint16_t cs = static_cast<uint16_t>(~(P - pprev));  // tcp-header.h:262
+                if (a.out) static_cast<uint16_t *>(a.out)[kb + i] = cs;
+                dev::store16_field(rsrc, field_at(i, lane == 0 ? e_last : el), cs);  // raw, as the reference
+              } else {
+                store(kb + i, P - pprev, 0);
+              }
+            }
+            p_last = dev::read_lane(P, cnt - 1);
+            e_last = dev::read_lane(e, cnt - 1);
+            jn += cnt;
+            if (cnt < 64) break;
+            jj = jn + lane;
+            e = ends_at(jn);
+          }
+          __builtin_amdgcn_wave_barrier();  // the next step rewrites the table
+          carry += dev::read_lane(incl, 63);
+          ring[u] = load_step(st + U);
+        }
+      }
+    };
+    if (al4)
+      stream_run(std::true_type{});
+    else
+      stream_run(std::false_type{});
+    if (jn < nv) {  // ends exactly at the last step's end (= span): the first gets the rest
+      const uint32_t rem = nv - jn;
+      for (uint32_t i = lane; i < rem; i += 64) {
+        const uint32_t v = jn + i;
+        if (v & 1u) {
+          const uint32_t sum = i == 0 ? carry - p_last : 0u;
+          if constexpr (OP == kFill) {
+            const uint16_t cs = static_cast<uint16_t>(~sum);
+            if (a.out) static_cast<uint16_t *>(a.out)[kb + (v >> 1)] = cs;
+            dev::store16_field(rsrc, field_at(v >> 1, i == 0 ? e_last : span), cs);
+          } else {
+            store(kb + (v >> 1), sum, 0);
+          }
+        }
+      }
+    }
+  }
+  if (bad) {  // wave-uniform: a layout the compacted walk does not take -> exact per-image pass
+    for (uint64_t k = kb; k < ke; ++k) {
+      const uint64_t start = FIXED ? k * S : a.offsets[k] - a.base;
+      const uint32_t len = FIXED ? L : a.lengths[k];
+      if (OP == kFill && len < 30) continue;  // precondition of kFill (the C ABI rejects these)
+      const uint32_t sum = dev::wave_image_sum<2, kRef>(arena, start, len, OP == kFill);
+      if (lane == 0) store(k, sum, start);
+    }
+  }
+}
+
+template <int U, int OP, bool FIXED>
+hipError_t launch_one(SSArgs a, uint32_t oversub, uint64_t min_waves, uint32_t num_cus, hipStream_t stream) {
+  static const uint32_t per_cu = dev::resident_blocks_per_cu(sstream_kernel<U, OP, FIXED>);
+  const uint64_t resident = static_cast<uint64_t>(per_cu) * num_cus;
+  uint64_t blocks = resident * oversub;
+  const uint64_t need = (a.count + kWavesPerBlock - 1) / kWavesPerBlock;  // >= 1 image per wave
+  const uint64_t least = (min_waves + kWavesPerBlock - 1) / kWavesPerBlock;
+  if (blocks < least) blocks = least;
+  if (blocks > need) blocks = need;
+  if (blocks == 0) return hipSuccess;
+  if (blocks > 0xFFFFFFFFull) return hipErrorInvalidValue;
+  a.per_wave = a.count / (blocks * kWavesPerBlock);
+  a.rem = a.count % (blocks * kWavesPerBlock);
+  hipLaunchKernelGGL((sstream_kernel<U, OP, FIXED>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0, stream, a);
+  return hipGetLastError();
+}
+
+template <int U, bool FIXED>
+hipError_t dispatch(int op, const SSArgs &a, uint32_t m, uint64_t min_waves, uint32_t num_cus, hipStream_t s) {
+  switch (op) {
+    case kChecksum: return launch_one<U, kChecksum, FIXED>(a, m, min_waves, num_cus, s);
+    case kVerify: return launch_one<U, kVerify, FIXED>(a, m, min_waves, num_cus, s);
+    case kFill: return launch_one<U, kFill, FIXED>(a, m, min_waves, num_cus, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace
+
+bool sstream_fixed_applies(uint64_t stride, uint32_t len) {
+  return stride >= len && len >= 2 && (stride & 15u) == 0 && stride <= (1u << 24);
+}
+
+hipError_t launch_sstream(int op, int variant, bool fixed, const RunArgs &r, uint32_t num_cus, hipStream_t stream) {
+  if (r.count == 0) return hipSuccess;
+  SSArgs a{};
+  a.arena = r.arena;
+  a.offsets = r.offsets;
+  a.lengths = r.lengths;
+  a.base = r.base;
+  a.count = r.count;
+  a.out = r.out;
+  a.order = (variant & 4) ? dev::kOrderDefault : 4u;  // groups of 16 blocks per XCD
+  uint64_t bytes = r.total_bytes;
+  uint64_t min_waves = (r.count + kMaxRun - 1) / kMaxRun;  // variable: <= 256 images per run
+  if (fixed) {
+    if (!sstream_fixed_applies(r.stride, r.len)) return hipErrorInvalidValue;
+    a.stride = static_cast<uint32_t>(r.stride);
+    a.len = r.len;
+    a.lead = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(r.arena) & 15u);  // the same for every image
+    a.nchunk = (a.lead + r.len + 15) >> 4;
+    uint32_t sh = 0;
+    while ((2u << sh) <= a.nchunk) ++sh;  // floor(log2 nchunk)
+    a.shift = sh;
+    a.magic = (a.nchunk & (a.nchunk - 1)) == 0
+                  ? 0u
+                  : static_cast<uint32_t>(((uint64_t{1} << (32 + sh)) + a.nchunk - 1) / a.nchunk);
+    bytes = r.count * r.len;
+    // runs below 2^31 arena bytes and 2^27 compacted chunks (u32 run arithmetic)
+    const uint64_t per = std::min<uint64_t>((uint64_t{1} << 30) / r.stride, (uint64_t{1} << 26) / a.nchunk);
+    min_waves = (r.count + per - 1) / std::max<uint64_t>(per, 1);
+  }
+  if (bytes == 0) bytes = r.count * 1024;
+  // grid: M x the resident grid, M a power of two (scripts/ss_sweep.py,
+  // profiles/r02/ss_sweep1.log).  Offset lists pay a descriptor round trip
+  // before a run's first data load, so their runs stay long -- >= 16 KiB of
+  // image bytes, U4: 1492-B images in 2048-B slots 80.3 % at M = 8 against
+  // 58.9 % at M = 32, a 96/608/1492 mix 67-68 % at M = 4-8 against 36 % --
+  // while fixed slots keep rstream's runs of >= 4 KiB and U8 from M = 32
+  // (85.4-85.8 %).
+  const uint32_t m = dev::oversub_for(r.oversub, bytes, static_cast<uint64_t>(num_cus) * 32, 1024,
+                                      fixed ? 4u << 10 : 16u << 10);
+  const int u = variant & 3;  // 0: policy, 1: U4, 2: U8
+  const bool u8 = u == 2 || (u == 0 && fixed && m >= 32);
+  if (fixed) return u8 ? dispatch<8, true>(op, a, m, min_waves, num_cus, stream)
+                       : dispatch<4, true>(op, a, m, min_waves, num_cus, stream);
+  return u8 ? dispatch<8, false>(op, a, m, min_waves, num_cus, stream)
+            : dispatch<4, false>(op, a, m, min_waves, num_cus, stream);
+}
+
+}  // namespace tcpck

@@ -34,6 +34,7 @@ OP_FILL = 1
 OP_VERIFY = 2
 
 LAYOUT_PACKED = 1
+LAYOUT_SORTED = 2
 
 # include/tcpck_tuning.h
 KERNEL_AUTO = 0
@@ -41,6 +42,7 @@ KERNEL_SEG = 1    # param: seg shape + 1 (1..11, SEG_SHAPES), 0 = by length
 KERNEL_RSTREAM = 5  # fixed stride == len: param = variant (10 = policy) | cap << 8 | oversub << 16
 KERNEL_VVSTREAM = 8  # packed variable or fixed (stride >= len): param = 0/1 U4/U8 byte split, 2/3 count split, 4 policy | oversub << 16
 KERNEL_GSTREAM = 9  # fixed stride == len, len a power of two in [32, 1024], 16-B aligned arena: param = 0/1/2 U4/U8/U2 (+4 default block order) | oversub << 16
+KERNEL_SSTREAM = 10  # slotted layouts (fixed slots, stride % 16 == 0, or any offset list): param = 0 policy, 1 U4, 2 U8 (+4 default block order) | oversub << 16
 SEG_SHAPES = {1: "G8/U2", 2: "G16/U6", 3: "G64/U4", 4: "G64/U2", 5: "G32/U3", 6: "G4/U8", 7: "W4/U4", 8: "W8/U4", 9: "W16/U2", 10: "W16/U4", 11: "W2/U4"}
 TUNING_EXPORTS = ("tcpck_batch_fixed_ex", "tcpck_batch_var_ex", "tcpck_ctx_set_debug", "tcpck_diag_stream")
 
@@ -229,8 +231,9 @@ class Context:
 
     def batch_var(self, op: int, arena, offsets, lengths, count: int, out, mode: int = MODE_REF,
                   total_bytes: int = 0, min_len: int = 0, max_len: int = 0, packed: bool = False,
-                  stream=None) -> None:
-        lay = Layout(total_bytes, min_len, max_len, LAYOUT_PACKED if packed else 0, 0)
+                  sorted: bool = False, stream=None) -> None:
+        lay = Layout(total_bytes, min_len, max_len,
+                     (LAYOUT_PACKED if packed else 0) | (LAYOUT_SORTED if sorted else 0), 0)
         _check(lib().tcpck_batch_var(self._h, op, mode, _ptr(arena), _ptr(offsets), _ptr(lengths),
                                      count, _ptr(out), ctypes.byref(lay), _stream(stream)),
                "tcpck_batch_var")
@@ -251,8 +254,9 @@ class Context:
 
     def batch_var_ex(self, op: int, arena, offsets, lengths, count: int, out, kernel: int,
                      param: int = 0, mode: int = MODE_REF, total_bytes: int = 0, min_len: int = 0,
-                     max_len: int = 0, packed: bool = False, stream=None) -> None:
-        lay = Layout(total_bytes, min_len, max_len, LAYOUT_PACKED if packed else 0, 0)
+                     max_len: int = 0, packed: bool = False, sorted: bool = False, stream=None) -> None:
+        lay = Layout(total_bytes, min_len, max_len,
+                     (LAYOUT_PACKED if packed else 0) | (LAYOUT_SORTED if sorted else 0), 0)
         _check(lib().tcpck_batch_var_ex(self._h, op, mode, _ptr(arena), _ptr(offsets), _ptr(lengths),
                                         count, _ptr(out), ctypes.byref(lay), kernel, param,
                                         _stream(stream)), "tcpck_batch_var_ex")

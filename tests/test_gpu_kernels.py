@@ -35,12 +35,14 @@ def host(t):
 
 def var_kernels():
     import tcpck
-    return [(tcpck.KERNEL_SEG, p) for p in SEG] + [(tcpck.KERNEL_VVSTREAM, v) for v in VVSTREAM]
+    return ([(tcpck.KERNEL_SEG, p) for p in SEG] + [(tcpck.KERNEL_VVSTREAM, v) for v in VVSTREAM] +
+            [(tcpck.KERNEL_SSTREAM, v) for v in (0, 1, 2)])
 
 
-def fixed_kernels():
+def fixed_kernels():  # sstream's fixed mode takes slots of a multiple of 16 B only (tests/test_gpu_sstream.py)
     import tcpck
-    return var_kernels() + [(tcpck.KERNEL_RSTREAM, v) for v in RSTREAM]
+    return ([(k, p) for k, p in var_kernels() if k != tcpck.KERNEL_SSTREAM] +
+            [(tcpck.KERNEL_RSTREAM, v) for v in RSTREAM])
 
 
 def packed_layout(count, seed, payloads, header=32):

@@ -316,6 +316,30 @@ def test_host_batch_var_vs_oracle(ctx, oracle_c):
     np.testing.assert_array_equal(out, oracle_c.batch(arena, off, ln, threads=8))
 
 
+@pytest.mark.parametrize("op", [0, 1, 2])
+def test_host_batch_var_slots_vs_oracle(ctx, oracle_c, op):
+    """Host receive arena in 2048-B slots (recv_burst's layout): the host sees the
+    offsets ascend and passes TCPCK_LAYOUT_SORTED, so the chunks run on sstream."""
+    import tcpck
+    from oracle import ref16 as R
+    rng = np.random.default_rng(401 + op)
+    count = 60000
+    ln = np.asarray((96, 608, 1492), np.uint32)[rng.integers(0, 3, count)]
+    off = np.arange(count, dtype=np.uint64) * 2048 + 2
+    arena = rng.integers(0, 256, count * 2048 + 16, dtype=np.uint8)
+    before = arena.copy()
+    out = np.zeros(count, np.uint16 if op != 2 else np.uint8)
+    ctx.set_chunk_bytes(16 << 20)
+    ctx.host_batch_var(op, arena, off, ln, count, out)
+    if op == 1:
+        exp = np.array([R.fill_np(before[int(off[k]):int(off[k]) + int(ln[k])]) for k in range(count)], np.uint16)
+        np.testing.assert_array_equal(out, exp)
+        np.testing.assert_array_equal(arena, before)  # fill_np patched `before` in place, as the reference
+    else:
+        exp = oracle_c.batch(arena, off, ln, threads=8)
+        np.testing.assert_array_equal(out, exp if op == 0 else (exp == 0).astype(np.uint8))
+
+
 
 def test_host_batch_recovers_after_failed_stage_growth(ctx, oracle_c):
     """a staging-buffer growth that fails with ENOMEM must
@@ -564,3 +588,67 @@ def test_auto_policy_jumbo_var(ctx, oracle_c, typical):
         ctx.batch_var(tcpck.OP_CHECKSUM, dev(arena_np), dev(off), dev(ln), count, out,
                       total_bytes=int(ln.sum()), packed=not gaps)
         np.testing.assert_array_equal(host(out).view(np.uint16), oracle_c.batch(arena_np, off, ln, threads=8))
+
+
+@pytest.mark.parametrize("length,stride", [(1492, 2048), (1024, 2048), (96, 256), (1492, 4096), (30, 64),
+                                           (9000, 16384), (1494, 2048), (1492, 2000)])
+@pytest.mark.parametrize("mis", [0, 6])
+def test_auto_policy_fixed_slots(ctx, oracle_c, length, stride, mis):
+    """Slots with larger gaps: sstream where the slot is a multiple of 16 B, else
+    seg.  CHECKSUM, FILL (results, fields, untouched gaps), VERIFY."""
+    import tcpck
+    from oracle import ref16 as R
+    rng = np.random.default_rng(length + stride + mis)
+    count = max(8, min(20000, (48 << 20) // stride))
+    arena_np = rng.integers(0, 256, count * stride + 16, dtype=np.uint8)
+    buf = dev(arena_np)
+    ptr = buf.data_ptr() + mis
+    view = arena_np[mis:]
+    out = torch.empty(count, dtype=torch.int16, device="cuda")
+    ctx.batch_fixed(tcpck.OP_CHECKSUM, ptr, stride, length, count, out)
+    np.testing.assert_array_equal(host(out).view(np.uint16),
+                                  oracle_c.batch(view, stride=stride, length=length, count=count, threads=8))
+    ctx.batch_fixed(tcpck.OP_FILL, ptr, stride, length, count, out)
+    exp_arena = view.copy()
+    exp = np.array([R.fill_np(exp_arena[k * stride:k * stride + length]) for k in range(count)], np.uint16)
+    np.testing.assert_array_equal(host(out).view(np.uint16), exp)
+    np.testing.assert_array_equal(host(buf)[mis:], exp_arena)
+    ok = torch.empty(count, dtype=torch.uint8, device="cuda")
+    ctx.batch_fixed(tcpck.OP_VERIFY, ptr, stride, length, count, ok)
+    assert bool(host(ok).all())
+
+
+@pytest.mark.parametrize("slot,mix", [(2048, (96, 608, 1492)), (1536, (32, 1492)), (2050, (34, 606, 1494)),
+                                      (65600, (40, 65536))])
+@pytest.mark.parametrize("hint", ["sorted", "none", "sorted_wrong"])
+def test_auto_policy_var_slots(ctx, oracle_c, slot, mix, hint):
+    """Variable images in receive slots: with TCPCK_LAYOUT_SORTED AUTO takes
+    sstream for CHECKSUM/VERIFY (seg without the hint, and for FILL); a wrong
+    SORTED hint (shuffled offsets) costs speed, never correctness."""
+    import tcpck
+    from oracle import ref16 as R
+    rng = np.random.default_rng(slot + len(mix) + len(hint))
+    count = max(8, min(30000, (64 << 20) // slot))
+    ln = np.asarray(mix, np.uint32)[rng.integers(0, len(mix), count)]
+    off = np.arange(count, dtype=np.uint64) * np.uint64(slot)
+    if hint == "sorted_wrong":
+        perm = rng.permutation(count)
+        off, ln = off[perm].copy(), ln[perm].copy()
+    arena_np = rng.integers(0, 256, count * slot + 16, dtype=np.uint8)
+    arena = dev(arena_np)
+    d_off, d_ln = dev(off), dev(ln)
+    kw = dict(total_bytes=int(ln.sum()), min_len=int(ln.min()), max_len=int(ln.max()), sorted=hint != "none")
+    out = torch.empty(count, dtype=torch.int16, device="cuda")
+    ctx.batch_var(tcpck.OP_CHECKSUM, arena, d_off, d_ln, count, out, **kw)
+    exp = oracle_c.batch(arena_np, off, ln, threads=8)
+    np.testing.assert_array_equal(host(out).view(np.uint16), exp)
+    ok = torch.empty(count, dtype=torch.uint8, device="cuda")
+    ctx.batch_var(tcpck.OP_VERIFY, arena, d_off, d_ln, count, ok, **kw)
+    np.testing.assert_array_equal(host(ok), (exp == 0).astype(np.uint8))
+    ctx.batch_var(tcpck.OP_FILL, arena, d_off, d_ln, count, out, **kw)
+    exp_arena = arena_np.copy()
+    expf = np.array([R.fill_np(exp_arena[int(off[k]):int(off[k]) + int(ln[k])]) for k in range(count)], np.uint16)
+    np.testing.assert_array_equal(host(out).view(np.uint16), expf)
+    np.testing.assert_array_equal(host(arena), exp_arena)
+    ctx.batch_var(tcpck.OP_VERIFY, arena, d_off, d_ln, count, ok, **kw)
+    assert bool(host(ok).all())
