@@ -80,8 +80,10 @@ extern "C" {
                                    read as one compacted stream per wave (lines
                                    wholly in a gap are never read; runs of <= 256
                                    images for offset lists); param = variant (0:
-                                   policy, 1: 4 steps in flight, 2: 8; + 4:
-                                   default block order, else XCD-chunked)
+                                   policy = 4 steps in flight, scattered block
+                                   order; 1: 4 steps in flight, 2: 8; + 4:
+                                   default block order, + 8: scattered, else
+                                   XCD-chunked)
                                    | (grid oversubscription << 16: 0 = by batch
                                    size, M = M x the resident grid)             */
 int tcpck_batch_fixed_ex(tcpck_ctx *ctx, int op, int mode, void *d_arena,

@@ -33,7 +33,8 @@ def main():
         n = (1 << 31) // S
         ln = np.asarray(mix, np.uint32)[rng.integers(0, len(mix), n)]
         cases.append((f"var {'/'.join(map(str, mix))} in {S}", S, None, n, np.arange(n, dtype=np.uint64) * np.uint64(S), ln))
-    cases.append(("fixed 1492 in 2048", 2048, 1492, (1 << 31) // 2048, None, None))
+    for S, L in ((2048, 1492), (4096, 1492), (256, 96), (16384, 9000), (2048, 1024)):
+        cases.append((f"fixed {L} in {S}", S, L, (1 << 31) // S, None, None))
     ops = {"checksum": K.OP_CHECKSUM, "fill": K.OP_FILL, "verify": K.OP_VERIFY}
     for name, S, L, n, off, ln in cases:
         arena = torch.empty(n * S, dtype=torch.uint8, device="cuda")

@@ -240,8 +240,13 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
     // streams the gaps as virtual images, 86 % against seg's 70 % (FILL 78 vs
     // 64 %; profiles/r01/jumbo_layout_probe.log, jumbo_layout_fill_probe.log)
     const bool jumbo_hull = stride > len && len <= 65536 && 16 * stride <= 17 * static_cast<uint64_t>(len);
+    // jumbo images in slots with larger gaps: the compacted slot stream where
+    // the slot is a multiple of 16 B (9000 B in 16-KiB slots 74.2 -> 85.0 %,
+    // FILL 65.6 -> 79.0 %, profiles/r02/slot_probe_ss3.log), else seg
+    const bool jumbo_slots = stride > len && !jumbo_hull && tcpck::sstream_fixed_applies(stride, len) &&
+                             (op != TCPCK_OP_FILL || len >= 30);
     if (mode != TCPCK_MODE_REF || len < 2 ||
-        (len > kFixedRunMaxLen && (stride > len ? !jumbo_hull : jumbo_on_seg(op, len))) ||
+        (len > kFixedRunMaxLen && !jumbo_slots && (stride > len ? !jumbo_hull : jumbo_on_seg(op, len))) ||
         stride > (1u << 24)) {
       kernel = TCPCK_KERNEL_SEG;
       param = kSegXcdOrder;  // shape by length
@@ -253,16 +258,16 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
       // per image (1536/1492 B 81% vs 77% for the length-based shape)
       const uint64_t l = len;
       const bool hull = len < 512 ? stride <= 2 * l : (len < 1024 ? 4 * stride <= 5 * l : 16 * stride <= 17 * l);
+      // (jumbo images reach here in slots: jumbo_hull -> vvstream, jumbo_slots -> sstream)
       if (hull && (op != TCPCK_OP_FILL || len >= 30)) {
         kernel = TCPCK_KERNEL_VVSTREAM;
         param = kVvPolicy | (op == TCPCK_OP_FILL && stride <= kFillKeepMaxLen ? kVvKeep : 0);
       } else if (tcpck::sstream_fixed_applies(stride, len) && (op != TCPCK_OP_FILL || len >= 30)) {
         // larger gaps in slots of a multiple of 16 B: the compacted slot stream
         // reads only the images' chunks (scripts/slot_probe.py,
-        // profiles/r02/slot_probe_ss2.log, % of the roof in image bytes, seg ->
-        // sstream): 1492 B in 2048-B slots 77.0 -> 83.2 % (FILL 57.7 -> 64.1),
-        // 96 in 256 B 39.8 -> 55.0 %, 9000 in 16 KiB 75.0 -> 81.7 %, 1492 in
-        // 4 KiB 64.9 -> 67.6 %
+        // profiles/r02/slot_probe_ss3.log, % of the roof in image bytes, seg ->
+        // sstream): 1492 B in 2048-B slots 77.4 -> 83.1 % (FILL 57.7 -> 60.1),
+        // in 4-KiB slots 65.7 -> 81.2 %, 96 in 256 B 39.9 -> 55.7 %
         kernel = TCPCK_KERNEL_SSTREAM;
         param = 0;
       } else {
@@ -380,10 +385,10 @@ hipError_t run_var(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const uint6
     const bool sorted = mode == TCPCK_MODE_REF && layout && (layout->flags & TCPCK_LAYOUT_SORTED);
     if (!packed && sorted && typical <= kRunMaxLen && op != TCPCK_OP_FILL) {
       // images in order with gaps (receive slots): the compacted slot stream
-      // (profiles/r02/slot_probe_ss2.log, seg -> sstream, CHECKSUM): a
-      // 96/608/1492 mix in 2048-B slots 58.8 -> 66.3 %, in 1536-B slots 57.4
-      // -> 68.9 %, 1492 B in 2048-B slots 73.4 -> 78.1 %; FILL stays on seg
-      // (42-56 % either way: the scattered field writes bound it)
+      // (profiles/r02/slot_probe_ss3.log, seg -> sstream, CHECKSUM): a
+      // 96/608/1492 mix in 2048-B slots 60.5 -> 70.3 %, in 1536-B slots 57.4
+      // -> 68.5 %, 1492 B in 2048-B slots 73.5 -> 78.3 %; FILL stays on seg
+      // (41-58 % either way: the scattered field writes bound it)
       kernel = TCPCK_KERNEL_SSTREAM;
       param = 0;
     } else if (!packed || typical > kRunMaxLen ||

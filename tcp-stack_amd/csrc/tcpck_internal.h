@@ -111,9 +111,9 @@ hipError_t launch_rstream(int op, int variant, const FixedStreamArgs &a, uint32_
 hipError_t launch_vvstream(int op, int variant, bool fixed, const RunArgs &a, uint32_t num_cus, hipStream_t stream);
 // ---- sstream (compacted slot stream), MODE_REF, all ops: images anywhere in
 // the arena -- fixed slots (fixed = true: stride % 16 == 0, stride >= len) or
-// offsets + lengths (fixed = false; runs of <= 256 images).  variant: 0 policy
-// (U8 from 32x oversubscription), 1 U4, 2 U8; + 4: default block order (else
-// XCD-chunked).  a.oversub: 0 = by size; a.total_bytes: image bytes hint.
+// offsets + lengths (fixed = false; runs of <= 128 images).  variant: 0 policy
+// (U4, scattered block order), 1 U4, 2 U8; + 4: default block order, + 8:
+// scattered (else XCD-chunked).  a.oversub: 0 = by size; a.total_bytes: image bytes hint.
 bool sstream_fixed_applies(uint64_t stride, uint32_t len);
 hipError_t launch_sstream(int op, int variant, bool fixed, const RunArgs &a, uint32_t num_cus, hipStream_t stream);
 // timing-only streaming micro-kernels (tcpck_diag.hip)

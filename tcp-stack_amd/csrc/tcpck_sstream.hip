@@ -27,8 +27,8 @@
 //   * fixed slots (stride % 16 == 0): n and h are the same for every image,
 //     i(q) = q / n by a multiply-high with a launcher-computed magic number,
 //     the ends are arithmetic -- no descriptors at all;
-//   * variable (offsets + lengths): runs of <= 256 images, so every descriptor
-//     of the run is read once, 4 per lane, before the stream: C and d per
+//   * variable (offsets + lengths): runs of <= 128 images, so every descriptor
+//     of the run is read once, 2 per lane, before the stream: C and d per
 //     image and the 2 n virtual ends go to per-wave LDS tables.  The step's
 //     chunk -> image map: the images that start inside the step post a flag at
 //     their first chunk, and lane l's image is the run's current image + the
@@ -56,7 +56,9 @@ using dev::kBlock;
 using dev::kWavesPerBlock;
 using dev::u32x4;
 
-constexpr uint32_t kMaxRun = 256;             // images per run, variable layouts
+constexpr uint32_t kMaxRun = 128;             // images per run, variable layouts
+constexpr int kPer = kMaxRun / 64;            // descriptors per lane
+constexpr uint32_t kOrderScatter = 0xFDu;     // block order: multiplicative scatter
 constexpr uint32_t kEnds = 2 * kMaxRun + 64;  // virtual ends (gap, image) + 64 read past the run
 
 struct SSArgs {
@@ -101,7 +103,11 @@ __global__ void __launch_bounds__(kBlock) sstream_kernel(SSArgs a) {
   __shared__ uint32_t s_fld[kWavesPerBlock][OP == kFill ? 64 : 1];      // kFill: field word + 1 per chunk
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wv = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6)));
-  const uint32_t bid = dev::ordered_block(blockIdx.x, gridDim.x, a.order);
+  // kOrderScatter: block b takes run group (b P) mod nb, P prime > nb -- the
+  // runs in flight at any time spread over the whole batch (tuning)
+  const uint32_t bid = a.order == kOrderScatter
+                           ? static_cast<uint32_t>((uint64_t{blockIdx.x} * 2654435761ull) % gridDim.x)
+                           : dev::ordered_block(blockIdx.x, gridDim.x, a.order);
   const uint64_t wid = static_cast<uint64_t>(bid) * kWavesPerBlock + wv;
   uint64_t kb, ke;
   dev::count_split(wid, a.per_wave, a.rem, kb, ke);
@@ -136,20 +142,20 @@ __global__ void __launch_bounds__(kBlock) sstream_kernel(SSArgs a) {
     al4 = ((h | L) & 3u) == 0;
     if (OP == kFill) bad = L < 30;
   } else {
-    uint64_t o[4];
-    uint32_t l[4];
+    uint64_t o[kPer];
+    uint32_t l[kPer];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {  // image 4 lane + i
-      const uint32_t j = 4 * lane + i;
+    for (int i = 0; i < kPer; ++i) {  // image kPer lane + i
+      const uint32_t j = kPer * lane + i;
       o[i] = j < nimg ? a.offsets[kb + j] - a.base : 0;
       l[i] = j < nimg ? a.lengths[kb + j] : 0u;
     }
     B = dev::align16_rel(arena, dev::read_lane64(o[0], 0));
-    uint32_t n[4], hh[4], r16[4], hi = 0;
+    uint32_t n[kPer], hh[kPer], r16[kPer], hi = 0;
     bool ok = true, odd = false, shrt = false;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const uint32_t j = 4 * lane + i;
+    for (int i = 0; i < kPer; ++i) {
+      const uint32_t j = kPer * lane + i;
       const uint64_t r = o[i] - B;  // from the run base; an image before it wraps high
       const bool in = j < nimg;
       ok = ok && (!in || (r < (uint64_t{1} << 30) && l[i] <= (1u << 23)));
@@ -164,20 +170,26 @@ __global__ void __launch_bounds__(kBlock) sstream_kernel(SSArgs a) {
     bad = __ballot(!ok) != 0;
     al4 = __ballot(odd) == 0;
     if (OP == kFill) bad = bad || __ballot(shrt) != 0;
-    const uint32_t e1 = n[0], e2 = e1 + n[1], e3 = e2 + n[2], e4 = e3 + n[3];
-    const uint32_t incl = dev::wave_inclusive_scan(e4);  // <= 256 x (2^19 + 1): no wrap
-    const uint32_t ex = incl - e4;
+    uint32_t c[kPer];  // exclusive prefix of n inside the lane, then across the wave
+    uint32_t lsum = 0;
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      c[i] = lsum;
+      lsum += n[i];
+    }
+    const uint32_t incl = dev::wave_inclusive_scan(lsum);  // <= 256 x (2^19 + 1): no wrap
+    const uint32_t ex = incl - lsum;
     T = dev::read_lane(incl, 63);
     R = (wave_max(hi) + 15u) & ~15u;
     bad = bad || T >= (1u << 27);
-    const uint32_t c[4] = {ex, ex + e1, ex + e2, ex + e3};
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const uint32_t j = 4 * lane + i;
+    for (int i = 0; i < kPer; ++i) {
+      const uint32_t j = kPer * lane + i;
       const bool in = j < nimg;
-      const uint32_t eg = 16u * c[i] + hh[i];
-      s_c[wv][j] = in ? c[i] : ~0u;
-      s_d[wv][j] = r16[i] - 16u * c[i];  // u32 wrap: d_i + 16 q lands in image i for its chunks
+      const uint32_t ci = ex + c[i];
+      const uint32_t eg = 16u * ci + hh[i];
+      s_c[wv][j] = in ? ci : ~0u;
+      s_d[wv][j] = r16[i] - 16u * ci;  // u32 wrap: d_i + 16 q lands in image i for its chunks
       s_end[wv][2 * j] = in ? eg : ~0u;
       s_end[wv][2 * j + 1] = in ? eg + l[i] : ~0u;
     }
@@ -426,9 +438,11 @@ hipError_t launch_sstream(int op, int variant, bool fixed, const RunArgs &r, uin
   a.base = r.base;
   a.count = r.count;
   a.out = r.out;
-  a.order = (variant & 4) ? dev::kOrderDefault : 4u;  // groups of 16 blocks per XCD
+  // + 4: default block order; + 8: scattered (the policy's); else groups of
+  // 16 blocks per XCD
+  a.order = (variant & 8) ? kOrderScatter : ((variant & 4) ? dev::kOrderDefault : 4u);
   uint64_t bytes = r.total_bytes;
-  uint64_t min_waves = (r.count + kMaxRun - 1) / kMaxRun;  // variable: <= 256 images per run
+  uint64_t min_waves = (r.count + kMaxRun - 1) / kMaxRun;  // variable: <= kMaxRun images per run
   if (fixed) {
     if (!sstream_fixed_applies(r.stride, r.len)) return hipErrorInvalidValue;
     a.stride = static_cast<uint32_t>(r.stride);
@@ -447,17 +461,24 @@ hipError_t launch_sstream(int op, int variant, bool fixed, const RunArgs &r, uin
     min_waves = (r.count + per - 1) / std::max<uint64_t>(per, 1);
   }
   if (bytes == 0) bytes = r.count * 1024;
-  // grid: M x the resident grid, M a power of two (scripts/ss_sweep.py,
-  // profiles/r02/ss_sweep1.log).  Offset lists pay a descriptor round trip
-  // before a run's first data load, so their runs stay long -- >= 16 KiB of
-  // image bytes, U4: 1492-B images in 2048-B slots 80.3 % at M = 8 against
-  // 58.9 % at M = 32, a 96/608/1492 mix 67-68 % at M = 4-8 against 36 % --
-  // while fixed slots keep rstream's runs of >= 4 KiB and U8 from M = 32
-  // (85.4-85.8 %).
+  // grid: M x the resident grid, M a power of two, blocks in the scattered
+  // order (scripts/ss_sweep.py, scripts/sparse_probe.py; profiles/r02/
+  // ss_sweep3_scatter.log, ss_sweep4_run128.log, sparse_probe2_orders.log).
+  // Sparse reads are sensitive to which addresses are in flight together: with
+  // the XCD-chunked order the same kernel ran 1492-B images in 4-KiB slots at
+  // 59-74 % and 2-KiB images in 4-KiB slots at 64-80 % depending on M, while the
+  // scattered order (the runs in flight spread over the whole batch) holds
+  // 78-88 % at every density >= 1/4 and block size tried.  Offset lists pay a
+  // descriptor round trip before a run's first data load, so their runs stay
+  // longer: >= 16 KiB of image bytes (var 96/608/1492 in 2048-B slots 72.0 %
+  // at M = 4 against 57 % at M = 16), fixed slots >= 8 KiB (1492 in 2048-B
+  // slots 83.0 %, in 4-KiB slots 82.0 %, 9000 in 16 KiB 86.4 % at M = 16).
+  // U4 throughout (U8 costs occupancy: 90 VGPRs against 58).
+  if (!(variant & 12)) a.order = kOrderScatter;
   const uint32_t m = dev::oversub_for(r.oversub, bytes, static_cast<uint64_t>(num_cus) * 32, 1024,
-                                      fixed ? 4u << 10 : 16u << 10);
+                                      fixed ? 8u << 10 : 16u << 10);
   const int u = variant & 3;  // 0: policy, 1: U4, 2: U8
-  const bool u8 = u == 2 || (u == 0 && fixed && m >= 32);
+  const bool u8 = u == 2;
   if (fixed) return u8 ? dispatch<8, true>(op, a, m, min_waves, num_cus, stream)
                        : dispatch<4, true>(op, a, m, min_waves, num_cus, stream);
   return u8 ? dispatch<8, false>(op, a, m, min_waves, num_cus, stream)

@@ -12,7 +12,7 @@ pytestmark = pytest.mark.gpu
 
 torch = pytest.importorskip("torch")
 
-VARIANTS = [0, 1, 2, 5]  # 0 policy, 1 U4, 2 U8; +4 default block order
+VARIANTS = [0, 1, 2, 5, 10]  # 0 policy, 1 U4, 2 U8; +4 default block order, +8 scattered
 
 
 @pytest.fixture(scope="module")
