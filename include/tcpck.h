@@ -141,6 +141,29 @@ int tcpck_batch_set_ack(tcpck_ctx *ctx, int mode, void *d_arena, const uint64_t 
                         uint64_t stride, uint64_t count, const uint32_t *d_acks, uint32_t ack,
                         uint16_t *d_out, tcpck_stream stream);
 
+/* ---- batched segmentation: send stream -> checksummed images -------------
+ * The data-segment send path in one device pass.  The reference, per segment:
+ * TcpSendingBuffer::GetAsTcpPacket(0, window) cuts the next <= window bytes
+ * off the send stream into a fresh packet with TcpLength = len
+ * (include/tcp-buffer.h:82-98); Estab sets ACK, seq = snd_nxt (then snd_nxt
+ * += len) and ack (src/state.cc:167-184); SetSource/SetDestination and
+ * TcpHeaderH2N (include/socket-internal.h:186-199); SendPacketsForSending
+ * zeroes and stores the checksum (include/socket-manager.h:259-260).  Here:
+ *   n = ceil(payload_bytes / seg) images, image k at d_images + k * stride:
+ *     bytes 0-31  = hdr (a 32-B network-order header: the connection's fields
+ *                   as TcpHeaderH2N leaves them) with TcpLength (10-11) =
+ *                   htons(len_k), seq (16-19) = htonl(seq0 + k * seg) and the
+ *                   checksum (28-29) of the image (raw, as the reference);
+ *     bytes 32..  = d_payload[k * seg, k * seg + len_k), len_k = seg except
+ *                   the last (the rest); the slot's bytes after the image = 0.
+ * payload_bytes even; seg a multiple of 4 in [4, 65532]; stride a multiple of
+ * 16, >= 32 + seg; d_payload 4-B and d_images 16-B aligned; hdr a host pointer
+ * (read during the call).  d_out: u16[n] checksums (may be NULL).  Both modes
+ * (RFC 1071 folds the same sums).  Asynchronous on `stream`. */
+int tcpck_batch_segment(tcpck_ctx *ctx, int mode, const void *d_payload, uint64_t payload_bytes,
+                        uint32_t seg, const void *hdr, uint32_t seq0, void *d_images, uint64_t stride,
+                        uint16_t *d_out, tcpck_stream stream);
+
 /* ---- batched, host memory (end to end incl. PCIe) ------------------------
  * Segments start and end in host memory (the loopback/socket buffers of
  * network-service.cc / tcp-buffer.h).  The batch is split into chunks that are

@@ -99,6 +99,13 @@ int tcpck_ctx_set_debug(tcpck_ctx *ctx, void *d_buf);
 int tcpck_diag_stream(tcpck_ctx *ctx, int variant, const void *d_buf, uint64_t bytes, void *d_out,
                       tcpck_stream stream);
 
+/* tcpck_batch_segment (tcpck.h) with param = variant (0: policy = 4 steps in
+ * flight, nt stores; 1: 8 in flight; 2: default-policy stores; 3: sc1 stores;
+ * + 8: default block order, else XCD-chunked) | (grid oversubscription << 16). */
+int tcpck_batch_segment_ex(tcpck_ctx *ctx, int mode, const void *d_payload, uint64_t payload_bytes,
+                           uint32_t seg, const void *hdr, uint32_t seq0, void *d_images, uint64_t stride,
+                           uint16_t *d_out, int param, tcpck_stream stream);
+
 int tcpck_batch_var_ex(tcpck_ctx *ctx, int op, int mode, void *d_arena,
                        const uint64_t *d_offsets, const uint32_t *d_lengths,
                        uint64_t count, void *d_out, const tcpck_layout *layout,

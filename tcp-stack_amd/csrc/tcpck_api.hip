@@ -629,6 +629,42 @@ int tcpck_batch_set_ack(tcpck_ctx *ctx, int mode, void *d_arena, const uint64_t 
                                           static_cast<hipStream_t>(stream)));
 }
 
+// ---- batched segmentation: send stream -> checksummed images --------------------
+int tcpck_batch_segment(tcpck_ctx *ctx, int mode, const void *d_payload, uint64_t payload_bytes, uint32_t seg,
+                        const void *hdr, uint32_t seq0, void *d_images, uint64_t stride, uint16_t *d_out,
+                        tcpck_stream stream) {
+  return tcpck_batch_segment_ex(ctx, mode, d_payload, payload_bytes, seg, hdr, seq0, d_images, stride, d_out, 0,
+                                stream);
+}
+
+int tcpck_batch_segment_ex(tcpck_ctx *ctx, int mode, const void *d_payload, uint64_t payload_bytes, uint32_t seg,
+                           const void *hdr, uint32_t seq0, void *d_images, uint64_t stride, uint16_t *d_out,
+                           int param, tcpck_stream stream) {
+  if (!ctx || (mode != TCPCK_MODE_REF && mode != TCPCK_MODE_RFC1071)) return TCPCK_EINVAL;
+  if (payload_bytes == 0) return TCPCK_OK;
+  if (!d_payload || !d_images || !hdr || (payload_bytes & 1)) return TCPCK_EINVAL;
+  if (seg < 4 || seg > 65532 || (seg & 3) || (stride & 15) || stride < 32ull + seg || stride > (1u << 24))
+    return TCPCK_EINVAL;
+  if ((reinterpret_cast<uintptr_t>(d_payload) & 3) || (reinterpret_cast<uintptr_t>(d_images) & 15))
+    return TCPCK_EINVAL;
+  const uint64_t n = (payload_bytes + seg - 1) / seg;
+  if (n > UINT64_MAX / stride) return TCPCK_EINVAL;
+  DeviceGuard g(ctx->device);
+  if (g.status() != hipSuccess) return hip_status(g.status());
+  tcpck::SegmentArgs a{};
+  a.payload = static_cast<const uint8_t *>(d_payload);
+  a.images = static_cast<uint8_t *>(d_images);
+  a.payload_bytes = payload_bytes;
+  a.count = n;
+  a.out = d_out;
+  a.seg = seg;
+  a.stride = static_cast<uint32_t>(stride);
+  std::memcpy(a.hdr, hdr, 32);
+  a.seq0 = seq0;
+  return hip_status(tcpck::launch_segment(mode, param & 0xFF, a, static_cast<uint32_t>(param >> 16) & 0xFFFFu,
+                                          static_cast<uint32_t>(ctx->num_cus), static_cast<hipStream_t>(stream)));
+}
+
 // ---- batched, host memory: chunked H2D -> kernel -> D2H on two streams ---------
 int tcpck_host_batch_fixed(tcpck_ctx *ctx, int op, int mode, void *h_arena, uint64_t stride,
                            uint32_t len, uint64_t count, void *h_out) {

@@ -116,6 +116,25 @@ hipError_t launch_vvstream(int op, int variant, bool fixed, const RunArgs &a, ui
 // scattered (else XCD-chunked).  a.oversub: 0 = by size; a.total_bytes: image bytes hint.
 bool sstream_fixed_applies(uint64_t stride, uint32_t len);
 hipError_t launch_sstream(int op, int variant, bool fixed, const RunArgs &a, uint32_t num_cus, hipStream_t stream);
+// ---- segment (tcpck_segment.hip): send stream -> checksummed images ------
+struct SegmentArgs {
+  const uint8_t *payload;    // the send stream (4-B aligned)
+  uint8_t *images;           // output: image k at k * stride (16-B aligned)
+  uint64_t payload_bytes;    // even
+  uint64_t count;            // images: ceil(payload_bytes / seg)
+  uint16_t *out;             // checksums (may be null)
+  uint64_t per_wave, rem;    // run split, set by the launcher
+  uint32_t seg;              // payload bytes per image (the last: the rest); % 4 == 0
+  uint32_t stride;           // % 16 == 0, >= 32 + seg
+  uint32_t nchunk, magic, shift;  // set by the launcher: chunks per slot and q / nchunk
+  uint32_t hdr[8];           // 32-B network-order header template (TcpLength, seq, checksum ignored)
+  uint32_t seq0;             // sequence number of image 0 (host order)
+  uint32_t order;            // block order, set by the launcher
+};
+// variant: 0 policy (U4, nt stores), 1 U8, 2 default-policy stores, 3 sc1
+// stores; + 8 default block order (else XCD-chunked).  oversub: 0 = by size
+hipError_t launch_segment(int mode, int variant, SegmentArgs a, uint32_t oversub, uint32_t num_cus,
+                          hipStream_t stream);
 // timing-only streaming micro-kernels (tcpck_diag.hip)
 // ---- retransmit ACK rewrite with incremental checksum update (tcpck_resend.hip) ----
 struct AckArgs {

@@ -44,7 +44,8 @@ KERNEL_VVSTREAM = 8  # packed variable or fixed (stride >= len): param = 0/1 U4/
 KERNEL_GSTREAM = 9  # fixed stride == len, len a power of two in [32, 1024], 16-B aligned arena: param = 0/1/2 U4/U8/U2 (+4 default block order) | oversub << 16
 KERNEL_SSTREAM = 10  # slotted layouts (fixed slots, stride % 16 == 0, or any offset list): param = 0 policy (U4, scattered order), 1 U4, 2 U8 (+4 default block order, +8 scattered) | oversub << 16
 SEG_SHAPES = {1: "G8/U2", 2: "G16/U6", 3: "G64/U4", 4: "G64/U2", 5: "G32/U3", 6: "G4/U8", 7: "W4/U4", 8: "W8/U4", 9: "W16/U2", 10: "W16/U4", 11: "W2/U4"}
-TUNING_EXPORTS = ("tcpck_batch_fixed_ex", "tcpck_batch_var_ex", "tcpck_ctx_set_debug", "tcpck_diag_stream")
+TUNING_EXPORTS = ("tcpck_batch_fixed_ex", "tcpck_batch_var_ex", "tcpck_ctx_set_debug", "tcpck_diag_stream",
+                  "tcpck_batch_segment_ex")
 
 # Every symbol include/tcpck.h declares (checked by tests/test_abi.py).
 EXPORTS = (
@@ -55,7 +56,7 @@ EXPORTS = (
     "tcpck_host_batch_fixed", "tcpck_host_batch_var", "tcpck_ctx_set_chunk_bytes",
     "tcpck_host_alloc", "tcpck_host_free", "tcpck_device_alloc", "tcpck_device_free",
     "tcpck_memcpy_h2d", "tcpck_memcpy_d2h", "tcpck_stream_sync",
-    "tcpck_synth_fixed", "tcpck_synth_var",
+    "tcpck_synth_fixed", "tcpck_synth_var", "tcpck_batch_segment",
 )
 
 
@@ -108,6 +109,8 @@ def lib() -> ctypes.CDLL:
         "tcpck_stream_sync": (i32, [vp, vp]),
         "tcpck_synth_fixed": (i32, [vp, u64, u32, u64, u64, u64, i32, vp]),
         "tcpck_synth_var": (i32, [vp, vp, vp, u32, u64, u64, u64, i32, vp]),
+        "tcpck_batch_segment": (i32, [vp, i32, vp, u64, u32, vp, u32, vp, u64, vp, vp]),
+        "tcpck_batch_segment_ex": (i32, [vp, i32, vp, u64, u32, vp, u32, vp, u64, vp, i32, vp]),
         # include/tcpck_tuning.h
         "tcpck_batch_fixed_ex": (i32, [vp, i32, i32, vp, u64, u32, u64, vp, i32, i32, vp]),
         "tcpck_batch_var_ex": (i32, [vp, i32, i32, vp, vp, vp, u64, vp, ctypes.POINTER(Layout), i32, i32, vp]),
@@ -245,6 +248,22 @@ class Context:
         _check(lib().tcpck_batch_set_ack(self._h, mode, _ptr(arena), _ptr(offsets), stride, count,
                                          _ptr(acks), ack & 0xFFFFFFFF, _ptr(out), _stream(stream)),
                "tcpck_batch_set_ack")
+
+    def batch_segment(self, payload, payload_bytes: int, seg: int, hdr, seq0: int, images, stride: int,
+                      out=None, mode: int = MODE_REF, param: int | None = None, stream=None) -> int:
+        """Send stream -> checksummed images (tcpck_batch_segment): image k at k * stride
+        = hdr with TcpLength/seq of segment k + payload[k seg, ...), checksum filled.
+        hdr: 32 bytes (network order).  Returns the number of images."""
+        h = _as_u8(hdr)
+        if h.size != 32:
+            raise ValueError("hdr must be 32 bytes")
+        args = (self._h, mode, _ptr(payload), payload_bytes, seg, h.ctypes.data, seq0 & 0xFFFFFFFF, _ptr(images),
+                stride, _ptr(out))
+        if param is None:
+            _check(lib().tcpck_batch_segment(*args, _stream(stream)), "tcpck_batch_segment")
+        else:
+            _check(lib().tcpck_batch_segment_ex(*args, param, _stream(stream)), "tcpck_batch_segment_ex")
+        return (payload_bytes + seg - 1) // seg
 
     # explicit kernel choice (include/tcpck_tuning.h)
     def batch_fixed_ex(self, op: int, arena, stride: int, length: int, count: int, out, kernel: int,

@@ -45,6 +45,34 @@ def golden():
     return Golden()
 
 
+class SegmentGolden:
+    """tests/golden/segment_golden.{bin,json}: the reference's data-segment send
+    path (tcp-buffer.h:82-98 .. socket-manager.h:259-260) on known send streams,
+    from tests/golden/gen_segment.cc."""
+
+    def __init__(self):
+        with open(os.path.join(GOLDEN_DIR, "segment_golden.json")) as f:
+            meta = json.load(f)
+        self.blob = np.fromfile(os.path.join(GOLDEN_DIR, meta["blob"]), dtype=np.uint8)
+        assert self.blob.size == meta["blob_bytes"]
+        self.cases = meta["cases"]
+
+    def payload(self, c):
+        return self.blob[c["payload_off"]:c["payload_off"] + c["payload_len"]].copy()
+
+    def template(self, c):
+        return self.blob[c["template_off"]:c["template_off"] + 32].copy()
+
+    def images(self, c):
+        """The reference's images, back to back."""
+        return self.blob[c["images_off"]:c["images_off"] + sum(c["lengths"])].copy()
+
+
+@pytest.fixture(scope="session")
+def segment_golden():
+    return SegmentGolden()
+
+
 @pytest.fixture(scope="session")
 def oracle_c():
     from oracle.ref16 import Ref16C
