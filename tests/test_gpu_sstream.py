@@ -239,3 +239,28 @@ def test_sstream_golden(ctx, golden, variant):
     ctx.batch_var_ex(tcpck.OP_CHECKSUM, dev(arena_np), dev(off), dev(ln), len(cases), out, tcpck.KERNEL_SSTREAM,
                      variant)
     np.testing.assert_array_equal(host(out).view(np.uint16), np.array([c["expected"] for c in cases], np.uint16))
+
+
+@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("case", ["packed_2mod16", "gaps_2mod4", "reversed_gaps"])
+def test_sstream_fill_any_offsets(ctx, variant, case):
+    """FILL on offset lists whose images share 16-B chunks with their neighbours
+    (packed at 2-B offsets), 2-mod-4 gaps, and reversed order (per-image pass)."""
+    import tcpck
+    rng = np.random.default_rng(len(case) * 17 + variant)
+    count = 9000
+    ln = (rng.integers(15, 800, count) * 2).astype(np.uint32)
+    gaps = np.zeros(count, np.uint64) if case == "packed_2mod16" else (rng.integers(0, 40, count) * 2 + 2).astype(np.uint64)
+    off = np.zeros(count, np.uint64)
+    off[1:] = np.cumsum(ln[:-1].astype(np.uint64) + gaps[:-1])
+    off += np.uint64(2)
+    if case == "reversed_gaps":
+        off, ln = off[::-1].copy(), ln[::-1].copy()
+    total = int((off + ln.astype(np.uint64)).max()) + 64
+    arena_np = rng.integers(0, 256, total, dtype=np.uint8)
+    arena = dev(arena_np)
+    out = torch.empty(count, dtype=torch.int16, device="cuda")
+    ctx.batch_var_ex(tcpck.OP_FILL, arena, dev(off), dev(ln), count, out, tcpck.KERNEL_SSTREAM, variant)
+    exp, exp_arena = fill_oracle(arena_np, off, ln)
+    np.testing.assert_array_equal(host(out).view(np.uint16), exp)
+    np.testing.assert_array_equal(host(arena), exp_arena)
