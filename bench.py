@@ -57,6 +57,15 @@ CONFIGS = {
            "fixed", 8 << 20, 1492),
 }
 STRONG = {"c5"}  # configs whose total work is fixed as N grows; the rest are per-GPU (weak)
+# round-2 ops (not BASELINE configs; same contract, their own metric):
+EXTRA = {
+    # the device-resident receive arena: 1M 2048-B slots, one datagram per slot
+    "slots": ("receive slots: 1M x 2048-B slots, images of 96/608/1492 B (C3's mix), offset list, "
+              "TCPCK_LAYOUT_SORTED, VERIFY", "slots", 1 << 20, 2048),
+    # the send path's producer: a 1.5 GB send stream cut into MSS segments
+    "segment": ("send stream 1.5 GiB -> 1460-B segments in 1504-B slots (header template + payload, "
+                "checksum filled; tcpck_batch_segment)", "segment", (1460 << 20) + 2, 1460),
+}
 
 
 def log(*a):
@@ -68,7 +77,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--config", default="c2", choices=sorted(CONFIGS) + ["c1"])
+    p.add_argument("--config", default="c2", choices=sorted(CONFIGS) + ["c1"] + sorted(EXTRA))
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline time budget")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-e2e", action="store_true")
@@ -139,7 +148,7 @@ def main():
             dist.init_process_group(backend)
 
     from tcpck.shard import gather_ranks, max_over_ranks, shard_range
-    desc, kind, count, L = CONFIGS[args.config]
+    desc, kind, count, L = CONFIGS[args.config] if args.config in CONFIGS else EXTRA[args.config]
     ctx = tcpck.Context(local)
     stream = torch.cuda.current_stream()
     if args.config in STRONG:
@@ -147,7 +156,35 @@ def main():
         count = stop - first
     else:
         first = rank * count  # weak: every rank checksums its own batch of the config's size
-    if kind == "fixed":
+    extra_bytes = 0  # algorithmic bytes per launch beyond the image bytes read (+2 per result)
+    if kind == "slots":
+        rng = np.random.default_rng(42 + rank)
+        ln = (np.asarray((64, 576, 1460), np.uint32)[rng.integers(0, 3, count)] + 32).astype(np.uint32)
+        off = np.arange(count, dtype=np.uint64) * np.uint64(L)
+        arena = torch.empty(count * L, dtype=torch.uint8, device="cuda")
+        d_off, d_ln = torch.from_numpy(off).cuda(), torch.from_numpy(ln).cuda()
+        tcpck.synth_var(arena, d_off, d_ln, 1492, count, seed=42, first_index=first, stream=stream)
+        img_bytes = int(ln.astype(np.int64).sum())
+        lmin, lmax = int(ln.min()), int(ln.max())
+
+        def step(out):
+            ctx.batch_var(tcpck.OP_VERIFY, arena, d_off, d_ln, count, out, total_bytes=img_bytes,
+                          min_len=lmin, max_len=lmax, sorted=True, stream=stream)
+    elif kind == "segment":
+        P, seg, stride = count, L, 1504
+        payload = torch.empty(P, dtype=torch.uint8, device="cuda")
+        tcpck.synth_fixed(payload, 1492, 1492, P // 1492, seed=42, first_index=first, stream=stream)
+        count = (P + seg - 1) // seg
+        images = torch.empty(count * stride, dtype=torch.uint8, device="cuda")
+        hdr = np.zeros(32, np.uint8)
+        hdr[0:4], hdr[4:8], hdr[12:14], hdr[14:16] = [127, 0, 0, 1], [127, 0, 0, 1], [0x3C, 0x8C], [0x3C, 0x8D]
+        hdr[20:24], hdr[25] = [0, 0, 0x1E, 0x61], 0x08  # ack 7777, ACK (state.cc:178-180)
+        img_bytes = P  # the stream read
+        extra_bytes = P + 32 * count  # the images written (header + payload; slot padding excluded)
+
+        def step(out):
+            ctx.batch_segment(payload, P, seg, hdr, 1001, images, stride, out, stream=stream)
+    elif kind == "fixed":
         arena = torch.empty(count * L, dtype=torch.uint8, device="cuda")
         tcpck.synth_fixed(arena, L, L, count, seed=42, first_index=first, stream=stream)
         img_bytes = count * L
@@ -167,7 +204,7 @@ def main():
         def step(out):
             ctx.batch_var(tcpck.OP_CHECKSUM, arena, d_off, d_ln, count, out, total_bytes=img_bytes,
                           min_len=lmin, max_len=lmax, packed=True, stream=stream)
-    out = torch.empty(count, dtype=torch.int16, device="cuda")
+    out = torch.empty(count, dtype=torch.int16 if kind != "slots" else torch.uint8, device="cuda")
     torch.cuda.synchronize()
 
     # Settle: an idle MI355X takes 10-50 ms of back-to-back HBM streaming to
@@ -224,7 +261,7 @@ def main():
     value = total_bytes / tmax / GIB
 
     # Checksum digest of this rank's results (parity spot-check on the host below).
-    res = out.cpu().numpy().view(np.uint16)
+    res = out.cpu().numpy().view(np.uint16) if out.dtype == torch.int16 else out.cpu().numpy()
 
     if rank != 0:
         if world > 1:
@@ -232,7 +269,7 @@ def main():
             dist.destroy_process_group()
         return
 
-    algo_bytes = img_bytes + 2 * count  # per launch: image bytes read + 2 B written per image
+    algo_bytes = img_bytes + extra_bytes + (2 if kind != "slots" else 1) * count  # + the results written
     achieved = algo_bytes / (launch_ms * 1e-3) / 1e9
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(args.config),
@@ -240,19 +277,25 @@ def main():
     if world > 1:  # rank 0's kernel above; every GPU's fraction here (equal shards)
         roofline["per_gpu_frac"] = [round(algo_bytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) for ms in launch_ms_all]
 
+    metric = METRIC
+    if kind == "slots":
+        metric = "GiB/s device-resident TCP verify over a slotted receive arena (image bytes); % HBM roofline"
+    elif kind == "segment":
+        metric = "GiB/s of device-resident send stream segmented into checksummed images; % HBM roofline (read + write)"
     rec = {
-        "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world,
+        "metric": metric, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(tmax / args.steps * 1e3, 5),
         "higher_is_better": True,
         "scaling": "strong" if args.config in STRONG else "weak", "vs_baseline": None, "dtype": "u16",
         "data": "synthetic (device-generated: send-path headers + splitmix64 payloads, seed 42)",
-        "config": {"workload": desc, "images_per_gpu": count, "image_bytes": L if L else "96/608/1492",
+        "config": {"workload": desc, "images_per_gpu": count, "image_bytes": {"slots": "96/608/1492 in 2048-B slots", "segment": "32 + 1460 in 1504-B slots"}.get(
+                       kind, L if L else "96/608/1492"),
                    "bytes_per_gpu": img_bytes, "parallelism": f"shard{world} (independent per-GPU batches, no collective)"},
         "roofline": roofline,
         "settle": {"ms": round(settle_ms, 1), "launches": settled,
                    "why": "untimed launches before the W warm-ups: the idle GPU's clock ramp lasts 10-50 ms"},
     }
-    if world == 1 and not args.no_cpu_baseline:
+    if world == 1 and not args.no_cpu_baseline and kind in ("fixed", "mixed"):
         rec["cpu_baseline"] = cpu_baseline(arena, res, kind, count, L, args.cpu_seconds,
                                            None if kind == "fixed" else (off, ln))
     if world == 1 and not args.no_e2e and kind == "fixed" and args.config not in STRONG:
