@@ -97,9 +97,12 @@ for s in ${STEPS:-tests smoke bench prof}; do
     os_c2) step os_c2 600 python scripts/oversub.py --what c2 --variants 0,9,10 --ms 8,16,24,32,40,48 ;;
     os_c3) step os_c3 600 python scripts/oversub.py --what c3 --variants 2,3 --ms 8,16,32 ;;
     prof_c3) step prof_c3 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c3 -o run --output-format csv -- python3 bench.py --config c3 --steps 10 --warmup 2 --no-cpu-baseline --no-e2e ;;
+    prof_slots) step prof_slots 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_slots -o run --output-format csv -- python3 bench.py --config slots --steps 10 --warmup 2 --no-cpu-baseline --no-e2e ;;
+    prof_segment) step prof_segment 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_segment -o run --output-format csv -- python3 bench.py --config segment --steps 10 --warmup 2 --no-cpu-baseline --no-e2e ;;
+    segtests2) step segtests2 600 python -u -m pytest tests/test_gpu_segment.py tests/test_gpu_sstream.py -x -q --timeout 300 --timeout-method thread ;;
     prof_c4) step prof_c4 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c4 -o run --output-format csv -- python3 bench.py --config c4 --steps 10 --warmup 2 --no-cpu-baseline --no-e2e ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-e2e ;;
-    pmc_c2|pmc_c3|pmc_c4)  # separate FETCH_SIZE / WRITE_SIZE passes (TCC slots), kernel trace only
+    pmc_c2|pmc_c3|pmc_c4|pmc_slots|pmc_segment)  # separate FETCH_SIZE / WRITE_SIZE passes (TCC slots), kernel trace only
       c=${s#pmc_}
       step ${s}_fetch 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d gpurun_out/pmc_${c}_fetch -o run --output-format csv -- python3 bench.py --config $c --steps 3 --warmup 1 --settle-ms 0 --no-cpu-baseline --no-e2e
       step ${s}_write 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d gpurun_out/pmc_${c}_write -o run --output-format csv -- python3 bench.py --config $c --steps 3 --warmup 1 --settle-ms 0 --no-cpu-baseline --no-e2e ;;

@@ -21,7 +21,7 @@ import statistics
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = ("rstream_kernel", "vvstream_kernel", "seg_kernel", "jumbo_kernel")
+KERNELS = ("rstream_kernel", "vvstream_kernel", "seg_kernel", "jumbo_kernel", "sstream_kernel", "segment_kernel")
 
 
 def per_launch(path: str, counter: str):
@@ -47,7 +47,7 @@ def main(rnd: str = "r01") -> None:
             summary = json.load(f)
     except (OSError, ValueError):
         summary = {}
-    for cfg in ("c2", "c3", "c4"):
+    for cfg in ("c2", "c3", "c4", "slots", "segment"):
         fp = os.path.join(src, f"pmc_{cfg}_fetch", "run_counter_collection.csv")
         wp = os.path.join(src, f"pmc_{cfg}_write", "run_counter_collection.csv")
         if not (os.path.exists(fp) and os.path.exists(wp)):

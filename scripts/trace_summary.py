@@ -10,7 +10,7 @@ import argparse
 import csv
 import statistics
 
-KERNELS = ("rstream_kernel", "vvstream_kernel", "seg_kernel", "jumbo_kernel")
+KERNELS = ("rstream_kernel", "vvstream_kernel", "seg_kernel", "jumbo_kernel", "sstream_kernel", "segment_kernel")
 
 
 def main():

@@ -52,7 +52,7 @@ using dev::u32x4;
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 __device__ __forceinline__ uint32_t bswap16(uint32_t x) { return ((x & 0xFFu) << 8) | ((x >> 8) & 0xFFu); }
 
-template <int U, int MODE, int SPOL>
+template <int U, int MODE, int SPOL, int LPOL = 2>
 __global__ void __launch_bounds__(kBlock) segment_kernel(SegmentArgs a) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wv = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6)));
@@ -98,7 +98,9 @@ __global__ void __launch_bounds__(kBlock) segment_kernel(SegmentArgs a) {
       const uint32_t len = len_of(i);
       if (pb < len && !is_tail(i, j, len)) voff = i * S + pb;
     }
-    return dev::load16_buf_nt(rin, voff, 0);
+    typedef unsigned v4u __attribute__((ext_vector_type(4)));
+    const v4u v = __builtin_amdgcn_raw_buffer_load_b128(rin, static_cast<int>(voff), 0, LPOL);
+    return u32x4{v.x, v.y, v.z, v.w};
   };
   auto store16 = [&](uint32_t voff, u32x4 w) {
     typedef unsigned v4u __attribute__((ext_vector_type(4)));
@@ -178,9 +180,9 @@ __global__ void __launch_bounds__(kBlock) segment_kernel(SegmentArgs a) {
   }
 }
 
-template <int U, int MODE, int SPOL>
+template <int U, int MODE, int SPOL, int LPOL = 2>
 hipError_t launch_one(SegmentArgs a, uint32_t oversub, uint32_t num_cus, hipStream_t stream) {
-  static const uint32_t per_cu = dev::resident_blocks_per_cu(segment_kernel<U, MODE, SPOL>);
+  static const uint32_t per_cu = dev::resident_blocks_per_cu(segment_kernel<U, MODE, SPOL, LPOL>);
   const uint64_t resident = static_cast<uint64_t>(per_cu) * num_cus;
   const uint64_t out_bytes = a.count * static_cast<uint64_t>(a.stride);
   // runs of >= 3 KiB of output (two 1.5-KB images), M a power of two up to
@@ -198,13 +200,14 @@ hipError_t launch_one(SegmentArgs a, uint32_t oversub, uint32_t num_cus, hipStre
   if (blocks > 0xFFFFFFFFull) return hipErrorInvalidValue;
   a.per_wave = a.count / (blocks * kWavesPerBlock);
   a.rem = a.count % (blocks * kWavesPerBlock);
-  hipLaunchKernelGGL((segment_kernel<U, MODE, SPOL>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0, stream, a);
+  hipLaunchKernelGGL((segment_kernel<U, MODE, SPOL, LPOL>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0, stream, a);
   return hipGetLastError();
 }
 
-template <int U, int SPOL>
+template <int U, int SPOL, int LPOL = 2>
 hipError_t by_mode(int mode, const SegmentArgs &a, uint32_t m, uint32_t num_cus, hipStream_t s) {
-  return mode == kRef ? launch_one<U, kRef, SPOL>(a, m, num_cus, s) : launch_one<U, kRfc1071, SPOL>(a, m, num_cus, s);
+  return mode == kRef ? launch_one<U, kRef, SPOL, LPOL>(a, m, num_cus, s)
+                      : launch_one<U, kRfc1071, SPOL, LPOL>(a, m, num_cus, s);
 }
 
 }  // namespace
@@ -220,14 +223,19 @@ hipError_t launch_segment(int mode, int variant, SegmentArgs a, uint32_t oversub
                 : static_cast<uint32_t>(((uint64_t{1} << (32 + sh)) + a.nchunk - 1) / a.nchunk);
   a.order = (variant & 8) ? dev::kOrderDefault : 4u;  // groups of 16 blocks per XCD
   // variant & 7: 0 = policy, 1 = U4 nt stores, 2 = U4 default-policy stores,
-  // 3 = U4 sc1 stores, 4 = U8 default-policy stores, 5 = U8 nt stores
+  // 3 = U4 sc1 stores, 4 = U8 default-policy stores, 5 = U8 nt stores, 6 = 2 with
+  // default-policy loads
   switch (variant & 7) {
-    case 0: return by_mode<4, 1>(mode, a, oversub, num_cus, stream);  // default-policy stores: 66.6 vs 61.2 % (nt)
+    // policy: default-policy stores (66.6 vs 61.2 % with nt at M = 32) and loads
+    // (9000-B segments 64.2 vs 60.6 %; MSS +0.2-0.5 %: the 4-B offset loads of
+    // 1460-B segments split lines between steps), profiles/r02/segment_probe4.log
+    case 0: return by_mode<4, 1, 0>(mode, a, oversub, num_cus, stream);
     case 1: return by_mode<4, 0>(mode, a, oversub, num_cus, stream);
     case 2: return by_mode<4, 1>(mode, a, oversub, num_cus, stream);
     case 3: return by_mode<4, 2>(mode, a, oversub, num_cus, stream);
     case 4: return by_mode<8, 1>(mode, a, oversub, num_cus, stream);
     case 5: return by_mode<8, 0>(mode, a, oversub, num_cus, stream);
+    case 6: return by_mode<4, 1, 0>(mode, a, oversub, num_cus, stream);  // default-policy loads too
     default: return hipErrorInvalidValue;
   }
 }
