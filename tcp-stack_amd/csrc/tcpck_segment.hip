@@ -180,6 +180,114 @@ __global__ void __launch_bounds__(kBlock) segment_kernel(SegmentArgs a) {
   }
 }
 
+// Jumbo segments: the block's W waves stream ONE image together, wave w taking
+// the image's 1 KiB steps w, w + W, ... (so the block reads W KiB of the image
+// per round, front to back), lane sums accumulated, the W partial sums met in
+// LDS; the block then takes the next image (grid-stride).  With one image per
+// wave, 64-KiB segments left few waves and a last round running alone.
+template <int W, int U, int MODE>
+__global__ void __launch_bounds__(64 * W) segment_wide_kernel(SegmentArgs a) {
+  __shared__ uint32_t s_part[W];
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wv = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6)));
+  const uint32_t S = a.seg, nc = a.nchunk;
+  const uint32_t nsteps = (nc + 63) >> 6;
+  const uint32_t bid = dev::ordered_block(blockIdx.x, gridDim.x, a.order);
+  const uint32_t last_len = static_cast<uint32_t>(a.payload_bytes - (a.count - 1) * static_cast<uint64_t>(S));
+  for (uint64_t k = bid; k < a.count; k += gridDim.x) {
+    const uint64_t p0 = k * S;
+    const uint32_t len = k + 1 == a.count ? last_len : S;
+    const auto rin = dev::make_rsrc(a.payload + p0, len);  // exactly the image's payload
+    const auto rout = dev::make_rsrc(a.images + k * static_cast<uint64_t>(a.stride), a.stride);
+    // chunks j >= 2 whose 16 B pass the payload's end are read dword by dword
+    auto load_step = [&](uint32_t t) -> u32x4 {
+      const uint32_t j = (t << 6) + lane;
+      uint32_t voff = 0xFFFFFFF0u;
+      if (j >= 2 && j < nc && 16 * (j - 2) + 16 <= len) voff = 16 * (j - 2);
+      typedef unsigned v4u __attribute__((ext_vector_type(4)));
+      const v4u v = __builtin_amdgcn_raw_buffer_load_b128(rin, static_cast<int>(voff), 0, 0);
+      return u32x4{v.x, v.y, v.z, v.w};
+    };
+    u32x4 ring[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) ring[u] = load_step(wv + W * u);
+    uint32_t acc = 0;
+    for (uint32_t g = wv; g < nsteps; g += W * U) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t t = g + W * u;
+        const uint32_t j = (t << 6) + lane;
+        u32x4 w = ring[u];
+        if (j < nc) {
+          if (j == 0) {
+            w = u32x4{a.hdr[0], a.hdr[1], (a.hdr[2] & 0x0000FFFFu) | (bswap16(len) << 16), a.hdr[3]};
+          } else if (j == 1) {
+            const uint32_t seq = a.seq0 + static_cast<uint32_t>(k * S);
+            w = u32x4{bswap32(seq), a.hdr[5], a.hdr[6], a.hdr[7] & 0xFFFF0000u};
+          } else {
+            const uint32_t pb = 16 * (j - 2);
+            if (pb >= len) {
+              w = u32x4{0u, 0u, 0u, 0u};
+            } else if (pb + 16 > len) {
+              const uint32_t valid = len - pb;
+              uint32_t d[4];
+#pragma unroll
+              for (int q = 0; q < 4; ++q) {
+                const uint32_t b = 4 * q;
+                d[q] = b + 4 <= valid ? __builtin_amdgcn_raw_buffer_load_b32(rin, static_cast<int>(pb + b), 0, 0)
+                                      : (b + 2 <= valid ? static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b16(
+                                                              rin, static_cast<int>(pb + b), 0, 0))
+                                                        : 0u);
+              }
+              w = u32x4{d[0], d[1], d[2], d[3]};
+            }
+          }
+          if (j != 1) {
+            typedef unsigned v4u __attribute__((ext_vector_type(4)));
+            const v4u v = {w.x, w.y, w.z, w.w};
+            __builtin_amdgcn_raw_buffer_store_b128(v, rout, static_cast<int>(j << 4), 0, 0);
+          }
+        } else {
+          w = u32x4{0u, 0u, 0u, 0u};
+        }
+        acc += dev::ref_chunk_sum_dot(w);  // < 2^32 for an image < 128 KiB: exact
+        ring[u] = load_step(t + W * U);
+      }
+    }
+    acc = dev::group_sum<64>(acc);
+    if (lane == 0) s_part[wv] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t sum = 0;
+#pragma unroll
+      for (int i = 0; i < W; ++i) sum += s_part[i];
+      const uint16_t c = dev::finish<MODE>(sum);
+      if (a.out) a.out[k] = c;
+      const uint32_t seq = a.seq0 + static_cast<uint32_t>(k * S);
+      typedef unsigned v4u __attribute__((ext_vector_type(4)));
+      const v4u v = {bswap32(seq), a.hdr[5], a.hdr[6], (a.hdr[7] & 0xFFFF0000u) | c};
+      __builtin_amdgcn_raw_buffer_store_b128(v, rout, 16, 0, 0);
+    }
+    __syncthreads();  // s_part is rewritten for the next image
+  }
+}
+
+template <int W, int U, int MODE>
+hipError_t launch_wide(SegmentArgs a, uint32_t oversub, uint32_t num_cus, hipStream_t stream) {
+  static const uint32_t per_cu = [] {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, segment_wide_kernel<W, U, MODE>, 64 * W, 0) != hipSuccess ||
+        nb < 1)
+      nb = 1;
+    return static_cast<uint32_t>(nb);
+  }();
+  uint64_t blocks = a.count;
+  const uint64_t cap = static_cast<uint64_t>(per_cu) * num_cus * (oversub ? oversub : 4);
+  if (blocks > cap) blocks = cap;
+  hipLaunchKernelGGL((segment_wide_kernel<W, U, MODE>), dim3(static_cast<uint32_t>(blocks)), dim3(64 * W), 0, stream, a);
+  return hipGetLastError();
+}
+
 template <int U, int MODE, int SPOL, int LPOL = 2>
 hipError_t launch_one(SegmentArgs a, uint32_t oversub, uint32_t num_cus, hipStream_t stream) {
   static const uint32_t per_cu = dev::resident_blocks_per_cu(segment_kernel<U, MODE, SPOL, LPOL>);
@@ -225,17 +333,36 @@ hipError_t launch_segment(int mode, int variant, SegmentArgs a, uint32_t oversub
   // variant & 7: 0 = policy, 1 = U4 nt stores, 2 = U4 default-policy stores,
   // 3 = U4 sc1 stores, 4 = U8 default-policy stores, 5 = U8 nt stores, 6 = 2 with
   // default-policy loads
-  switch (variant & 7) {
+  switch (variant & 7) {  // (bit 3: default block order)
     // policy: default-policy stores (66.6 vs 61.2 % with nt at M = 32) and loads
     // (9000-B segments 64.2 vs 60.6 %; MSS +0.2-0.5 %: the 4-B offset loads of
     // 1460-B segments split lines between steps), profiles/r02/segment_probe4.log
-    case 0: return by_mode<4, 1, 0>(mode, a, oversub, num_cus, stream);
+    // jumbo segments stream with W waves per image (segment_probe5.log): 65532 B
+    // W16 67.4 % against 60.5 % one image per wave, 16 KiB 68.5 vs 60.9 %, 9000 B
+    // W4 65.4 vs 64.1 %; below 8 KiB (MSS) the run kernel (W4 at 1460 B: 35 %)
+    case 0:
+      if (a.seg >= 16384)
+        return mode == kRef ? launch_wide<16, 2, kRef>(a, oversub, num_cus, stream)
+                            : launch_wide<16, 2, kRfc1071>(a, oversub, num_cus, stream);
+      if (a.seg >= 8192)
+        return mode == kRef ? launch_wide<4, 4, kRef>(a, oversub, num_cus, stream)
+                            : launch_wide<4, 4, kRfc1071>(a, oversub, num_cus, stream);
+      return by_mode<4, 1, 0>(mode, a, oversub, num_cus, stream);
     case 1: return by_mode<4, 0>(mode, a, oversub, num_cus, stream);
     case 2: return by_mode<4, 1>(mode, a, oversub, num_cus, stream);
     case 3: return by_mode<4, 2>(mode, a, oversub, num_cus, stream);
     case 4: return by_mode<8, 1>(mode, a, oversub, num_cus, stream);
     case 5: return by_mode<8, 0>(mode, a, oversub, num_cus, stream);
     case 6: return by_mode<4, 1, 0>(mode, a, oversub, num_cus, stream);  // default-policy loads too
+    case 7: {  // W waves per image (variant >> 4: 0 -> 4, 1 -> 8, 2 -> 16)
+      const int wsel = (variant >> 4) & 3;
+      if (wsel == 1) return mode == kRef ? launch_wide<8, 4, kRef>(a, oversub, num_cus, stream)
+                                         : launch_wide<8, 4, kRfc1071>(a, oversub, num_cus, stream);
+      if (wsel == 2) return mode == kRef ? launch_wide<16, 2, kRef>(a, oversub, num_cus, stream)
+                                         : launch_wide<16, 2, kRfc1071>(a, oversub, num_cus, stream);
+      return mode == kRef ? launch_wide<4, 4, kRef>(a, oversub, num_cus, stream)
+                          : launch_wide<4, 4, kRfc1071>(a, oversub, num_cus, stream);
+    }
     default: return hipErrorInvalidValue;
   }
 }
