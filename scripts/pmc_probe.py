@@ -54,6 +54,28 @@ def main():
                                          total_bytes=total))
         print("ok", flush=True)
         return
+    if "--ss" in sys.argv:  # sstream: variable images in 2048-B slots vs fixed 1492 B in 4-KiB slots (same density)
+        import numpy as np
+        S = 2048
+        n = (1 << 31) // S
+        rng = np.random.default_rng(7)
+        ln = np.asarray((96, 608, 1492), np.uint32)[rng.integers(0, 3, n)]
+        off = np.arange(n, dtype=np.uint64) * np.uint64(S)
+        a = torch.empty(n * S, dtype=torch.uint8, device="cuda")
+        d_off, d_ln = torch.from_numpy(off).cuda(), torch.from_numpy(ln).cuda()
+        K.synth_var(a, d_off, d_ln, 1492, n, seed=3)
+        out = torch.empty(n, dtype=torch.int16, device="cuda")
+        run(lambda: ctx.batch_var_ex(K.OP_CHECKSUM, a, d_off, d_ln, n, out, K.KERNEL_SSTREAM, 0,
+                                     total_bytes=int(ln.sum())))
+        del a, out
+        S, L = 4096, 1492
+        n = (1 << 31) // S
+        a = torch.empty(n * S, dtype=torch.uint8, device="cuda")
+        K.synth_fixed(a, S, L, n, seed=3)
+        out = torch.empty(n, dtype=torch.int16, device="cuda")
+        run(lambda: ctx.batch_fixed_ex(K.OP_CHECKSUM, a, S, L, n, out, K.KERNEL_SSTREAM, 0))
+        print("ok", flush=True)
+        return
     a = torch.empty(n * L, dtype=torch.uint8, device="cuda")
     K.synth_fixed(a, L, L, n, seed=42)
     out = torch.empty(n, dtype=torch.int16, device="cuda")
