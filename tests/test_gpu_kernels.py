@@ -194,12 +194,13 @@ def test_rstream_fixed_vs_oracle(ctx, oracle_c, variant, length, count):
 
 
 @pytest.mark.parametrize("variant", RSTREAM)
-@pytest.mark.parametrize("length", [30, 32, 96, 1492, 2000])
+@pytest.mark.parametrize("length", [30, 32, 96, 128, 130, 196, 1024, 1492, 1494, 2000, 9000])
 def test_rstream_fill_verify(ctx, variant, length):
+    """Includes 2-mod-4 lengths (fields at every 16-B phase) and jumbo images."""
     import tcpck
     from oracle import ref16 as R
     rng = np.random.default_rng(length + 10 * variant)
-    count = 9000
+    count = 9000 if length < 4096 else 1500
     arena_np = rng.integers(0, 256, count * length, dtype=np.uint8)
     arena = dev(arena_np)
     out = torch.empty(count, dtype=torch.int16, device="cuda")
