@@ -235,6 +235,14 @@ static bool jumbo_on_seg(int op, uint64_t len) {
 hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t stride, uint32_t len,
                      uint64_t count, void *out, int kernel, int param, hipStream_t s) {
   const uint32_t num_cus = static_cast<uint32_t>(ctx->num_cus);
+  if (kernel == TCPCK_KERNEL_AUTO && mode == TCPCK_MODE_RFC1071 && stride == len && len >= 512 &&
+      len <= kFixedRunMaxLen) {
+    // RFC 1071 on packed fixed images: rstream's prefix is an exact u32 word
+    // sum, so its image differences fold like any sum (C2 in RFC 1071 mode at
+    // the REF rate instead of seg's; profiles/r02/rfc_probe.log)
+    kernel = TCPCK_KERNEL_RSTREAM;
+    param = kRstreamPolicy;
+  }
   if (kernel == TCPCK_KERNEL_AUTO) {
     // jumbo images in slots with small gaps (9000 B in 9216-B slots): vvstream
     // streams the gaps as virtual images, 86 % against seg's 70 % (FILL 78 vs
@@ -306,8 +314,9 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
     }
   }
   if (kernel == TCPCK_KERNEL_RSTREAM) {
-    if (mode != TCPCK_MODE_REF || stride != len || len < 16 || len > (1u << 24)) return hipErrorInvalidValue;
+    if (stride != len || len < 16 || len > (1u << 24)) return hipErrorInvalidValue;
     tcpck::FixedStreamArgs a{};
+    a.mode = mode == TCPCK_MODE_REF ? tcpck::kRef : tcpck::kRfc1071;
     a.arena = arena;
     a.stride = stride;
     a.count = count;

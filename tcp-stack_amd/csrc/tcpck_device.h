@@ -190,15 +190,18 @@ __device__ __forceinline__ uint64_t read_lane64(uint64_t x, uint32_t lane) {
   return (static_cast<uint64_t>(hi) << 32) | lo;
 }
 
-// Sum (REF arithmetic, low 16 bits meaningful) of the first r/2 words of a
-// 16-byte chunk given as four dwords; r even in [0, 16).  Used by the scalar
-// boundary walks with wave-uniform inputs (readlane'd dwords): scalar code.
+// Sum of the first r/2 words of a 16-byte chunk given as four dwords; r even
+// in [0, 16).  REF arithmetic (low 16 bits meaningful) unless EXACT (the exact
+// u32 word sum, for RFC 1071).  Used by the scalar boundary walks with
+// wave-uniform inputs (readlane'd dwords): scalar code.
+template <bool EXACT = false>
 __device__ __forceinline__ uint32_t words_before(uint32_t r, uint32_t x, uint32_t y, uint32_t z, uint32_t w) {
   const uint32_t nw = r >> 1;
   uint32_t h = 0;
-  if (nw >= 2) h += x + (x >> 16);
-  if (nw >= 4) h += y + (y >> 16);
-  if (nw >= 6) h += z + (z >> 16);
+  auto both = [](uint32_t d) -> uint32_t { return EXACT ? (d & 0xFFFFu) + (d >> 16) : d + (d >> 16); };
+  if (nw >= 2) h += both(x);
+  if (nw >= 4) h += both(y);
+  if (nw >= 6) h += both(z);
   if (nw & 1) {
     const uint32_t d = nw == 1 ? x : (nw == 3 ? y : (nw == 5 ? z : w));
     h += d & 0xFFFFu;

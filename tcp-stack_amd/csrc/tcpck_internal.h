@@ -72,6 +72,7 @@ struct FixedStreamArgs {
   uint64_t per_wave;       // run split, set by the launcher: count = per_wave * waves + rem,
   uint64_t rem;            // wave w owns per_wave + (w < rem) images (no 64-bit division on device)
   uint32_t order;          // block order (dev::ordered_block; 0xFF default)
+  int mode;                // kRef, or kRfc1071 (variant 20 only)
 };
 
 // Fixed stride == len == S, S a power of two in [32, 1024], 16-B aligned arena

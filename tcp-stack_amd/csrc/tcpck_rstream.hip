@@ -49,7 +49,10 @@ using dev::u32x4;
 // orders each XCD streams compact regions instead of every eighth run
 // (measured +4% at C2; the HBM bytes do not change), and
 // neighbouring runs share an XCD's L2 for the run-edge line (FLAV bit 2).
-template <int U, int OP, bool STAMP, int PRIO = 0, int FLAV = 0>
+// MODE: kRef, or kRfc1071 -- the run's prefix P is an exact u32 running sum
+// of its words, so P(end) - P(start) is an image's exact word sum (< 2^32 for
+// images < 128 KiB) and RFC 1071 folds it like any other sum
+template <int U, int OP, bool STAMP, int PRIO = 0, int FLAV = 0, int MODE = kRef>
 __global__ void __launch_bounds__(kBlock) rstream_kernel(FixedStreamArgs a) {
   const uint32_t lane = threadIdx.x & 63;
   // readfirstlane: the wave index is uniform, but hipcc cannot prove anything
@@ -131,7 +134,7 @@ __global__ void __launch_bounds__(kBlock) rstream_kernel(FixedStreamArgs a) {
   };
   auto emit = [&](uint32_t jr, uint32_t sum) {  // jr = run-relative image index, sum = its word sum
     const uint32_t j = jr - out_rel;
-    stage = lane == j ? (~sum & 0xFFFFu) : stage;  // j, sum wave-uniform: v_cmp + v_cndmask
+    stage = lane == j ? static_cast<uint32_t>(dev::finish<MODE>(sum)) : stage;  // j, sum wave-uniform: v_cmp + v_cndmask
     if (j == 63) {
       flush(64);
       out_rel += 64;
@@ -188,7 +191,7 @@ __global__ void __launch_bounds__(kBlock) rstream_kernel(FixedStreamArgs a) {
         const uint32_t r = rel & 15u;
         uint32_t P = carry + dev::read_lane(incl, lb) - dev::read_lane(tot, lb);
         if (r)
-          P += dev::words_before(r, dev::read_lane(w.x, lb), dev::read_lane(w.y, lb), dev::read_lane(w.z, lb),
+          P += dev::words_before<MODE == kRfc1071>(r, dev::read_lane(w.x, lb), dev::read_lane(w.y, lb), dev::read_lane(w.z, lb),
                             dev::read_lane(w.w, lb));
         emit(jn - 1, P - p_last);
         p_last = P;
@@ -213,9 +216,9 @@ __global__ void __launch_bounds__(kBlock) rstream_kernel(FixedStreamArgs a) {
   }
 }
 
-template <int U, int OP, bool STAMP, int PRIO = 0, int FLAV = 0>
+template <int U, int OP, bool STAMP, int PRIO = 0, int FLAV = 0, int MODE = kRef>
 hipError_t launch_one(const FixedStreamArgs &a, uint32_t num_cus, hipStream_t stream) {
-  static const uint32_t per_cu = dev::resident_blocks_per_cu(rstream_kernel<U, OP, STAMP, PRIO, FLAV>);
+  static const uint32_t per_cu = dev::resident_blocks_per_cu(rstream_kernel<U, OP, STAMP, PRIO, FLAV, MODE>);
   const uint32_t cap = (a.blocks_per_cu && a.blocks_per_cu < per_cu) ? a.blocks_per_cu : per_cu;
   const uint64_t resident = static_cast<uint64_t>(cap) * num_cus;
   // runs of >= 4 KiB (4-8 KiB: C2 1M x 1492 B at 32x, C5 8M at 256x), up to 1024 x the resident grid
@@ -226,17 +229,17 @@ hipError_t launch_one(const FixedStreamArgs &a, uint32_t num_cus, hipStream_t st
   FixedStreamArgs b = a;
   b.per_wave = a.count / (blocks * kWavesPerBlock);
   b.rem = a.count % (blocks * kWavesPerBlock);
-  hipLaunchKernelGGL((rstream_kernel<U, OP, STAMP, PRIO, FLAV>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0,
+  hipLaunchKernelGGL((rstream_kernel<U, OP, STAMP, PRIO, FLAV, MODE>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0,
                      stream, b);
   return hipGetLastError();
 }
 
-template <int U, bool STAMP, int PRIO = 0, int FLAV = 0>
+template <int U, bool STAMP, int PRIO = 0, int FLAV = 0, int MODE = kRef>
 hipError_t dispatch(int op, const FixedStreamArgs &a, uint32_t num_cus, hipStream_t s) {
   switch (op) {
-    case kChecksum: return launch_one<U, kChecksum, STAMP, PRIO, FLAV>(a, num_cus, s);
-    case kFill: return launch_one<U, kFill, STAMP, PRIO, FLAV>(a, num_cus, s);
-    case kVerify: return launch_one<U, kVerify, STAMP, PRIO, FLAV>(a, num_cus, s);
+    case kChecksum: return launch_one<U, kChecksum, STAMP, PRIO, FLAV, MODE>(a, num_cus, s);
+    case kFill: return launch_one<U, kFill, STAMP, PRIO, FLAV, MODE>(a, num_cus, s);
+    case kVerify: return launch_one<U, kVerify, STAMP, PRIO, FLAV, MODE>(a, num_cus, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -248,6 +251,12 @@ hipError_t launch_rstream(int op, int variant, const FixedStreamArgs &a, uint32_
   if (a.stride < 16 || a.count == 0) return hipErrorInvalidValue;
   const uint64_t max_run = ((a.count + 2047) / 2048 + 1) * a.stride + 128;
   if (max_run >= (uint64_t{1} << 31)) return hipErrorInvalidValue;
+  if (a.mode != kRef) {  // RFC 1071: the policy's variant, images < 128 KiB (exact u32 sums)
+    if (variant != 20 || a.stride >= (1u << 17)) return hipErrorInvalidValue;
+    FixedStreamArgs b = a;
+    b.order = 4u;
+    return dispatch<4, false, 0, 7, kRfc1071>(op, b, num_cus, stream);
+  }
   switch (variant) {
     case 0: return dispatch<4, false>(op, a, num_cus, stream);
     case 1: return dispatch<2, false>(op, a, num_cus, stream);

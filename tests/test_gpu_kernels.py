@@ -594,3 +594,54 @@ def test_gstream_reject(ctx):
         with pytest.raises(tcpck.TcpckError):
             ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, a, 64, 64, 100, o, tcpck.KERNEL_GSTREAM, v)
     ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, a, 64, 64, 0, o, tcpck.KERNEL_GSTREAM, 0)  # empty batch: no-op
+
+
+@pytest.mark.parametrize("length", [512, 1024, 1492, 1494, 2000, 4096, 9000, 65536])
+@pytest.mark.parametrize("kind", ["random", "ones", "zeros", "sum_ffff"])
+def test_rstream_rfc1071_vs_oracle(ctx, oracle_c, length, kind):
+    """Opt-in RFC 1071 mode on rstream (the policy's variant 20): the run prefix is
+    an exact u32 word sum, so the image differences fold exactly -- including
+    all-0xFF images, all-zero images (+0 vs -0) and images whose word sum is a
+    multiple of 0xFFFF.  CHECKSUM, FILL (arena) and VERIFY against the RFC oracle."""
+    import tcpck
+    from oracle import ref16 as R
+    rng = np.random.default_rng(length)
+    count = max(16, min(60000, (64 << 20) // length))  # several images per run: boundaries inside runs
+    if kind == "random":
+        arena_np = rng.integers(0, 256, count * length, dtype=np.uint8)
+    elif kind == "ones":
+        arena_np = np.full(count * length, 0xFF, np.uint8)
+    elif kind == "zeros":
+        arena_np = np.zeros(count * length, np.uint8)
+    else:  # word sums that are multiples of 0xFFFF: a 0xFFFF word, the rest zero
+        arena_np = np.zeros(count * length, np.uint8)
+        arena_np[(np.arange(count) * length + 40)] = 0xFF
+        arena_np[(np.arange(count) * length + 41)] = 0xFF
+    out = torch.empty(count, dtype=torch.int16, device="cuda")
+    arena = dev(arena_np)
+    exp = oracle_c.batch(arena_np, stride=length, length=length, count=count, mode=1, threads=8)
+    for oversub in (0, 1, 16):
+        ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, arena, length, length, count, out, tcpck.KERNEL_RSTREAM,
+                           20 | (oversub << 16), mode=1)
+        np.testing.assert_array_equal(host(out).view(np.uint16), exp)
+    ctx.batch_fixed(tcpck.OP_CHECKSUM, arena, length, length, count, out, mode=1)  # AUTO
+    np.testing.assert_array_equal(host(out).view(np.uint16), exp)
+    ctx.batch_fixed_ex(tcpck.OP_FILL, arena, length, length, count, out, tcpck.KERNEL_RSTREAM, 20, mode=1)
+    exp_arena = arena_np.copy()
+    expf = np.array([R.fill_np(exp_arena[k * length:(k + 1) * length], 1) for k in range(count)], np.uint16)
+    np.testing.assert_array_equal(host(out).view(np.uint16), expf)
+    np.testing.assert_array_equal(host(arena), exp_arena)
+    ok = torch.empty(count, dtype=torch.uint8, device="cuda")
+    ctx.batch_fixed_ex(tcpck.OP_VERIFY, arena, length, length, count, ok, tcpck.KERNEL_RSTREAM, 20, mode=1)
+    exp_ok = (oracle_c.batch(exp_arena, stride=length, length=length, count=count, mode=1, threads=8) == 0)
+    np.testing.assert_array_equal(host(ok).astype(bool), exp_ok)
+
+
+def test_rstream_rfc1071_rejects(ctx):
+    import tcpck
+    a = torch.zeros(1 << 20, dtype=torch.uint8, device="cuda")
+    o = torch.zeros(16, dtype=torch.int16, device="cuda")
+    with pytest.raises(tcpck.TcpckError):  # RFC 1071 on rstream: the policy's variant only
+        ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, a, 1492, 1492, 16, o, tcpck.KERNEL_RSTREAM, 10, mode=1)
+    with pytest.raises(tcpck.TcpckError):  # images of 128 KiB and more: the exact u32 sum could wrap
+        ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, a, 1 << 17, 1 << 17, 4, o, tcpck.KERNEL_RSTREAM, 20, mode=1)
