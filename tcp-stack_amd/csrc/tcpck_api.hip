@@ -242,6 +242,11 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
     // the REF rate instead of seg's; profiles/r02/rfc_probe.log)
     kernel = TCPCK_KERNEL_RSTREAM;
     param = kRstreamPolicy;
+  } else if (kernel == TCPCK_KERNEL_AUTO && mode == TCPCK_MODE_RFC1071 && stride == len && len >= 2 && len < 512 &&
+             (op != TCPCK_OP_FILL || len >= 30)) {
+    // RFC 1071 on small packed images: vvstream's fixed mode with exact u32 prefix tables
+    kernel = TCPCK_KERNEL_VVSTREAM;
+    param = kVvPolicy;
   }
   if (kernel == TCPCK_KERNEL_AUTO) {
     // jumbo images in slots with small gaps (9000 B in 9216-B slots): vvstream
@@ -351,9 +356,10 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
     return tcpck::launch_sstream(op, param & 0xFF, true, a, num_cus, s);
   }
   if (kernel == TCPCK_KERNEL_VVSTREAM) {  // any even length: the prefix table takes any number of ends per step
-    if (mode != TCPCK_MODE_REF || len == 0 || stride > (1u << 24) || (op == TCPCK_OP_FILL && len < 30))
-      return hipErrorInvalidValue;
+    if (len == 0 || stride > (1u << 24) || (op == TCPCK_OP_FILL && len < 30)) return hipErrorInvalidValue;
+    if (mode != TCPCK_MODE_REF && (len >= (1u << 17) || (param & 32))) return hipErrorInvalidValue;
     tcpck::RunArgs a{};
+    a.mode = mode == TCPCK_MODE_REF ? tcpck::kRef : tcpck::kRfc1071;
     a.arena = arena;
     a.stride = stride;
     a.len = len;
@@ -392,7 +398,15 @@ hipError_t run_var(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const uint6
     // vs 72 %, FILL 79 vs 66 %), seg above (a 40000/60032 mix: 83.5 vs 82 %,
     // FILL 83 vs 79 %; profiles/r01/jumbo_layout_probe.log, jumbo_layout_fill_probe.log)
     const bool sorted = mode == TCPCK_MODE_REF && layout && (layout->flags & TCPCK_LAYOUT_SORTED);
-    if (!packed && sorted && typical <= kRunMaxLen && op != TCPCK_OP_FILL) {
+    const bool rfc_packed = mode == TCPCK_MODE_RFC1071 && layout && (layout->flags & TCPCK_LAYOUT_PACKED) &&
+                            typical <= kRunMaxLen && layout->max_len != 0 && layout->max_len < (1u << 17) &&
+                            (op != TCPCK_OP_FILL || (layout->min_len != 0 && layout->min_len >= 30));
+    if (rfc_packed) {
+      // RFC 1071 on packed variable layouts: vvstream with exact u32 prefix
+      // tables (C3 in RFC 1071 mode, profiles/r02/rfc_probe.log)
+      kernel = TCPCK_KERNEL_VVSTREAM;
+      param = kVvPolicy;
+    } else if (!packed && sorted && typical <= kRunMaxLen && op != TCPCK_OP_FILL) {
       // images in order with gaps (receive slots): the compacted slot stream
       // (profiles/r02/slot_probe_ss3.log, seg -> sstream, CHECKSUM): a
       // 96/608/1492 mix in 2048-B slots 60.5 -> 70.3 %, in 1536-B slots 57.4
@@ -410,8 +424,9 @@ hipError_t run_var(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const uint6
     }
   }
   if (kernel == TCPCK_KERNEL_VVSTREAM) {
-    if (mode != TCPCK_MODE_REF) return hipErrorInvalidValue;
+    if (mode != TCPCK_MODE_REF && (param & 32)) return hipErrorInvalidValue;
     tcpck::RunArgs a{};
+    a.mode = mode == TCPCK_MODE_REF ? tcpck::kRef : tcpck::kRfc1071;
     a.arena = arena;
     a.offsets = off;
     a.lengths = len;

@@ -58,6 +58,7 @@ struct RunArgs {
   uint32_t oversub;          // grid = resident blocks x this (0 = by size)
   uint64_t total_bytes;      // batch byte span hint (0 = unknown)
   uint32_t blocks_per_cu;    // vvstream: occupancy cap (LDS padding) and grid base, 0 = by resources
+  int mode;                  // vvstream: kRef or kRfc1071
 };
 
 // Fixed stride == len for rstream (tcpck_rstream.hip).

@@ -79,12 +79,16 @@ __device__ __forceinline__ u32x4 zero_word(u32x4 w, uint32_t wi) {
 }
 
 // LAYOUT: 0 packed variable, 1 fixed packed (stride == len), 2 fixed gapped
-template <int U, int OP, int SPLIT, int LAYOUT, bool KEEP = false>
+// MODE kRfc1071: the prefix table holds exact u32 sums -- u32 P at the dword
+// positions when every end is 4-B aligned (as in REF), else u32 P at every
+// word position (twice the LDS of REF's packed u16 table) -- so P(end) -
+// P(start) is an image's exact word sum and folds
+template <int U, int OP, int SPLIT, int LAYOUT, bool KEEP = false, int MODE = kRef>
 __global__ void __launch_bounds__(kBlock) vvstream_kernel(VVArgs a) {
   constexpr bool FIXED = LAYOUT != 0;
   constexpr bool GAP = LAYOUT == 2;
   __shared__ uint32_t s_end[kWavesPerBlock][FIXED ? 1 : kRing + kMirror];
-  __shared__ __attribute__((aligned(16))) uint32_t s_pre[kWavesPerBlock][256];  // packed u16 prefixes
+  __shared__ __attribute__((aligned(16))) uint32_t s_pre[kWavesPerBlock][MODE == kRef ? 256 : 512];  // the step's prefixes
   __shared__ uint32_t s_fld[kWavesPerBlock][OP == kFill ? 64 : 1];              // kFill: field word + 1 per chunk
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wv = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6)));
@@ -124,7 +128,7 @@ __global__ void __launch_bounds__(kBlock) vvstream_kernel(VVArgs a) {
 
   // k = batch image index, start = its offset in the arena
   auto store = [&](uint64_t k, uint32_t sum, uint64_t start) {
-    const uint16_t c = static_cast<uint16_t>(~sum);  // tcp-header.h:262
+    const uint16_t c = dev::finish<MODE>(sum);  // tcp-header.h:262 (REF)
     if constexpr (OP == kVerify) {
       static_cast<uint8_t *>(a.out)[k] = (c == 0) ? 1 : 0;
     } else {
@@ -134,7 +138,7 @@ __global__ void __launch_bounds__(kBlock) vvstream_kernel(VVArgs a) {
   };
   // the streaming path's form: start_rel run-relative (from A0), field store through the run's rsrc
   auto store_rel = [&](uint64_t k, uint32_t sum, uint32_t start_rel, __amdgpu_buffer_rsrc_t r) {
-    const uint16_t c = static_cast<uint16_t>(~sum);  // tcp-header.h:262
+    const uint16_t c = dev::finish<MODE>(sum);  // tcp-header.h:262 (REF)
     if constexpr (OP == kVerify) {
       static_cast<uint8_t *>(a.out)[k] = (c == 0) ? 1 : 0;
     } else {
@@ -346,9 +350,12 @@ __global__ void __launch_bounds__(kBlock) vvstream_kernel(VVArgs a) {
               // when every end is 4-B aligned, else packed low/high per dword
               const uint32_t p0 = carry + incl - tot;
               const uint32_t b1 = p0 + q1, b2 = p0 + q2, b3 = p0 + q3;
-              if constexpr (AL4)
+              if constexpr (AL4) {
                 pre4[lane] = u32x4{p0, b1, b2, b3};
-              else
+              } else if constexpr (MODE == kRfc1071) {  // exact u32 at all 8 word positions
+                pre4[2 * lane] = u32x4{p0, p0 + (w.x & 0xFFFFu), b1, b1 + (w.y & 0xFFFFu)};
+                pre4[2 * lane + 1] = u32x4{b2, b2 + (w.z & 0xFFFFu), b3, b3 + (w.w & 0xFFFFu)};
+              } else
                 pre4[lane] = u32x4{__builtin_amdgcn_perm(p0 + w.x, p0, 0x05040100u),
                                    __builtin_amdgcn_perm(b1 + w.y, b1, 0x05040100u),
                                    __builtin_amdgcn_perm(b2 + w.z, b2, 0x05040100u),
@@ -358,7 +365,8 @@ __global__ void __launch_bounds__(kBlock) vvstream_kernel(VVArgs a) {
             }
             const uint32_t cnt = static_cast<uint32_t>(__popcll(bal));  // lanes 0..cnt-1 (ends ascend)
             const uint32_t off = min(e - sb, 1022u);                    // the table is laid out like the step
-            const uint32_t P = AL4 ? s_pre[wv][off >> 2] : static_cast<uint32_t>(pre16[off >> 1]);
+            const uint32_t P = AL4 ? s_pre[wv][off >> 2]
+                                   : (MODE == kRfc1071 ? s_pre[wv][off >> 1] : static_cast<uint32_t>(pre16[off >> 1]));
             // P of image jn + lane - 1: lane 0 keeps p_last (wave_shr:1, bound_ctrl off)
             const uint32_t pprev = static_cast<uint32_t>(
                 __builtin_amdgcn_update_dpp(static_cast<int>(p_last), static_cast<int>(P), 0x138, 0xF, 0xF, false));
@@ -404,15 +412,15 @@ __global__ void __launch_bounds__(kBlock) vvstream_kernel(VVArgs a) {
       const uint64_t start = FIXED ? k * S : a.offsets[k] - a.base;
       const uint32_t len = FIXED ? L : a.lengths[k];
       if (OP == kFill && len < 30) continue;  // precondition of kFill (the C ABI rejects these)
-      const uint32_t sum = dev::wave_image_sum<2, kRef>(arena, start, len, OP == kFill);
+      const uint32_t sum = dev::wave_image_sum<2, MODE>(arena, start, len, OP == kFill);
       if (lane == 0) store(k, sum, start);
     }
   }
 }
 
-template <int U, int OP, int SPLIT, int LAYOUT, bool KEEP = false>
+template <int U, int OP, int SPLIT, int LAYOUT, bool KEEP = false, int MODE = kRef>
 hipError_t launch_one(const RunArgs &s, uint32_t oversub, int flags, uint32_t num_cus, hipStream_t stream) {
-  static const uint32_t per_cu = dev::resident_blocks_per_cu(vvstream_kernel<U, OP, SPLIT, LAYOUT, KEEP>);
+  static const uint32_t per_cu = dev::resident_blocks_per_cu(vvstream_kernel<U, OP, SPLIT, LAYOUT, KEEP, MODE>);
   const uint64_t resident = static_cast<uint64_t>(per_cu) * num_cus;
   uint64_t blocks = resident * (oversub ? oversub : 1);
   const uint64_t need = (s.count + kWavesPerBlock - 1) / kWavesPerBlock;
@@ -431,13 +439,21 @@ hipError_t launch_one(const RunArgs &s, uint32_t oversub, int flags, uint32_t nu
   a.len = s.len;
   a.order = (flags & 8) ? 4u : dev::kOrderDefault;  // groups of 16 blocks per XCD
   a.keep_first = (flags & 16) ? 1u : 0u;
-  hipLaunchKernelGGL((vvstream_kernel<U, OP, SPLIT, LAYOUT, KEEP>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0,
+  hipLaunchKernelGGL((vvstream_kernel<U, OP, SPLIT, LAYOUT, KEEP, MODE>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0,
                      stream, a);
   return hipGetLastError();
 }
 
 template <int U, int SPLIT, int LAYOUT>
 hipError_t dispatch(int op, const RunArgs &a, uint32_t oversub, int flags, uint32_t num_cus, hipStream_t s) {
+  if (a.mode != kRef) {  // RFC 1071 (no KEEP variant)
+    switch (op) {
+      case kChecksum: return launch_one<U, kChecksum, SPLIT, LAYOUT, false, kRfc1071>(a, oversub, flags, num_cus, s);
+      case kVerify: return launch_one<U, kVerify, SPLIT, LAYOUT, false, kRfc1071>(a, oversub, flags, num_cus, s);
+      case kFill: return launch_one<U, kFill, SPLIT, LAYOUT, false, kRfc1071>(a, oversub, flags, num_cus, s);
+      default: return hipErrorInvalidValue;
+    }
+  }
   switch (op) {
     case kChecksum: return launch_one<U, kChecksum, SPLIT, LAYOUT>(a, oversub, flags, num_cus, s);
     case kVerify: return launch_one<U, kVerify, SPLIT, LAYOUT>(a, oversub, flags, num_cus, s);

@@ -645,3 +645,65 @@ def test_rstream_rfc1071_rejects(ctx):
         ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, a, 1492, 1492, 16, o, tcpck.KERNEL_RSTREAM, 10, mode=1)
     with pytest.raises(tcpck.TcpckError):  # images of 128 KiB and more: the exact u32 sum could wrap
         ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, a, 1 << 17, 1 << 17, 4, o, tcpck.KERNEL_RSTREAM, 20, mode=1)
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 28])
+@pytest.mark.parametrize("payloads", [(64, 576, 1460), (66, 578, 1462), (-30, -2, 0, 64), (0, 9000, 65504)])
+@pytest.mark.parametrize("count", [1, 65, 257, 5000, 70001])
+def test_vvstream_rfc1071_var(ctx, oracle_c, variant, payloads, count):
+    """RFC 1071 on vvstream, packed variable layouts: the u32 prefix table at dword
+    positions (4-B aligned ends) or at every word position (2-mod-4 ends), exact
+    sums folded.  CHECKSUM and VERIFY against the RFC oracle, misaligned arenas."""
+    import tcpck
+    off, ln, total = packed_layout(count, count + len(payloads) + variant, payloads)
+    if total > (96 << 20):
+        return
+    rng = np.random.default_rng(count * 3 + variant)
+    arena_np = rng.integers(0, 256, total + 128, dtype=np.uint8)
+    if count > 3:
+        k = count // 2
+        arena_np[int(off[k]):int(off[k]) + int(ln[k])] = 0xFF  # an all-ones image
+    buf = dev(arena_np)
+    d_off, d_ln = dev(off), dev(ln)
+    for mis in (0, 2):
+        out = torch.empty(count, dtype=torch.int16, device="cuda")
+        ctx.batch_var_ex(tcpck.OP_CHECKSUM, buf.data_ptr() + mis, d_off, d_ln, count, out, tcpck.KERNEL_VVSTREAM,
+                         variant, mode=1, packed=True, total_bytes=total)
+        exp = oracle_c.batch(arena_np[mis:], off, ln, mode=1, threads=8)
+        np.testing.assert_array_equal(host(out).view(np.uint16), exp)
+    ok = torch.empty(count, dtype=torch.uint8, device="cuda")
+    ctx.batch_var(tcpck.OP_VERIFY, buf, d_off, d_ln, count, ok, mode=1, packed=True, total_bytes=total,
+                  min_len=int(ln.min()), max_len=int(ln.max()))  # AUTO
+    np.testing.assert_array_equal(host(ok), (oracle_c.batch(arena_np, off, ln, mode=1, threads=8) == 0).astype(np.uint8))
+
+
+@pytest.mark.parametrize("stride,length", [(32, 32), (96, 96), (98, 98), (256, 256), (510, 510), (128, 96),
+                                           (1536, 1492), (1000, 998)])
+@pytest.mark.parametrize("count", [1, 63, 4000, 100000])
+def test_vvstream_rfc1071_fixed_fill(ctx, oracle_c, stride, length, count):
+    """RFC 1071 on vvstream's fixed and gapped modes: CHECKSUM, FILL (arena byte-exact)
+    and VERIFY; packed small images through AUTO as well."""
+    import tcpck
+    from oracle import ref16 as R
+    if count * stride > (64 << 20):
+        count = (64 << 20) // stride
+    rng = np.random.default_rng(stride + length + count)
+    arena_np = rng.integers(0, 256, count * stride + 64, dtype=np.uint8)
+    arena = dev(arena_np)
+    out = torch.empty(count, dtype=torch.int16, device="cuda")
+    exp = oracle_c.batch(arena_np, stride=stride, length=length, count=count, mode=1, threads=8)
+    ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, arena, stride, length, count, out, tcpck.KERNEL_VVSTREAM, 4, mode=1)
+    np.testing.assert_array_equal(host(out).view(np.uint16), exp)
+    if stride == length:
+        ctx.batch_fixed(tcpck.OP_CHECKSUM, arena, stride, length, count, out, mode=1)
+        np.testing.assert_array_equal(host(out).view(np.uint16), exp)
+    ctx.batch_fixed_ex(tcpck.OP_FILL, arena, stride, length, count, out, tcpck.KERNEL_VVSTREAM, 4, mode=1)
+    exp_arena = arena_np.copy()
+    expf = np.array([R.fill_np(exp_arena[k * stride:k * stride + length], 1) for k in range(count)], np.uint16)
+    np.testing.assert_array_equal(host(out).view(np.uint16), expf)
+    np.testing.assert_array_equal(host(arena), exp_arena)
+    ok = torch.empty(count, dtype=torch.uint8, device="cuda")
+    ctx.batch_fixed_ex(tcpck.OP_VERIFY, arena, stride, length, count, ok, tcpck.KERNEL_VVSTREAM, 4, mode=1)
+    np.testing.assert_array_equal(host(ok).astype(bool),
+                                  oracle_c.batch(exp_arena, stride=stride, length=length, count=count, mode=1,
+                                                 threads=8) == 0)
