@@ -160,11 +160,12 @@ def test_run_kernels_reject(ctx):
     ln = torch.full((8,), 1000, dtype=torch.int32, device="cuda")
     with pytest.raises(tcpck.TcpckError):  # rstream: gaps
         ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, a, 1500, 1492, 100, o, tcpck.KERNEL_RSTREAM, 0)
-    for kern in (tcpck.KERNEL_RSTREAM, tcpck.KERNEL_VVSTREAM):  # RFC 1071 mode: seg only
-        with pytest.raises(tcpck.TcpckError):
-            ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, a, 1492, 1492, 100, o, kern, 0, mode=1)
-    with pytest.raises(tcpck.TcpckError):
-        ctx.batch_var_ex(tcpck.OP_CHECKSUM, a, off, ln, 8, o, tcpck.KERNEL_VVSTREAM, 0, mode=1)
+    with pytest.raises(tcpck.TcpckError):  # RFC 1071 on rstream: the policy's variant (20) only
+        ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, a, 1492, 1492, 100, o, tcpck.KERNEL_RSTREAM, 0, mode=1)
+    with pytest.raises(tcpck.TcpckError):  # RFC 1071 on vvstream: not with the FILL default-policy reads (+32)
+        ctx.batch_fixed_ex(tcpck.OP_FILL, a, 96, 96, 100, o, tcpck.KERNEL_VVSTREAM, 36, mode=1)
+    with pytest.raises(tcpck.TcpckError):  # sstream: reference mode only
+        ctx.batch_var_ex(tcpck.OP_CHECKSUM, a, off, ln, 8, o, tcpck.KERNEL_SSTREAM, 0, mode=1)
     with pytest.raises(tcpck.TcpckError):  # removed kernels
         ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, a, 1492, 1492, 100, o, 2, 0)
     with pytest.raises(tcpck.TcpckError):
