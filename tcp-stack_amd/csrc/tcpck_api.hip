@@ -258,7 +258,14 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
     // FILL 65.6 -> 79.0 %, profiles/r02/slot_probe_ss3.log), else seg
     const bool jumbo_slots = stride > len && !jumbo_hull && tcpck::sstream_fixed_applies(stride, len) &&
                              (op != TCPCK_OP_FILL || len >= 30);
-    if (mode != TCPCK_MODE_REF || len < 2 ||
+    // RFC 1071: slots with larger gaps (beyond vvstream's hull rule) on sstream
+    // with exact u32 prefix tables; every other layout not routed above on seg
+    const bool rfc_slots = mode == TCPCK_MODE_RFC1071 && stride > len && len < (1u << 17) &&
+                           tcpck::sstream_fixed_applies(stride, len) && (op != TCPCK_OP_FILL || len >= 30);
+    if (rfc_slots) {
+      kernel = TCPCK_KERNEL_SSTREAM;
+      param = 0;
+    } else if (mode != TCPCK_MODE_REF || len < 2 ||
         (len > kFixedRunMaxLen && !jumbo_slots && (stride > len ? !jumbo_hull : jumbo_on_seg(op, len))) ||
         stride > (1u << 24)) {
       kernel = TCPCK_KERNEL_SEG;
@@ -344,9 +351,11 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
   }
   if (kernel == TCPCK_KERNEL_SSTREAM) {  // fixed slots: stride % 16 == 0, stride >= len
     if (count == 1) stride = (static_cast<uint64_t>(len) + 15) & ~uint64_t{15};  // one image: never read
-    if (mode != TCPCK_MODE_REF || !tcpck::sstream_fixed_applies(stride, len) || (op == TCPCK_OP_FILL && len < 30))
+    if (!tcpck::sstream_fixed_applies(stride, len) || (op == TCPCK_OP_FILL && len < 30) ||
+        (mode != TCPCK_MODE_REF && len >= (1u << 17)))
       return hipErrorInvalidValue;
     tcpck::RunArgs a{};
+    a.mode = mode == TCPCK_MODE_REF ? tcpck::kRef : tcpck::kRfc1071;
     a.arena = arena;
     a.stride = stride;
     a.len = len;
@@ -397,7 +406,6 @@ hipError_t run_var(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const uint6
     // (20000 B 86 % vs seg 76 %, FILL 82 vs 71 %; a 9000/20000/40000 mix 83
     // vs 72 %, FILL 79 vs 66 %), seg above (a 40000/60032 mix: 83.5 vs 82 %,
     // FILL 83 vs 79 %; profiles/r01/jumbo_layout_probe.log, jumbo_layout_fill_probe.log)
-    const bool sorted = mode == TCPCK_MODE_REF && layout && (layout->flags & TCPCK_LAYOUT_SORTED);
     const bool rfc_packed = mode == TCPCK_MODE_RFC1071 && layout && (layout->flags & TCPCK_LAYOUT_PACKED) &&
                             typical <= kRunMaxLen && layout->max_len != 0 && layout->max_len < (1u << 17) &&
                             (op != TCPCK_OP_FILL || (layout->min_len != 0 && layout->min_len >= 30));
@@ -406,7 +414,10 @@ hipError_t run_var(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const uint6
       // tables (C3 in RFC 1071 mode, profiles/r02/rfc_probe.log)
       kernel = TCPCK_KERNEL_VVSTREAM;
       param = kVvPolicy;
-    } else if (!packed && sorted && typical <= kRunMaxLen && op != TCPCK_OP_FILL) {
+    } else if (!packed && typical <= kRunMaxLen && op != TCPCK_OP_FILL && layout &&
+               (layout->flags & TCPCK_LAYOUT_SORTED) &&
+               (mode == TCPCK_MODE_REF || (layout->max_len != 0 && layout->max_len < (1u << 17)))) {
+      // (RFC 1071 too, with exact u32 prefix tables, when every image is below 128 KiB)
       // images in order with gaps (receive slots): the compacted slot stream
       // (profiles/r02/slot_probe_ss3.log, seg -> sstream, CHECKSUM): a
       // 96/608/1492 mix in 2048-B slots 60.5 -> 70.3 %, in 1536-B slots 57.4
@@ -438,9 +449,9 @@ hipError_t run_var(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const uint6
     a.blocks_per_cu = static_cast<uint32_t>(param >> 8) & 0xFFu;
     return tcpck::launch_vvstream(op, param & 0xFF, false, a, static_cast<uint32_t>(ctx->num_cus), s);
   }
-  if (kernel == TCPCK_KERNEL_SSTREAM) {  // any offset list (runs of <= 256 images)
-    if (mode != TCPCK_MODE_REF) return hipErrorInvalidValue;
+  if (kernel == TCPCK_KERNEL_SSTREAM) {  // any offset list (runs of <= 128 images)
     tcpck::RunArgs a{};
+    a.mode = mode == TCPCK_MODE_REF ? tcpck::kRef : tcpck::kRfc1071;
     a.arena = arena;
     a.offsets = off;
     a.lengths = len;

@@ -75,6 +75,7 @@ struct SSArgs {
   uint32_t lead;            // fixed: offset of every image inside its first chunk
   uint32_t magic, shift;    // fixed: q / nchunk == mulhi(q, magic) >> shift (magic 0: q >> shift)
   uint32_t order;           // block order (dev::ordered_block)
+  int mode;                 // kRef or kRfc1071
 };
 
 __device__ __forceinline__ u32x4 zero_word(u32x4 w, uint32_t wi) {
@@ -93,13 +94,15 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t x) {
   return x;
 }
 
-template <int U, int OP, bool FIXED>
+// MODE kRfc1071: exact u32 prefix tables (as tcpck_vvstream.hip), the
+// differences folded
+template <int U, int OP, bool FIXED, int MODE = kRef>
 __global__ void __launch_bounds__(kBlock) sstream_kernel(SSArgs a) {
   __shared__ uint32_t s_end[kWavesPerBlock][FIXED ? 1 : kEnds];         // virtual ends, compacted bytes
   __shared__ uint32_t s_c[kWavesPerBlock][FIXED ? 1 : kMaxRun + 64];    // first compacted chunk, ~0 past the run
   __shared__ uint32_t s_d[kWavesPerBlock][FIXED ? 1 : kMaxRun];         // chunk q of image i at d_i + 16 q
   __shared__ uint32_t s_flag[kWavesPerBlock][FIXED ? 1 : 64];           // images starting at chunk q0 + l
-  __shared__ __attribute__((aligned(16))) uint32_t s_pre[kWavesPerBlock][256];  // the step's prefix table
+  __shared__ __attribute__((aligned(16))) uint32_t s_pre[kWavesPerBlock][MODE == kRef ? 256 : 512];  // the step's prefix table
   __shared__ uint32_t s_fld[kWavesPerBlock][OP == kFill ? 64 : 1];      // kFill: field word + 1 per chunk
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wv = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6)));
@@ -116,7 +119,7 @@ __global__ void __launch_bounds__(kBlock) sstream_kernel(SSArgs a) {
   uint8_t *const arena = a.arena;
 
   auto store = [&](uint64_t k, uint32_t sum, uint64_t start) {
-    const uint16_t c = static_cast<uint16_t>(~sum);  // tcp-header.h:262
+    const uint16_t c = dev::finish<MODE>(sum);  // tcp-header.h:262 (REF)
     if constexpr (OP == kVerify) {
       static_cast<uint8_t *>(a.out)[k] = (c == 0) ? 1 : 0;
     } else {
@@ -321,7 +324,10 @@ __global__ void __launch_bounds__(kBlock) sstream_kernel(SSArgs a) {
               const uint32_t b1 = p0 + q1, b2 = p0 + q2, b3 = p0 + q3;
               if constexpr (AL4)
                 pre4[lane] = u32x4{p0, b1, b2, b3};
-              else
+              else if constexpr (MODE == kRfc1071) {
+                pre4[2 * lane] = u32x4{p0, p0 + (w.x & 0xFFFFu), b1, b1 + (w.y & 0xFFFFu)};
+                pre4[2 * lane + 1] = u32x4{b2, b2 + (w.z & 0xFFFFu), b3, b3 + (w.w & 0xFFFFu)};
+              } else
                 pre4[lane] = u32x4{__builtin_amdgcn_perm(p0 + w.x, p0, 0x05040100u),
                                    __builtin_amdgcn_perm(b1 + w.y, b1, 0x05040100u),
                                    __builtin_amdgcn_perm(b2 + w.z, b2, 0x05040100u),
@@ -331,7 +337,8 @@ __global__ void __launch_bounds__(kBlock) sstream_kernel(SSArgs a) {
             }
             const uint32_t cnt = static_cast<uint32_t>(__popcll(bal));  // lanes 0..cnt-1 (ends ascend)
             const uint32_t off = min(e - sb, 1022u);
-            const uint32_t P = AL4 ? s_pre[wv][off >> 2] : static_cast<uint32_t>(pre16[off >> 1]);
+            const uint32_t P = AL4 ? s_pre[wv][off >> 2]
+                                   : (MODE == kRfc1071 ? s_pre[wv][off >> 1] : static_cast<uint32_t>(pre16[off >> 1]));
             const uint32_t pprev = static_cast<uint32_t>(
                 __builtin_amdgcn_update_dpp(static_cast<int>(p_last), static_cast<int>(P), 0x138, 0xF, 0xF, false));
             // the previous virtual end (= this image's start), read by DPP with
@@ -344,7 +351,7 @@ __global__ void __launch_bounds__(kBlock) sstream_kernel(SSArgs a) {
             if (inb && (jj & 1u)) {  // an image end (odd virtual index)
               const uint32_t i = jj >> 1;
               if constexpr (OP == kFill) {
-                const uint16_t cs = static_cast<uint16_t>(~(P - pprev));  // tcp-header.h:262
+                const uint16_t cs = dev::finish<MODE>(P - pprev);  // tcp-header.h:262 (REF)
                 if (a.out) static_cast<uint16_t *>(a.out)[kb + i] = cs;
                 dev::store16_field(rsrc, field_at(i, lane == 0 ? e_last : el), cs);  // raw, as the reference
               } else {
@@ -375,7 +382,7 @@ __global__ void __launch_bounds__(kBlock) sstream_kernel(SSArgs a) {
         if (v & 1u) {
           const uint32_t sum = i == 0 ? carry - p_last : 0u;
           if constexpr (OP == kFill) {
-            const uint16_t cs = static_cast<uint16_t>(~sum);
+            const uint16_t cs = dev::finish<MODE>(sum);
             if (a.out) static_cast<uint16_t *>(a.out)[kb + (v >> 1)] = cs;
             dev::store16_field(rsrc, field_at(v >> 1, i == 0 ? e_last : span), cs);
           } else {
@@ -390,15 +397,15 @@ __global__ void __launch_bounds__(kBlock) sstream_kernel(SSArgs a) {
       const uint64_t start = FIXED ? k * S : a.offsets[k] - a.base;
       const uint32_t len = FIXED ? L : a.lengths[k];
       if (OP == kFill && len < 30) continue;  // precondition of kFill (the C ABI rejects these)
-      const uint32_t sum = dev::wave_image_sum<2, kRef>(arena, start, len, OP == kFill);
+      const uint32_t sum = dev::wave_image_sum<2, MODE>(arena, start, len, OP == kFill);
       if (lane == 0) store(k, sum, start);
     }
   }
 }
 
-template <int U, int OP, bool FIXED>
+template <int U, int OP, bool FIXED, int MODE = kRef>
 hipError_t launch_one(SSArgs a, uint32_t oversub, uint64_t min_waves, uint32_t num_cus, hipStream_t stream) {
-  static const uint32_t per_cu = dev::resident_blocks_per_cu(sstream_kernel<U, OP, FIXED>);
+  static const uint32_t per_cu = dev::resident_blocks_per_cu(sstream_kernel<U, OP, FIXED, MODE>);
   const uint64_t resident = static_cast<uint64_t>(per_cu) * num_cus;
   uint64_t blocks = resident * oversub;
   const uint64_t need = (a.count + kWavesPerBlock - 1) / kWavesPerBlock;  // >= 1 image per wave
@@ -409,12 +416,20 @@ hipError_t launch_one(SSArgs a, uint32_t oversub, uint64_t min_waves, uint32_t n
   if (blocks > 0xFFFFFFFFull) return hipErrorInvalidValue;
   a.per_wave = a.count / (blocks * kWavesPerBlock);
   a.rem = a.count % (blocks * kWavesPerBlock);
-  hipLaunchKernelGGL((sstream_kernel<U, OP, FIXED>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0, stream, a);
+  hipLaunchKernelGGL((sstream_kernel<U, OP, FIXED, MODE>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0, stream, a);
   return hipGetLastError();
 }
 
 template <int U, bool FIXED>
 hipError_t dispatch(int op, const SSArgs &a, uint32_t m, uint64_t min_waves, uint32_t num_cus, hipStream_t s) {
+  if (a.mode != kRef) {
+    switch (op) {
+      case kChecksum: return launch_one<U, kChecksum, FIXED, kRfc1071>(a, m, min_waves, num_cus, s);
+      case kVerify: return launch_one<U, kVerify, FIXED, kRfc1071>(a, m, min_waves, num_cus, s);
+      case kFill: return launch_one<U, kFill, FIXED, kRfc1071>(a, m, min_waves, num_cus, s);
+      default: return hipErrorInvalidValue;
+    }
+  }
   switch (op) {
     case kChecksum: return launch_one<U, kChecksum, FIXED>(a, m, min_waves, num_cus, s);
     case kVerify: return launch_one<U, kVerify, FIXED>(a, m, min_waves, num_cus, s);
@@ -438,6 +453,7 @@ hipError_t launch_sstream(int op, int variant, bool fixed, const RunArgs &r, uin
   a.base = r.base;
   a.count = r.count;
   a.out = r.out;
+  a.mode = r.mode;
   // + 4: default block order; + 8: scattered (the policy's); else groups of
   // 16 blocks per XCD
   a.order = (variant & 8) ? kOrderScatter : ((variant & 4) ? dev::kOrderDefault : 4u);

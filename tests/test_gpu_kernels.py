@@ -164,8 +164,8 @@ def test_run_kernels_reject(ctx):
         ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, a, 1492, 1492, 100, o, tcpck.KERNEL_RSTREAM, 0, mode=1)
     with pytest.raises(tcpck.TcpckError):  # RFC 1071 on vvstream: not with the FILL default-policy reads (+32)
         ctx.batch_fixed_ex(tcpck.OP_FILL, a, 96, 96, 100, o, tcpck.KERNEL_VVSTREAM, 36, mode=1)
-    with pytest.raises(tcpck.TcpckError):  # sstream: reference mode only
-        ctx.batch_var_ex(tcpck.OP_CHECKSUM, a, off, ln, 8, o, tcpck.KERNEL_SSTREAM, 0, mode=1)
+    with pytest.raises(tcpck.TcpckError):  # RFC 1071 on sstream: images below 128 KiB
+        ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, a, 1 << 18, 1 << 17, 2, o, tcpck.KERNEL_SSTREAM, 0, mode=1)
     with pytest.raises(tcpck.TcpckError):  # removed kernels
         ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, a, 1492, 1492, 100, o, 2, 0)
     with pytest.raises(tcpck.TcpckError):

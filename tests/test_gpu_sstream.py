@@ -174,8 +174,8 @@ def test_sstream_fixed_rejects(ctx):
     for stride, length in ((1500, 1492), (1492, 1492), (2056, 2058)):  # stride % 16 != 0, or stride < len
         with pytest.raises(tcpck.TcpckError):
             ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, a, stride, length, 100, o, tcpck.KERNEL_SSTREAM, 0)
-    with pytest.raises(tcpck.TcpckError):  # RFC 1071: seg only
-        ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, a, 2048, 1492, 100, o, tcpck.KERNEL_SSTREAM, 0, mode=1)
+    with pytest.raises(tcpck.TcpckError):  # RFC 1071: images below 128 KiB (exact u32 sums)
+        ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, a, 1 << 18, 1 << 17, 2, o, tcpck.KERNEL_SSTREAM, 0, mode=1)
     with pytest.raises(tcpck.TcpckError):
         ctx.batch_fixed_ex(tcpck.OP_FILL, a, 32, 28, 100, o, tcpck.KERNEL_SSTREAM, 0)
 
@@ -264,3 +264,53 @@ def test_sstream_fill_any_offsets(ctx, variant, case):
     exp, exp_arena = fill_oracle(arena_np, off, ln)
     np.testing.assert_array_equal(host(out).view(np.uint16), exp)
     np.testing.assert_array_equal(host(arena), exp_arena)
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("slot,lengths", SLOTS[:-1])
+@pytest.mark.parametrize("count", [1, 257, 40000])
+def test_sstream_rfc1071(ctx, oracle_c, variant, slot, lengths, count):
+    """RFC 1071 on the slot stream: exact u32 prefix tables (dword or word
+    positions), folded differences; CHECKSUM, VERIFY (AUTO with the SORTED hint)
+    and FILL against the RFC oracle."""
+    import tcpck
+    from oracle import ref16 as R
+    if count * slot > (160 << 20):
+        count = (160 << 20) // slot
+    off, ln, total = slot_layout(count, slot, lengths, seed=count + slot + 7 * variant)
+    rng = np.random.default_rng(count * 11 + slot)
+    arena_np = rng.integers(0, 256, total + 128, dtype=np.uint8)
+    if count > 2:
+        k = count // 2
+        arena_np[int(off[k]):int(off[k]) + int(ln[k])] = 0xFF
+    arena = dev(arena_np)
+    d_off, d_ln = dev(off), dev(ln)
+    exp = oracle_c.batch(arena_np, off, ln, mode=1, threads=8)
+    out = torch.empty(count, dtype=torch.int16, device="cuda")
+    ctx.batch_var_ex(tcpck.OP_CHECKSUM, arena, d_off, d_ln, count, out, tcpck.KERNEL_SSTREAM, variant, mode=1)
+    np.testing.assert_array_equal(host(out).view(np.uint16), exp)
+    ok = torch.empty(count, dtype=torch.uint8, device="cuda")
+    ctx.batch_var(tcpck.OP_VERIFY, arena, d_off, d_ln, count, ok, mode=1, sorted=True, total_bytes=int(ln.sum()),
+                  min_len=int(ln.min()), max_len=int(ln.max()))
+    np.testing.assert_array_equal(host(ok), (exp == 0).astype(np.uint8))
+    if min(lengths) >= 30:
+        ctx.batch_var_ex(tcpck.OP_FILL, arena, d_off, d_ln, count, out, tcpck.KERNEL_SSTREAM, variant, mode=1)
+        exp_arena = arena_np.copy()
+        expf = np.array([R.fill_np(exp_arena[int(off[k]):int(off[k]) + int(ln[k])], 1) for k in range(count)],
+                        np.uint16)
+        np.testing.assert_array_equal(host(out).view(np.uint16), expf)
+        np.testing.assert_array_equal(host(arena), exp_arena)
+
+
+@pytest.mark.parametrize("stride,length", [(2048, 1492), (2048, 1494), (256, 96), (16384, 9000), (80, 34)])
+def test_sstream_rfc1071_fixed_auto(ctx, oracle_c, stride, length):
+    import tcpck
+    count = max(8, min(30000, (48 << 20) // stride))
+    rng = np.random.default_rng(stride + length)
+    arena_np = rng.integers(0, 256, count * stride, dtype=np.uint8)
+    arena = dev(arena_np)
+    out = torch.empty(count, dtype=torch.int16, device="cuda")
+    ctx.batch_fixed(tcpck.OP_CHECKSUM, arena, stride, length, count, out, mode=1)
+    np.testing.assert_array_equal(host(out).view(np.uint16),
+                                  oracle_c.batch(arena_np, stride=stride, length=length, count=count, mode=1,
+                                                 threads=8))
