@@ -180,7 +180,7 @@ __global__ void __launch_bounds__(kBlock) sstream_kernel(SSArgs a) {
       c[i] = lsum;
       lsum += n[i];
     }
-    const uint32_t incl = dev::wave_inclusive_scan(lsum);  // <= 256 x (2^19 + 1): no wrap
+    const uint32_t incl = dev::wave_inclusive_scan(lsum);  // <= 128 x (2^19 + 1): no wrap
     const uint32_t ex = incl - lsum;
     T = dev::read_lane(incl, 63);
     R = (wave_max(hi) + 15u) & ~15u;
