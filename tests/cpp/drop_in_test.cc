@@ -9,9 +9,11 @@
 //       verify   -> CalculateChecksum(...) == 0                      (socket-manager.h:182)
 //   drop_in_test layout                      header field layout / H2N / flags / operator<<
 //   drop_in_test batch <n> <seed>            PacketBatch (GPU) vs per-packet CalculateChecksum
+//   drop_in_test segment <bytes> <win> <seed> tcpck_batch_segment (GPU) vs the per-packet send path
 #include <tcp_stack/packet-batch.h>
 #include <tcp_stack/tcp-header.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -164,10 +166,78 @@ static int Batch(size_t n, unsigned seed) {
   return bad == 0 ? 0 : 1;
 }
 
+// The send path of INTEGRATION.md section 2 in C++: the header template built
+// with the drop-in, one tcpck_batch_segment call on a device-resident stream,
+// and every image compared byte for byte with the per-packet reference
+// sequence (MakeTcpPacket + payload, TcpLength, Estab's ACK/seq/ack,
+// addresses, TcpHeaderH2N, zero + CalculateChecksum) built with the drop-in.
+static int Segment(size_t bytes, uint32_t window, unsigned seed) {
+  std::mt19937_64 rng(seed);
+  std::vector<char> stream(bytes);
+  for (auto &c : stream) c = static_cast<char>(rng());
+  const uint32_t host_ip = 0x0A000001u, peer_ip = 0x0A000002u, snd_nxt = 0xFFFFF000u, rcv_nxt = 4242;
+  const uint16_t host_port = 15500, peer_port = 15501;
+  TcpHeader hdr;  // INTEGRATION.md section 2, verbatim
+  hdr.SetAck(true);
+  hdr.AcknowledgementNumber() = rcv_nxt;
+  hdr.SourceAddress() = host_ip;  hdr.SourcePort() = host_port;
+  hdr.DestinationAddress() = peer_ip;  hdr.DestinationPort() = peer_port;
+  TcpHeaderH2N(hdr);
+  const uint64_t n = (bytes + window - 1) / window;
+  const uint64_t stride = (32 + window + 15) / 16 * 16;
+  tcpck_ctx *ctx = nullptr;
+  if (tcpck_ctx_create(0, &ctx) != TCPCK_OK) return 3;
+  void *d_stream = nullptr, *d_slots = nullptr, *d_sums = nullptr;
+  if (tcpck_device_alloc(ctx, bytes, &d_stream) || tcpck_device_alloc(ctx, n * stride, &d_slots) ||
+      tcpck_device_alloc(ctx, n * 2, &d_sums) || tcpck_memcpy_h2d(ctx, d_stream, stream.data(), bytes))
+    return 3;
+  int st = tcpck_batch_segment(ctx, TCPCK_MODE_REF, d_stream, bytes, window, &hdr, snd_nxt, d_slots, stride,
+                               static_cast<uint16_t *>(d_sums), nullptr);
+  if (st == TCPCK_OK) st = tcpck_stream_sync(ctx, nullptr);
+  std::vector<uint8_t> slots(n * stride);
+  std::vector<uint16_t> sums(n);
+  if (st || tcpck_memcpy_d2h(ctx, slots.data(), d_slots, slots.size()) ||
+      tcpck_memcpy_d2h(ctx, sums.data(), d_sums, n * 2)) {
+    std::fprintf(stderr, "segment: %s\n", tcpck_strerror(st));
+    return 3;
+  }
+  size_t bad = 0;
+  uint32_t seq = snd_nxt;
+  for (uint64_t k = 0; k < n; ++k) {
+    const size_t len = std::min<size_t>(window, bytes - k * window);
+    auto p = MakeTcpPacket(stream.data() + k * window, len);  // GetAsTcpPacket (tcp-buffer.h:82-98)
+    TcpHeader &h = p->GetHeader();
+    h.TcpLength() = static_cast<uint16_t>(len);
+    h.SetAck(true);                                           // Estab (state.cc:178-182)
+    h.SequenceNumber() = seq;
+    h.AcknowledgementNumber() = rcv_nxt;
+    seq += h.TcpLength();
+    h.SourceAddress() = host_ip;  h.SourcePort() = host_port; // socket-internal.h:52-60
+    h.DestinationAddress() = peer_ip;  h.DestinationPort() = peer_port;
+    TcpHeaderH2N(h);
+    h.Checksum() = 0;                                         // socket-manager.h:259-260
+    h.Checksum() = CalculateChecksum(*p);
+    auto b = p->GetBuffer();
+    bad += std::memcmp(b.first, slots.data() + k * stride, b.second) != 0;
+    bad += sums[k] != h.Checksum();
+    for (size_t t = b.second; t < stride; ++t) bad += slots[k * stride + t] != 0;
+  }
+  tcpck_device_free(ctx, d_stream);
+  tcpck_device_free(ctx, d_slots);
+  tcpck_device_free(ctx, d_sums);
+  tcpck_ctx_destroy(ctx);
+  std::printf("segment bytes=%zu window=%u images=%llu mismatches=%zu\n", bytes, window,
+              static_cast<unsigned long long>(n), bad);
+  return bad == 0 ? 0 : 1;
+}
+
 int main(int argc, char **argv) {
+  if (argc >= 5 && !std::strcmp(argv[1], "segment"))
+    return Segment(std::strtoull(argv[2], nullptr, 10), static_cast<uint32_t>(std::atoi(argv[3])), std::atoi(argv[4]));
   if (argc >= 4 && !std::strcmp(argv[1], "golden")) return Golden(argv[2], argv[3]);
   if (argc >= 2 && !std::strcmp(argv[1], "layout")) return Layout();
   if (argc >= 4 && !std::strcmp(argv[1], "batch")) return Batch(std::strtoull(argv[2], nullptr, 10), std::atoi(argv[3]));
-  std::fprintf(stderr, "usage: %s golden <blob> <manifest> | layout | batch <n> <seed>\n", argv[0]);
+  std::fprintf(stderr, "usage: %s golden <blob> <manifest> | layout | batch <n> <seed> | segment <bytes> <window> <seed>\n",
+               argv[0]);
   return 2;
 }

@@ -92,6 +92,19 @@ def test_packet_batch_gpu(built_lib):
     assert "gpu_images=0" not in lines[-1]
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("nbytes,window", [(5000, 1024), (3 * 1460 + 2, 1460), (2 * 65532 + 8, 65532),
+                                           (1_000_000, 1448), (40, 4), (2, 1024), (9000 * 40 + 6, 9000)])
+def test_segment_cpp_gpu(built_lib, nbytes, window):
+    """tcpck_batch_segment from C++, with the header template built through the
+    drop-in exactly as INTEGRATION.md shows, against the per-packet send path
+    (MakeTcpPacket, Estab's fields, TcpHeaderH2N, CalculateChecksum) built with
+    the same drop-in: every image byte, checksum and zeroed slot tail."""
+    exe = build("opt")
+    lines = run(exe, "segment", nbytes, window, 11)
+    assert lines[-1].endswith("mismatches=0"), lines
+
+
 def test_loopback_c1(built_lib):
     """Config C1: segments over UDP loopback, filled and verified through the drop-in."""
     import json
