@@ -652,3 +652,58 @@ def test_auto_policy_var_slots(ctx, oracle_c, slot, mix, hint):
     np.testing.assert_array_equal(host(arena), exp_arena)
     ctx.batch_var(tcpck.OP_VERIFY, arena, d_off, d_ln, count, ok, **kw)
     assert bool(host(ok).all())
+
+
+def test_concurrent_threads_and_streams(ctx, oracle_c):
+    """The ABI is reentrant (the reference calls the checksum from
+    several threads unlocked): four host threads, each on its own HIP stream
+    and its own layout, launch batches concurrently on one ctx and on a second
+    ctx; every result equals the oracle."""
+    import threading
+    import tcpck
+    import synth_np
+    ctx2 = tcpck.Context(0)
+    rng = np.random.default_rng(77)
+    jobs = []
+    for t in range(4):
+        if t % 2 == 0:
+            L, n = (1492, 96)[t // 2], 30000
+            a = rng.integers(0, 256, n * L, dtype=np.uint8)
+            jobs.append(("fixed", a, L, n, oracle_c.batch(a, stride=L, length=L, count=n, threads=4)))
+        else:
+            off, ln, total = synth_np.mixed_layout(30000, seed=t)
+            a = rng.integers(0, 256, total, dtype=np.uint8)
+            jobs.append(("var", a, (off, ln, total), 30000, oracle_c.batch(a, off, ln, threads=4)))
+    errors = []
+
+    def worker(t):
+        try:
+            c = ctx if t < 2 else ctx2
+            s = torch.cuda.Stream()
+            kind, a, geo, n, exp = jobs[t]
+            with torch.cuda.stream(s):
+                buf = torch.from_numpy(a).cuda()
+                out = torch.empty(n, dtype=torch.int16, device="cuda")
+                if kind == "var":
+                    off, ln, total = geo
+                    d_off, d_ln = torch.from_numpy(off).cuda(), torch.from_numpy(ln).cuda()
+            s.synchronize()
+            for _ in range(50):
+                if kind == "fixed":
+                    c.batch_fixed(tcpck.OP_CHECKSUM, buf, geo, geo, n, out, stream=s)
+                else:
+                    c.batch_var(tcpck.OP_CHECKSUM, buf, d_off, d_ln, n, out, total_bytes=int(ln.sum()), packed=True,
+                                stream=s)
+            s.synchronize()
+            if not np.array_equal(out.cpu().numpy().view(np.uint16), exp):
+                errors.append(f"thread {t}: mismatch")
+        except Exception as e:  # noqa: BLE001 -- reported below
+            errors.append(f"thread {t}: {e!r}")
+
+    ths = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    ctx2.close()
+    assert not errors, errors
