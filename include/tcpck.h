@@ -59,6 +59,15 @@ extern "C" {
                                 also receives it unless out == NULL.  len >= 30 */
 #define TCPCK_OP_VERIFY 2    /* out[k] (u8) = (checksum of image k == 0)
                                 (receive path, socket-manager.h:182)            */
+#define TCPCK_OP_RECEIVE 3   /* ReceivePacket's front half (socket-manager.h:
+                                182-184): out[k] (u8) as VERIFY, on the network-
+                                order image; then image k's 32-B header is
+                                converted to host order in place (TcpHeaderN2H,
+                                see tcpck_batch_header_swap).  Images >= 32 B.
+                                The VERIFY pass, then the header pass, on the
+                                stream.  Device batches only (not
+                                tcpck_host_batch_*).  tcpck_batch_receive can
+                                write the headers to a dense array instead. */
 
 /* ---- layout hints (tcpck_layout.flags) ---------------------------------- */
 #define TCPCK_LAYOUT_PACKED 1u /* images are back to back in index order:
@@ -140,6 +149,39 @@ int tcpck_batch_var(tcpck_ctx *ctx, int op, int mode, void *d_arena,
 int tcpck_batch_set_ack(tcpck_ctx *ctx, int mode, void *d_arena, const uint64_t *d_offsets,
                         uint64_t stride, uint64_t count, const uint32_t *d_acks, uint32_t ack,
                         uint16_t *d_out, tcpck_stream stream);
+
+/* ---- batched header byte order: TcpHeaderN2H / TcpHeaderH2N -------------
+ * ReceivePacket verifies the network-order image and then converts its header
+ * to host order (include/socket-manager.h:182-184); TcpHeaderN2H and
+ * TcpHeaderH2N (include/tcp-header.h:193-221) are the same permutation: u32
+ * byte swaps of bytes 0-3, 4-7, 16-19, 20-23 (addresses, seq, ack) and u16
+ * swaps of 10-11, 12-13, 14-15, 26-27, 30-31 (TcpLength, ports, window,
+ * urgent pointer); bytes 8-9, 24-25, 28-29 and the payload are untouched.
+ * Applied in place to the first 32 bytes of every image: image k at
+ * k * stride (d_offsets == NULL; stride even, >= 32) or at d_offsets[k]
+ * (precondition: even, image >= 32 B).  d_arena even.  A receive batch is
+ * tcpck_batch_*(TCPCK_OP_VERIFY) then this call on the same stream.
+ * Asynchronous on `stream`. */
+#define TCPCK_HEADER_BYTES 32
+int tcpck_batch_header_swap(tcpck_ctx *ctx, void *d_arena, const uint64_t *d_offsets,
+                            uint64_t stride, uint64_t count, tcpck_stream stream);
+
+/* ---- batched receive: verdicts + host-order headers -----------------------
+ * ReceivePacket's front half (include/socket-manager.h:181-185) for a batch:
+ * d_ok[k] (u8) = (CalculateChecksum(image k) == 0) on the network-order
+ * image, and image k's header in host order (TcpHeaderN2H).  Layout: image k
+ * at k * stride, `len` bytes (d_offsets == NULL; len >= 32, even) or at
+ * d_offsets[k], d_lengths[k] bytes (precondition: >= 32; `layout` as in
+ * tcpck_batch_var, may be NULL).  d_arena even.
+ *   d_hdr == NULL: headers converted in place (== TCPCK_OP_RECEIVE);
+ *   d_hdr != NULL: 4-B aligned, 32 * count bytes: header k in host order at
+ *                  d_hdr + 32 k, the arena left as received.  One dense array
+ *                  of whole lines instead of one partial-line write per image
+ *                  (the cheaper form on this part, DESIGN.md "Receive path").
+ * Asynchronous on `stream`. */
+int tcpck_batch_receive(tcpck_ctx *ctx, int mode, void *d_arena, uint64_t stride, uint32_t len,
+                        const uint64_t *d_offsets, const uint32_t *d_lengths, uint64_t count,
+                        uint8_t *d_ok, void *d_hdr, const tcpck_layout *layout, tcpck_stream stream);
 
 /* ---- batched segmentation: send stream -> checksummed images -------------
  * The data-segment send path in one device pass.  The reference, per segment:

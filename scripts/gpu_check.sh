@@ -78,6 +78,8 @@ for s in ${STEPS:-tests smoke bench prof}; do
     gsprobe) step gsprobe 600 python scripts/gstream_probe.py ;;
     resend) step resend_tests 300 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread -k set_ack &&
       step resend 300 python scripts/resend_probe.py ;;
+    receive) step receive_tests 300 python -u -m pytest tests/test_gpu_receive.py -x -q --timeout 120 --timeout-method thread &&
+      step receive 300 python scripts/receive_probe.py ;;
     fillpol) step fillpol 300 python scripts/fill_write_probe.py --store-policy ;;
     pmc_rs) step pmc_rs 120 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d gpurun_out/pmc_rs -o run --output-format csv -- python3 scripts/pmc_probe.py --rs ;;
     os_c5x) step os_c5x 600 python scripts/oversub.py --what c5,c2 --variants 18,20,21 --ms 16,32,64,128 ;;

@@ -71,6 +71,8 @@ bool valid_op_mode(int op, int mode) {
   return (op == TCPCK_OP_CHECKSUM || op == TCPCK_OP_FILL || op == TCPCK_OP_VERIFY) &&
          (mode == TCPCK_MODE_REF || mode == TCPCK_MODE_RFC1071);
 }
+// device batches also take RECEIVE (VERIFY + TcpHeaderN2H)
+bool valid_device_op_mode(int op, int mode) { return valid_op_mode(op == TCPCK_OP_RECEIVE ? TCPCK_OP_VERIFY : op, mode); }
 
 // ---- host single-image path (product code, not the oracle) ---------------
 // SWAR over 8-byte words: the two u16 halves of each 32-bit lane are split
@@ -232,8 +234,8 @@ static bool jumbo_on_seg(int op, uint64_t len) {
   return op == TCPCK_OP_FILL ? fits && len > 24576 : fits;
 }
 
-hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t stride, uint32_t len,
-                     uint64_t count, void *out, int kernel, int param, hipStream_t s) {
+hipError_t run_fixed_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t stride, uint32_t len,
+                          uint64_t count, void *out, int kernel, int param, hipStream_t s) {
   const uint32_t num_cus = static_cast<uint32_t>(ctx->num_cus);
   if (kernel == TCPCK_KERNEL_AUTO && mode == TCPCK_MODE_RFC1071 && stride == len && len >= 512 &&
       len <= kFixedRunMaxLen) {
@@ -325,6 +327,7 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
       param = kRstreamPolicy;
     }
   }
+  if (op == TCPCK_OP_RECEIVE) op = TCPCK_OP_VERIFY;  // the header pass follows (run_fixed)
   if (kernel == TCPCK_KERNEL_RSTREAM) {
     if (stride != len || len < 16 || len > (1u << 24)) return hipErrorInvalidValue;
     tcpck::FixedStreamArgs a{};
@@ -391,9 +394,24 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
   return tcpck::launch_seg(op, mode, true, shape, a, num_cus, s);
 }
 
-hipError_t run_var(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const uint64_t *off, const uint32_t *len,
-                   uint64_t base, uint64_t count, void *out, const tcpck_layout *layout, int kernel, int param,
-                   hipStream_t s) {
+// RECEIVE = the VERIFY pass, then the header pass on the same stream (fusing
+// the header work into rstream's stream measured no faster: DESIGN.md "Receive
+// path").  hdr: host-order headers to hdr[32k, 32k + 32) instead of in place.
+hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t stride, uint32_t len,
+                     uint64_t count, void *out, int kernel, int param, hipStream_t s, uint8_t *hdr = nullptr) {
+  const hipError_t e = run_fixed_impl(ctx, op, mode, arena, stride, len, count, out, kernel, param, s);
+  if (e != hipSuccess || op != TCPCK_OP_RECEIVE) return e;
+  tcpck::HeaderArgs h{};
+  h.arena = arena;
+  h.stride = stride;
+  h.count = count;
+  h.out = hdr;
+  return tcpck::launch_header_swap(h, static_cast<uint32_t>(ctx->num_cus), s);
+}
+
+hipError_t run_var_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const uint64_t *off, const uint32_t *len,
+                        uint64_t base, uint64_t count, void *out, const tcpck_layout *layout, int kernel, int param,
+                        hipStream_t s) {
   const uint64_t typical = (layout && layout->total_bytes) ? layout->total_bytes / count : 1500;
   const bool packed = mode == TCPCK_MODE_REF && layout && (layout->flags & TCPCK_LAYOUT_PACKED);
   // packed, reference mode: vvstream for every op (any image lengths; C3 89.1%
@@ -434,6 +452,7 @@ hipError_t run_var(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const uint6
       param = kVvPolicy | (op == TCPCK_OP_FILL && typical <= kFillKeepMaxLen ? kVvKeep : 0);
     }
   }
+  if (op == TCPCK_OP_RECEIVE) op = TCPCK_OP_VERIFY;  // the header pass follows (run_var)
   if (kernel == TCPCK_KERNEL_VVSTREAM) {
     if (mode != TCPCK_MODE_REF && (param & 32)) return hipErrorInvalidValue;
     tcpck::RunArgs a{};
@@ -474,6 +493,20 @@ hipError_t run_var(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const uint6
   a.order = ((param >> 24) & 1u) ? 4u : 0xFFu;  // bit 24: XCD-chunked order, groups of 16 blocks
   const auto shape = (param & 0xFF) > 0 ? static_cast<tcpck::SegShape>((param & 0xFF) - 1) : tcpck::shape_for_len(typical);
   return tcpck::launch_seg(op, mode, false, shape, a, static_cast<uint32_t>(ctx->num_cus), s);
+}
+
+hipError_t run_var(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const uint64_t *off, const uint32_t *len,
+                   uint64_t base, uint64_t count, void *out, const tcpck_layout *layout, int kernel, int param,
+                   hipStream_t s, uint8_t *hdr = nullptr) {
+  if (op == TCPCK_OP_RECEIVE && base != 0) return hipErrorInvalidValue;  // device batches only
+  const hipError_t e = run_var_impl(ctx, op, mode, arena, off, len, base, count, out, layout, kernel, param, s);
+  if (e != hipSuccess || op != TCPCK_OP_RECEIVE) return e;
+  tcpck::HeaderArgs h{};
+  h.arena = arena;
+  h.offsets = off;
+  h.count = count;
+  h.out = hdr;
+  return tcpck::launch_header_swap(h, static_cast<uint32_t>(ctx->num_cus), s);
 }
 
 // Patches bytes 28-29 of host images after a FILL computed on the device
@@ -613,11 +646,13 @@ int tcpck_ctx_set_debug(tcpck_ctx *ctx, void *d_buf) {
 
 int tcpck_batch_fixed_ex(tcpck_ctx *ctx, int op, int mode, void *d_arena, uint64_t stride, uint32_t len,
                          uint64_t count, void *d_out, int kernel, int param, tcpck_stream stream) {
-  if (!ctx || !valid_op_mode(op, mode)) return TCPCK_EINVAL;
+  if (!ctx || !valid_device_op_mode(op, mode)) return TCPCK_EINVAL;
   if (count == 0) return TCPCK_OK;
   if (!d_arena || (len & 1) || (stride & 1) || (count > 1 && stride < len)) return TCPCK_EINVAL;
   if (!d_out && op != TCPCK_OP_FILL) return TCPCK_EINVAL;
   if (op == TCPCK_OP_FILL && len < 30) return TCPCK_EINVAL;
+  if (op == TCPCK_OP_RECEIVE && (len < TCPCK_HEADER_BYTES || (reinterpret_cast<uintptr_t>(d_arena) & 1)))
+    return TCPCK_EINVAL;
   if (count > 1 && stride > (UINT64_MAX - len) / (count - 1)) return TCPCK_EINVAL;
   if (count == 1) stride = len;  // one image: its stride is never read; the run kernels assume stride >= len
   DeviceGuard g(ctx->device);
@@ -629,9 +664,10 @@ int tcpck_batch_fixed_ex(tcpck_ctx *ctx, int op, int mode, void *d_arena, uint64
 int tcpck_batch_var_ex(tcpck_ctx *ctx, int op, int mode, void *d_arena, const uint64_t *d_offsets,
                        const uint32_t *d_lengths, uint64_t count, void *d_out, const tcpck_layout *layout,
                        int kernel, int param, tcpck_stream stream) {
-  if (!ctx || !valid_op_mode(op, mode)) return TCPCK_EINVAL;
+  if (!ctx || !valid_device_op_mode(op, mode)) return TCPCK_EINVAL;
   if (count == 0) return TCPCK_OK;
   if (!d_arena || !d_offsets || !d_lengths) return TCPCK_EINVAL;
+  if (op == TCPCK_OP_RECEIVE && (reinterpret_cast<uintptr_t>(d_arena) & 1)) return TCPCK_EINVAL;
   if (!d_out && op != TCPCK_OP_FILL) return TCPCK_EINVAL;
   DeviceGuard g(ctx->device);
   if (g.status() != hipSuccess) return hip_status(g.status());
@@ -662,6 +698,60 @@ int tcpck_batch_set_ack(tcpck_ctx *ctx, int mode, void *d_arena, const uint64_t 
   a.out = d_out;
   return hip_status(tcpck::launch_set_ack(mode, a, static_cast<uint32_t>(ctx->num_cus),
                                           static_cast<hipStream_t>(stream)));
+}
+
+// ---- receive batch: verdicts + host-order headers ------------------------------------
+int tcpck_batch_receive(tcpck_ctx *ctx, int mode, void *d_arena, uint64_t stride, uint32_t len,
+                        const uint64_t *d_offsets, const uint32_t *d_lengths, uint64_t count, uint8_t *d_ok,
+                        void *d_hdr, const tcpck_layout *layout, tcpck_stream stream) {
+  if (!d_hdr) {
+    return d_offsets ? tcpck_batch_var(ctx, TCPCK_OP_RECEIVE, mode, d_arena, d_offsets, d_lengths, count, d_ok,
+                                       layout, stream)
+                     : tcpck_batch_fixed(ctx, TCPCK_OP_RECEIVE, mode, d_arena, stride, len, count, d_ok, stream);
+  }
+  if (!ctx || !valid_device_op_mode(TCPCK_OP_VERIFY, mode)) return TCPCK_EINVAL;
+  if (count == 0) return TCPCK_OK;
+  if (!d_arena || !d_ok || (reinterpret_cast<uintptr_t>(d_arena) & 1) || (reinterpret_cast<uintptr_t>(d_hdr) & 3))
+    return TCPCK_EINVAL;
+  if (count > (UINT64_MAX >> 6)) return TCPCK_EINVAL;
+  if (!d_offsets) {
+    if ((len & 1) || (stride & 1) || len < TCPCK_HEADER_BYTES || (count > 1 && stride < len)) return TCPCK_EINVAL;
+    if (count > 1 && stride > (UINT64_MAX - len) / (count - 1)) return TCPCK_EINVAL;
+    if (count == 1) stride = len;
+  } else if (!d_lengths) {
+    return TCPCK_EINVAL;
+  }
+  DeviceGuard g(ctx->device);
+  if (g.status() != hipSuccess) return hip_status(g.status());
+  auto *arena = static_cast<uint8_t *>(d_arena);
+  auto *hdr = static_cast<uint8_t *>(d_hdr);
+  const auto s = static_cast<hipStream_t>(stream);
+  return hip_status(d_offsets ? run_var(ctx, TCPCK_OP_RECEIVE, mode, arena, d_offsets, d_lengths, 0, count, d_ok,
+                                        layout, TCPCK_KERNEL_AUTO, 0, s, hdr)
+                              : run_fixed(ctx, TCPCK_OP_RECEIVE, mode, arena, stride, len, count, d_ok,
+                                          TCPCK_KERNEL_AUTO, 0, s, hdr));
+}
+
+// ---- header byte order: TcpHeaderN2H / TcpHeaderH2N in place -----------------------
+int tcpck_batch_header_swap(tcpck_ctx *ctx, void *d_arena, const uint64_t *d_offsets, uint64_t stride,
+                            uint64_t count, tcpck_stream stream) {
+  if (!ctx) return TCPCK_EINVAL;
+  if (count == 0) return TCPCK_OK;
+  if (!d_arena || (reinterpret_cast<uintptr_t>(d_arena) & 1)) return TCPCK_EINVAL;
+  if (count > (UINT64_MAX >> 4)) return TCPCK_EINVAL;
+  if (!d_offsets) {
+    if ((stride & 1) || (count > 1 && stride < TCPCK_HEADER_BYTES)) return TCPCK_EINVAL;
+    if (count > 1 && stride > (UINT64_MAX - TCPCK_HEADER_BYTES) / (count - 1)) return TCPCK_EINVAL;
+  }
+  DeviceGuard g(ctx->device);
+  if (g.status() != hipSuccess) return hip_status(g.status());
+  tcpck::HeaderArgs a{};
+  a.arena = static_cast<uint8_t *>(d_arena);
+  a.offsets = d_offsets;
+  a.stride = stride;
+  a.count = count;
+  return hip_status(tcpck::launch_header_swap(a, static_cast<uint32_t>(ctx->num_cus),
+                                              static_cast<hipStream_t>(stream)));
 }
 
 // ---- batched segmentation: send stream -> checksummed images --------------------

@@ -117,6 +117,19 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *p, uint3
 __device__ __forceinline__ void store16_field(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint16_t v) {
   __builtin_amdgcn_raw_buffer_store_b16(v, r, static_cast<int>(voff), 0, 16);
 }
+
+// ---- TcpHeaderN2H == TcpHeaderH2N on the 32 header bytes (tcp-header.h:193-221) ----
+// v_perm_b32 selector for header dword j (header bytes 4j..4j+3): j = 0, 1, 4, 5
+// hold a u32 field (addresses, seq, ack): byte reverse; j = 3 the two u16
+// ports: swap within each half; j = 2, 6, 7: bytes 8-9 / 24-25 / 28-29 stay,
+// the upper u16 (TcpLength, window, urgent pointer) swaps.
+__device__ __forceinline__ uint32_t n2h_selector(uint32_t j) {
+  return j == 3 ? 0x02030001u : ((j == 2 || j >= 6) ? 0x02030100u : 0x00010203u);
+}
+__device__ __forceinline__ uint32_t n2h_dword(uint32_t h, uint32_t sel) {
+  return __builtin_amdgcn_perm(h, h, sel);
+}
+
 __device__ __forceinline__ u32x4 load16_buf_nt(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
   typedef unsigned v4u __attribute__((ext_vector_type(4)));
   const v4u v = __builtin_amdgcn_raw_buffer_load_b128(r, static_cast<int>(voff), static_cast<int>(soff), 2);

@@ -1,0 +1,81 @@
+// tcpck_header.hip -- batched header byte-order conversion, in place.
+//
+// The receive path verifies a packet on its network-order bytes and only then
+// converts the header to host order (ReceivePacket, include/socket-manager.h:
+// 182-184: CalculateChecksum(*packet) == 0, then TcpHeaderN2H); the send path
+// converts before its checksum (TcpHeaderH2N, socket-internal.h:196).  The two
+// conversions are the same byte permutation (tcp-header.h:193-221): u32 byte
+// swaps of SourceAddress (bytes 0-3), DestinationAddress (4-7), SequenceNumber
+// (16-19) and AcknowledgementNumber (20-23); u16 swaps of TcpLength (10-11),
+// SourcePort (12-13), DestinationPort (14-15), Window (26-27) and
+// UrgentPointer (30-31).  Bytes 8-9 (zero, PTCL), 24-25 (offset, flags) and
+// 28-29 (checksum) stay as they are.
+//
+// Layout: 8 lanes per image, lane j owns header bytes 4j..4j+3, so a wave
+// covers 8 images and each image's 32 bytes are one contiguous 8-lane group.
+// Images are only 2-B aligned (even offsets), hence two u16 accesses per lane.
+// Per image 32 bytes read and at most 28 written; like the ACK rewrite the pass
+// is bound by the scattered lines it touches (one or two per image), not by
+// streaming bandwidth.  EXTRACT (tcpck_batch_receive with a header array):
+// the arena stays as it is and header k goes to out[32k, 32k + 32) instead --
+// the writes are dense whole lines, not one partial line per image.
+#include "tcpck_device.h"
+#include "tcpck_internal.h"
+
+namespace tcpck {
+
+namespace {
+
+using dev::kBlock;
+
+__device__ __forceinline__ uint16_t bswap16(uint16_t v) { return static_cast<uint16_t>((v >> 8) | (v << 8)); }
+
+template <bool FIXED, bool EXTRACT>
+__global__ void __launch_bounds__(kBlock) header_swap_kernel(HeaderArgs a) {
+  const uint64_t step = static_cast<uint64_t>(gridDim.x) * kBlock;
+  const uint64_t total = a.count * 8;
+  for (uint64_t t = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x; t < total; t += step) {
+    const uint64_t k = t >> 3;
+    const uint32_t j = static_cast<uint32_t>(t & 7);
+    const uint64_t start = FIXED ? k * a.stride : a.offsets[k];
+    uint16_t *w = reinterpret_cast<uint16_t *>(a.arena + start) + 2 * j;
+    const uint16_t lo = w[0], hi = w[1];
+    if constexpr (EXTRACT) {
+      // dense output: lane group k writes the 32 B of header k, whole lines
+      const uint32_t h = static_cast<uint32_t>(lo) | (static_cast<uint32_t>(hi) << 16);
+      reinterpret_cast<uint32_t *>(a.out)[t] = dev::n2h_dword(h, dev::n2h_selector(j));
+    } else if (j == 0 || j == 1 || j == 4 || j == 5) {
+      // j = 0, 1, 4, 5: a u32 field (its two u16 halves trade places, each swapped)
+      w[0] = bswap16(hi);
+      w[1] = bswap16(lo);
+    } else {
+      // j = 3: two u16 ports;  j = 2, 6, 7: only the upper u16 is a swapped field
+      if (j == 3) w[0] = bswap16(lo);
+      w[1] = bswap16(hi);
+    }
+  }
+}
+
+template <bool FIXED, bool EXTRACT>
+hipError_t launch_one(const HeaderArgs &a, uint32_t num_cus, hipStream_t s) {
+  static const uint32_t per_cu = dev::resident_blocks_per_cu(header_swap_kernel<FIXED, EXTRACT>);
+  uint64_t blocks = (a.count * 8 + kBlock - 1) / kBlock;
+  // grid-stride beyond 8 resident grids (4 loads in flight per lane measured no faster:
+  // profiles/r02/receive_probe.log)
+  const uint64_t cap = static_cast<uint64_t>(per_cu) * num_cus * 8;
+  if (blocks > cap) blocks = cap;
+  hipLaunchKernelGGL((header_swap_kernel<FIXED, EXTRACT>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0, s,
+                     a);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t launch_header_swap(const HeaderArgs &a, uint32_t num_cus, hipStream_t stream) {
+  if (a.count == 0) return hipSuccess;
+  if (a.out)
+    return a.offsets ? launch_one<false, true>(a, num_cus, stream) : launch_one<true, true>(a, num_cus, stream);
+  return a.offsets ? launch_one<false, false>(a, num_cus, stream) : launch_one<true, false>(a, num_cus, stream);
+}
+
+}  // namespace tcpck

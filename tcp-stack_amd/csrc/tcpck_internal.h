@@ -137,7 +137,6 @@ struct SegmentArgs {
 // stores; + 8 default block order (else XCD-chunked).  oversub: 0 = by size
 hipError_t launch_segment(int mode, int variant, SegmentArgs a, uint32_t oversub, uint32_t num_cus,
                           hipStream_t stream);
-// timing-only streaming micro-kernels (tcpck_diag.hip)
 // ---- retransmit ACK rewrite with incremental checksum update (tcpck_resend.hip) ----
 struct AckArgs {
   uint8_t *arena;
@@ -150,6 +149,17 @@ struct AckArgs {
 };
 hipError_t launch_set_ack(int mode, const AckArgs &a, uint32_t num_cus, hipStream_t stream);
 
+// ---- header byte-order conversion, TcpHeaderN2H == TcpHeaderH2N (tcpck_header.hip) ----
+struct HeaderArgs {
+  uint8_t *arena;
+  const uint64_t *offsets;  // null: image k at k * stride
+  uint64_t stride;
+  uint64_t count;
+  uint8_t *out;             // null: convert in place; else header k -> out[32k, 32k + 32), arena untouched
+};
+hipError_t launch_header_swap(const HeaderArgs &a, uint32_t num_cus, hipStream_t stream);
+
+// timing-only streaming micro-kernels (tcpck_diag.hip)
 hipError_t launch_diag_stream(int variant, const uint8_t *buf, uint64_t bytes, uint32_t *out, uint32_t num_cus,
                               hipStream_t s);
 

@@ -32,6 +32,8 @@ MODE_RFC1071 = 1
 OP_CHECKSUM = 0
 OP_FILL = 1
 OP_VERIFY = 2
+OP_RECEIVE = 3  # VERIFY + TcpHeaderN2H in place (device batches)
+HEADER_BYTES = 32
 
 LAYOUT_PACKED = 1
 LAYOUT_SORTED = 2
@@ -56,7 +58,8 @@ EXPORTS = (
     "tcpck_host_batch_fixed", "tcpck_host_batch_var", "tcpck_ctx_set_chunk_bytes",
     "tcpck_host_alloc", "tcpck_host_free", "tcpck_device_alloc", "tcpck_device_free",
     "tcpck_memcpy_h2d", "tcpck_memcpy_d2h", "tcpck_stream_sync",
-    "tcpck_synth_fixed", "tcpck_synth_var", "tcpck_batch_segment",
+    "tcpck_synth_fixed", "tcpck_synth_var", "tcpck_batch_segment", "tcpck_batch_header_swap",
+    "tcpck_batch_receive",
 )
 
 
@@ -111,6 +114,8 @@ def lib() -> ctypes.CDLL:
         "tcpck_synth_var": (i32, [vp, vp, vp, u32, u64, u64, u64, i32, vp]),
         "tcpck_batch_segment": (i32, [vp, i32, vp, u64, u32, vp, u32, vp, u64, vp, vp]),
         "tcpck_batch_segment_ex": (i32, [vp, i32, vp, u64, u32, vp, u32, vp, u64, vp, i32, vp]),
+        "tcpck_batch_header_swap": (i32, [vp, vp, vp, u64, u64, vp]),
+        "tcpck_batch_receive": (i32, [vp, i32, vp, u64, u32, vp, vp, u64, vp, vp, ctypes.POINTER(Layout), vp]),
         # include/tcpck_tuning.h
         "tcpck_batch_fixed_ex": (i32, [vp, i32, i32, vp, u64, u32, u64, vp, i32, i32, vp]),
         "tcpck_batch_var_ex": (i32, [vp, i32, i32, vp, vp, vp, u64, vp, ctypes.POINTER(Layout), i32, i32, vp]),
@@ -248,6 +253,25 @@ class Context:
         _check(lib().tcpck_batch_set_ack(self._h, mode, _ptr(arena), _ptr(offsets), stride, count,
                                          _ptr(acks), ack & 0xFFFFFFFF, _ptr(out), _stream(stream)),
                "tcpck_batch_set_ack")
+
+    def batch_header_swap(self, arena, count: int, offsets=None, stride: int = 0, stream=None) -> None:
+        """TcpHeaderN2H (== TcpHeaderH2N, tcp-header.h:193-221) in place on the first 32 bytes of
+        every image (tcpck_batch_header_swap); after VERIFY this completes ReceivePacket's
+        front half (socket-manager.h:182-184)."""
+        _check(lib().tcpck_batch_header_swap(self._h, _ptr(arena), _ptr(offsets), stride, count,
+                                             _stream(stream)), "tcpck_batch_header_swap")
+
+    def batch_receive(self, arena, count: int, ok, hdr=None, stride: int = 0, length: int = 0, offsets=None,
+                      lengths=None, mode: int = MODE_REF, total_bytes: int = 0, min_len: int = 0, max_len: int = 0,
+                      packed: bool = False, sorted: bool = False, stream=None) -> None:
+        """ReceivePacket's front half for a batch (tcpck_batch_receive): ok[k] = verdict on the
+        network-order image; headers in host order in place (hdr None) or into hdr (32 B per image,
+        the arena left as received).  Fixed layout (stride, length) or offsets + lengths."""
+        lay = Layout(total_bytes, min_len, max_len,
+                     (LAYOUT_PACKED if packed else 0) | (LAYOUT_SORTED if sorted else 0), 0)
+        _check(lib().tcpck_batch_receive(self._h, mode, _ptr(arena), stride, length, _ptr(offsets), _ptr(lengths),
+                                         count, _ptr(ok), _ptr(hdr), ctypes.byref(lay), _stream(stream)),
+               "tcpck_batch_receive")
 
     def batch_segment(self, payload, payload_bytes: int, seg: int, hdr, seq0: int, images, stride: int,
                       out=None, mode: int = MODE_REF, param: int | None = None, stream=None) -> int:

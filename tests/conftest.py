@@ -73,6 +73,32 @@ def segment_golden():
     return SegmentGolden()
 
 
+class ReceiveGolden:
+    """tests/golden/receive_golden.{bin,json}: 96 wire images from the
+    reference's send side (24 of them damaged) and the same arena after
+    ReceivePacket's verdict + TcpHeaderN2H (socket-manager.h:181-184), with the
+    host-order fields the accessors read, from tests/golden/gen_receive.cc."""
+
+    def __init__(self):
+        with open(os.path.join(GOLDEN_DIR, "receive_golden.json")) as f:
+            meta = json.load(f)
+        blob = np.fromfile(os.path.join(GOLDEN_DIR, meta["blob"]), dtype=np.uint8)
+        assert blob.size == meta["blob_bytes"]
+        n = meta["arena_bytes"]
+        self.wire = blob[meta["wire_off"]:meta["wire_off"] + n].copy()
+        self.host = blob[meta["host_off"]:meta["host_off"] + n].copy()
+        self.offsets = np.asarray(meta["offsets"], np.uint64)
+        self.lengths = np.asarray(meta["lengths"], np.uint32)
+        self.ok = np.asarray(meta["ok"], np.uint8)
+        self.damage = np.asarray(meta["damage"])
+        self.fields = {k: np.asarray(v, np.uint64) for k, v in meta["fields"].items()}
+
+
+@pytest.fixture(scope="session")
+def receive_golden():
+    return ReceiveGolden()
+
+
 @pytest.fixture(scope="session")
 def oracle_c():
     from oracle.ref16 import Ref16C

@@ -12,3 +12,7 @@ g++ -std=c++17 -O1 -Wall -I"$REF/include" -o /tmp/tcpck_gen_golden "$HERE/gen_go
 # socket-manager.h:259-260) on known send streams.
 g++ -std=c++17 -O1 -Wall -I"$REF/include" -o /tmp/tcpck_gen_segment "$HERE/gen_segment.cc"
 /tmp/tcpck_gen_segment "$HERE" 2>/dev/null
+# Receive-path fixtures: wire images from the reference's send side, then
+# ReceivePacket's verdict + TcpHeaderN2H (socket-manager.h:181-184).
+g++ -std=c++17 -O1 -Wall -I"$REF/include" -o /tmp/tcpck_gen_receive "$HERE/gen_receive.cc"
+/tmp/tcpck_gen_receive "$HERE"
