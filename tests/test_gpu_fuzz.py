@@ -1,8 +1,9 @@
 """Randomised parity of the AUTO policy (tcpck_batch_fixed / tcpck_batch_var /
-tcpck_batch_segment): seeded random layouts -- fixed strides and lengths around
-every policy boundary, packed / sorted-with-gaps / unordered offset lists, empty
-and jumbo images, misaligned arenas, both modes, every op, right and wrong
-SORTED hints -- each checked against the oracle (oracle/ref16.c, pinned to the
+tcpck_batch_segment / tcpck_batch_receive): seeded random layouts -- fixed
+strides and lengths around every policy boundary, packed / sorted-with-gaps /
+unordered offset lists, empty and jumbo images, misaligned arenas, both modes,
+every op (RECEIVE in place and into a header array too), right and wrong SORTED
+hints -- each checked against the oracle (oracle/ref16.c, pinned to the
 reference's golden vectors).  Sizes stay small (<= 16 MB per case); the seeds
 are fixed, so a failure names a reproducible case."""
 import numpy as np
@@ -46,6 +47,28 @@ def check_fill(arena_np, offs, lens, mode, run):
     return exp_arena
 
 
+def check_receive(ctx, arena_np, mis, offs, lens, mode, seed, layout):
+    """RECEIVE on a fresh copy of the arena (ReceivePacket's front half,
+    socket-manager.h:182-184): into a header array (arena untouched) or in
+    place, by seed; verdicts and bytes against oracle.ref16.receive_np."""
+    from oracle import ref16 as R
+    buf = dev(arena_np)
+    n = len(offs)
+    ok = torch.empty(n, dtype=torch.uint8, device="cuda")
+    exp = arena_np.copy()
+    exp_ok = R.receive_np(exp[mis:], offs, lens, mode)
+    if seed % 2:
+        hdr = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
+        ctx.batch_receive(buf.data_ptr() + mis, n, ok, hdr, mode=mode, **layout)
+        o = np.asarray(offs, np.int64)
+        np.testing.assert_array_equal(host(hdr).reshape(n, 32), exp[mis:][o[:, None] + np.arange(32)[None, :]])
+        np.testing.assert_array_equal(host(buf), arena_np)
+    else:
+        ctx.batch_receive(buf.data_ptr() + mis, n, ok, None, mode=mode, **layout)
+        np.testing.assert_array_equal(host(buf), exp)
+    np.testing.assert_array_equal(host(ok), exp_ok)
+
+
 @pytest.mark.parametrize("seed", range(200))
 def test_fuzz_fixed(ctx, oracle_c, seed):
     import tcpck
@@ -82,6 +105,9 @@ def test_fuzz_fixed(ctx, oracle_c, seed):
         exp_arena = check_fill(view, offs, lens, mode, run)
         np.testing.assert_array_equal(host(buf)[mis:], exp_arena, err_msg=f"{stride}/{length}x{count} fill arena")
         np.testing.assert_array_equal(host(buf)[:mis], arena_np[:mis])
+    if length >= 32 and mis % 2 == 0:
+        check_receive(ctx, arena_np, mis, np.arange(count, dtype=np.int64) * stride, np.full(count, length, np.uint32),
+                      mode, seed, dict(stride=stride, length=length))
 
 
 @pytest.mark.parametrize("seed", range(200))
@@ -142,6 +168,9 @@ def test_fuzz_var(ctx, oracle_c, seed):
             return host(out).view(np.uint16)
         exp_arena = check_fill(view, off, ln, mode, run)
         np.testing.assert_array_equal(host(buf)[mis:], exp_arena, err_msg=f"{kind}/{dist} fill arena")
+    if ln.min() >= 32 and kind != "unordered":  # RECEIVE's in-place headers must not overlap
+        check_receive(ctx, arena_np, mis, off.astype(np.int64), ln, mode, seed,
+                      dict(offsets=d_off, lengths=d_ln, **hints))
 
 
 @pytest.mark.parametrize("seed", range(80))
