@@ -62,10 +62,18 @@ EXTRA = {
     # the device-resident receive arena: 1M 2048-B slots, one datagram per slot
     "slots": ("receive slots: 1M x 2048-B slots, images of 96/608/1492 B (C3's mix), offset list, "
               "TCPCK_LAYOUT_SORTED, VERIFY", "slots", 1 << 20, 2048),
+    # the receive path's front half on the same ring: verdicts + host-order headers into a dense array
+    "receive": ("receive ring: 1M x 2048-B slots, images of 96/608/1492 B, offset list, TCPCK_LAYOUT_SORTED; "
+                "tcpck_batch_receive: verdicts + TcpHeaderN2H into a 32-B-per-image header array",
+                "receive", 1 << 20, 2048),
     # the send path's producer: a 1.5 GB send stream cut into MSS segments
     "segment": ("send stream 1.5 GiB -> 1460-B segments in 1504-B slots (header template + payload, "
                 "checksum filled; tcpck_batch_segment)", "segment", (1460 << 20) + 2, 1460),
 }
+
+
+IMAGE_BYTES = {"slots": "96/608/1492 in 2048-B slots", "receive": "96/608/1492 in 2048-B slots",
+               "segment": "32 + 1460 in 1504-B slots"}
 
 
 def log(*a):
@@ -157,7 +165,7 @@ def main():
     else:
         first = rank * count  # weak: every rank checksums its own batch of the config's size
     extra_bytes = 0  # algorithmic bytes per launch beyond the image bytes read (+2 per result)
-    if kind == "slots":
+    if kind in ("slots", "receive"):
         rng = np.random.default_rng(42 + rank)
         ln = (np.asarray((64, 576, 1460), np.uint32)[rng.integers(0, 3, count)] + 32).astype(np.uint32)
         off = np.arange(count, dtype=np.uint64) * np.uint64(L)
@@ -167,9 +175,17 @@ def main():
         img_bytes = int(ln.astype(np.int64).sum())
         lmin, lmax = int(ln.min()), int(ln.max())
 
-        def step(out):
-            ctx.batch_var(tcpck.OP_VERIFY, arena, d_off, d_ln, count, out, total_bytes=img_bytes,
-                          min_len=lmin, max_len=lmax, sorted=True, stream=stream)
+        if kind == "slots":
+            def step(out):
+                ctx.batch_var(tcpck.OP_VERIFY, arena, d_off, d_ln, count, out, total_bytes=img_bytes,
+                              min_len=lmin, max_len=lmax, sorted=True, stream=stream)
+        else:
+            hdr_out = torch.empty(count * 32, dtype=torch.uint8, device="cuda")
+            extra_bytes = 32 * count  # the header array written
+
+            def step(out):
+                ctx.batch_receive(arena, count, out, hdr_out, offsets=d_off, lengths=d_ln, total_bytes=img_bytes,
+                                  min_len=lmin, max_len=lmax, sorted=True, stream=stream)
     elif kind == "segment":
         P, seg, stride = count, L, 1504
         payload = torch.empty(P, dtype=torch.uint8, device="cuda")
@@ -204,7 +220,8 @@ def main():
         def step(out):
             ctx.batch_var(tcpck.OP_CHECKSUM, arena, d_off, d_ln, count, out, total_bytes=img_bytes,
                           min_len=lmin, max_len=lmax, packed=True, stream=stream)
-    out = torch.empty(count, dtype=torch.int16 if kind != "slots" else torch.uint8, device="cuda")
+    verdicts = kind in ("slots", "receive")  # u8 results
+    out = torch.empty(count, dtype=torch.uint8 if verdicts else torch.int16, device="cuda")
     torch.cuda.synchronize()
 
     # Settle: an idle MI355X takes 10-50 ms of back-to-back HBM streaming to
@@ -269,7 +286,7 @@ def main():
             dist.destroy_process_group()
         return
 
-    algo_bytes = img_bytes + extra_bytes + (2 if kind != "slots" else 1) * count  # + the results written
+    algo_bytes = img_bytes + extra_bytes + (1 if verdicts else 2) * count  # + the results written
     achieved = algo_bytes / (launch_ms * 1e-3) / 1e9
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(args.config),
@@ -280,6 +297,9 @@ def main():
     metric = METRIC
     if kind == "slots":
         metric = "GiB/s device-resident TCP verify over a slotted receive arena (image bytes); % HBM roofline"
+    elif kind == "receive":
+        metric = ("GiB/s device-resident TCP receive (verify + TcpHeaderN2H into a header array) over a slotted "
+                  "receive arena (image bytes); % HBM roofline (read + write)")
     elif kind == "segment":
         metric = "GiB/s of device-resident send stream segmented into checksummed images; % HBM roofline (read + write)"
     rec = {
@@ -288,8 +308,7 @@ def main():
         "higher_is_better": True,
         "scaling": "strong" if args.config in STRONG else "weak", "vs_baseline": None, "dtype": "u16",
         "data": "synthetic (device-generated: send-path headers + splitmix64 payloads, seed 42)",
-        "config": {"workload": desc, "images_per_gpu": count, "image_bytes": {"slots": "96/608/1492 in 2048-B slots", "segment": "32 + 1460 in 1504-B slots"}.get(
-                       kind, L if L else "96/608/1492"),
+        "config": {"workload": desc, "images_per_gpu": count, "image_bytes": IMAGE_BYTES.get(kind, L if L else "96/608/1492"),
                    "bytes_per_gpu": img_bytes, "parallelism": f"shard{world} (independent per-GPU batches, no collective)"},
         "roofline": roofline,
         "settle": {"ms": round(settle_ms, 1), "launches": settled,

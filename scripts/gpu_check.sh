@@ -105,7 +105,9 @@ for s in ${STEPS:-tests smoke bench prof}; do
     segtests2) step segtests2 600 python -u -m pytest tests/test_gpu_segment.py tests/test_gpu_sstream.py -x -q --timeout 300 --timeout-method thread ;;
     prof_c4) step prof_c4 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c4 -o run --output-format csv -- python3 bench.py --config c4 --steps 10 --warmup 2 --no-cpu-baseline --no-e2e ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-e2e ;;
-    pmc_c2|pmc_c3|pmc_c4|pmc_slots|pmc_segment)  # separate FETCH_SIZE / WRITE_SIZE passes (TCC slots), kernel trace only
+    bench_receive) step bench_receive 600 python bench.py --config receive ;;
+    prof_receive) step prof_receive 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_receive -o run --output-format csv -- python3 bench.py --config receive --steps 10 --warmup 2 --no-cpu-baseline --no-e2e ;;
+    pmc_c2|pmc_c3|pmc_c4|pmc_slots|pmc_segment|pmc_receive)  # separate FETCH_SIZE / WRITE_SIZE passes (TCC slots), kernel trace only
       c=${s#pmc_}
       step ${s}_fetch 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d gpurun_out/pmc_${c}_fetch -o run --output-format csv -- python3 bench.py --config $c --steps 3 --warmup 1 --settle-ms 0 --no-cpu-baseline --no-e2e
       step ${s}_write 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d gpurun_out/pmc_${c}_write -o run --output-format csv -- python3 bench.py --config $c --steps 3 --warmup 1 --settle-ms 0 --no-cpu-baseline --no-e2e ;;

@@ -21,20 +21,23 @@ import statistics
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = ("rstream_kernel", "vvstream_kernel", "seg_kernel", "jumbo_kernel", "sstream_kernel", "segment_kernel")
+KERNELS = ("rstream_kernel", "vvstream_kernel", "seg_kernel", "jumbo_kernel", "sstream_kernel", "segment_kernel",
+           "header_swap_kernel")
 
 
 def per_launch(path: str, counter: str):
-    vals, name = [], None
+    """Mean counter value per launch of each step kernel, summed over the step's
+    kernels (one for every config but `receive`: VERIFY, then the header pass)."""
+    vals: dict[str, list[float]] = {}
     with open(path) as f:
         for r in csv.DictReader(f):
-            if r["Counter_Name"] != counter or not any(k in r["Kernel_Name"] for k in KERNELS):
+            key = next((k for k in KERNELS if k in r["Kernel_Name"]), None)
+            if r["Counter_Name"] != counter or key is None:
                 continue
-            name = r["Kernel_Name"]
-            vals.append(float(r["Counter_Value"]))
+            vals.setdefault(key, []).append(float(r["Counter_Value"]))
     if not vals:
         raise SystemExit(f"no checksum-kernel rows for {counter} in {path}")
-    return name, statistics.mean(vals), len(vals)
+    return " + ".join(sorted(vals)), sum(statistics.mean(v) for v in vals.values()), min(len(v) for v in vals.values())
 
 
 def main(rnd: str = "r01") -> None:
@@ -47,7 +50,7 @@ def main(rnd: str = "r01") -> None:
             summary = json.load(f)
     except (OSError, ValueError):
         summary = {}
-    for cfg in ("c2", "c3", "c4", "slots", "segment"):
+    for cfg in ("c2", "c3", "c4", "slots", "segment", "receive"):
         fp = os.path.join(src, f"pmc_{cfg}_fetch", "run_counter_collection.csv")
         wp = os.path.join(src, f"pmc_{cfg}_write", "run_counter_collection.csv")
         if not (os.path.exists(fp) and os.path.exists(wp)):

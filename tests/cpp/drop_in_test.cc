@@ -10,6 +10,7 @@
 //   drop_in_test layout                      header field layout / H2N / flags / operator<<
 //   drop_in_test batch <n> <seed>            PacketBatch (GPU) vs per-packet CalculateChecksum
 //   drop_in_test segment <bytes> <win> <seed> tcpck_batch_segment (GPU) vs the per-packet send path
+//   drop_in_test receive <n> <slot> <seed>    tcpck_batch_receive (GPU) vs ReceivePacket's verdict + N2H
 #include <tcp_stack/packet-batch.h>
 #include <tcp_stack/tcp-header.h>
 
@@ -231,13 +232,97 @@ static int Segment(size_t bytes, uint32_t window, unsigned seed) {
   return bad == 0 ? 0 : 1;
 }
 
+// The receive path of INTEGRATION.md section 2 in C++: datagrams in the slots
+// of a device ring, one tcpck_batch_receive call (verdicts + host-order
+// headers into a dense array, then in place), against ReceivePacket's front
+// half per packet with the drop-in (MakeNetPacket, CalculateChecksum == 0,
+// TcpHeaderN2H; socket-manager.h:181-184).
+static int Receive(size_t n, uint32_t slot, unsigned seed) {
+  std::mt19937_64 rng(seed);
+  std::vector<uint8_t> ring(n * slot, 0);
+  std::vector<uint64_t> offsets(n);
+  std::vector<uint32_t> lengths(n);
+  for (size_t k = 0; k < n; ++k) {
+    const size_t len = (rng() % ((slot - 32) / 2 + 1)) * 2;  // even payloads, 0 .. slot - 32
+    auto p = MakeTcpPacket(len);
+    for (char *c = p->begin(); c != p->end(); ++c) *c = static_cast<char>(rng());
+    TcpHeader &h = p->GetHeader();
+    h.SourceAddress() = static_cast<uint32_t>(rng());
+    h.DestinationAddress() = static_cast<uint32_t>(rng());
+    h.PTCL() = 6;
+    h.TcpLength() = static_cast<uint16_t>(len);
+    h.SourcePort() = static_cast<uint16_t>(rng());
+    h.DestinationPort() = static_cast<uint16_t>(rng());
+    h.SequenceNumber() = static_cast<uint32_t>(rng());
+    h.AcknowledgementNumber() = static_cast<uint32_t>(rng());
+    h.SetAck(k & 1);
+    h.SetSyn(k % 5 == 0);
+    h.Window() = static_cast<uint16_t>(rng());
+    TcpHeaderH2N(h);
+    h.Checksum() = 0;
+    h.Checksum() = CalculateChecksum(*p);
+    auto b = p->GetBuffer();
+    offsets[k] = k * slot;
+    lengths[k] = static_cast<uint32_t>(b.second);
+    std::memcpy(ring.data() + offsets[k], b.first, b.second);
+    if (k % 7 == 3) ring[offsets[k] + rng() % b.second] ^= 0x04;  // a damaged datagram
+  }
+  tcpck_ctx *ctx = nullptr;
+  if (tcpck_ctx_create(0, &ctx) != TCPCK_OK) return 3;
+  void *d_ring = nullptr, *d_off = nullptr, *d_len = nullptr, *d_ok = nullptr, *d_hdr = nullptr;
+  if (tcpck_device_alloc(ctx, ring.size(), &d_ring) || tcpck_device_alloc(ctx, n * 8, &d_off) ||
+      tcpck_device_alloc(ctx, n * 4, &d_len) || tcpck_device_alloc(ctx, n, &d_ok) ||
+      tcpck_device_alloc(ctx, n * 32, &d_hdr) || tcpck_memcpy_h2d(ctx, d_ring, ring.data(), ring.size()) ||
+      tcpck_memcpy_h2d(ctx, d_off, offsets.data(), n * 8) || tcpck_memcpy_h2d(ctx, d_len, lengths.data(), n * 4))
+    return 3;
+  uint64_t bytes = 0;
+  for (auto l : lengths) bytes += l;
+  tcpck_layout lay = {bytes, 32, slot, TCPCK_LAYOUT_SORTED, 0};
+  auto *off = static_cast<const uint64_t *>(d_off);
+  auto *len = static_cast<const uint32_t *>(d_len);
+  auto *okp = static_cast<uint8_t *>(d_ok);
+  std::vector<uint8_t> ok(n), ok2(n), hdrs(n * 32), after(ring.size());
+  int st = tcpck_batch_receive(ctx, TCPCK_MODE_REF, d_ring, 0, 0, off, len, n, okp, d_hdr, &lay, nullptr);
+  if (st == TCPCK_OK) st = tcpck_stream_sync(ctx, nullptr);
+  if (st || tcpck_memcpy_d2h(ctx, ok.data(), d_ok, n) || tcpck_memcpy_d2h(ctx, hdrs.data(), d_hdr, n * 32) ||
+      tcpck_memcpy_d2h(ctx, after.data(), d_ring, ring.size()))
+    return 3;
+  size_t bad = after != ring;  // the header array leaves the ring as received
+  st = tcpck_batch_receive(ctx, TCPCK_MODE_REF, d_ring, 0, 0, off, len, n, okp, nullptr, &lay, nullptr);
+  if (st == TCPCK_OK) st = tcpck_stream_sync(ctx, nullptr);
+  if (st || tcpck_memcpy_d2h(ctx, ok2.data(), d_ok, n) || tcpck_memcpy_d2h(ctx, after.data(), d_ring, ring.size())) {
+    std::fprintf(stderr, "receive: %s\n", tcpck_strerror(st));
+    return 3;
+  }
+  size_t damaged = 0;
+  for (size_t k = 0; k < n; ++k) {
+    // ReceivePacket (socket-manager.h:181-184), per packet, with the drop-in
+    auto p = MakeNetPacket(reinterpret_cast<const char *>(ring.data() + offsets[k]), lengths[k]);
+    const bool valid = CalculateChecksum(*p) == 0;
+    TcpHeaderN2H(p->GetHeader());
+    damaged += !valid;
+    bad += ok[k] != valid;
+    bad += ok2[k] != valid;
+    bad += std::memcmp(hdrs.data() + 32 * k, &p->GetHeader(), 32) != 0;
+    auto b = p->GetBuffer();
+    bad += std::memcmp(after.data() + offsets[k], b.first, b.second) != 0;
+    for (size_t t = b.second; t < slot; ++t) bad += after[offsets[k] + t] != 0;
+  }
+  for (void *d : {d_ring, d_off, d_len, d_ok, d_hdr}) tcpck_device_free(ctx, d);
+  tcpck_ctx_destroy(ctx);
+  std::printf("receive n=%zu slot=%u damaged=%zu mismatches=%zu\n", n, slot, damaged, bad);
+  return bad == 0 && (damaged > 0 || n <= 3) ? 0 : 1;
+}
+
 int main(int argc, char **argv) {
+  if (argc >= 5 && !std::strcmp(argv[1], "receive"))
+    return Receive(std::strtoull(argv[2], nullptr, 10), static_cast<uint32_t>(std::atoi(argv[3])), std::atoi(argv[4]));
   if (argc >= 5 && !std::strcmp(argv[1], "segment"))
     return Segment(std::strtoull(argv[2], nullptr, 10), static_cast<uint32_t>(std::atoi(argv[3])), std::atoi(argv[4]));
   if (argc >= 4 && !std::strcmp(argv[1], "golden")) return Golden(argv[2], argv[3]);
   if (argc >= 2 && !std::strcmp(argv[1], "layout")) return Layout();
   if (argc >= 4 && !std::strcmp(argv[1], "batch")) return Batch(std::strtoull(argv[2], nullptr, 10), std::atoi(argv[3]));
-  std::fprintf(stderr, "usage: %s golden <blob> <manifest> | layout | batch <n> <seed> | segment <bytes> <window> <seed>\n",
+  std::fprintf(stderr, "usage: %s golden <blob> <manifest> | layout | batch <n> <seed> | segment <bytes> <window> <seed> | receive <n> <slot> <seed>\n",
                argv[0]);
   return 2;
 }

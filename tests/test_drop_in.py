@@ -105,6 +105,18 @@ def test_segment_cpp_gpu(built_lib, nbytes, window):
     assert lines[-1].endswith("mismatches=0"), lines
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,slot", [(5000, 2048), (20000, 1536), (300, 9216), (1, 64), (4000, 48)])
+def test_receive_cpp_gpu(built_lib, n, slot):
+    """tcpck_batch_receive from C++ on a ring of datagram slots (INTEGRATION.md
+    section 2), against ReceivePacket's front half per packet through the
+    drop-in (MakeNetPacket, CalculateChecksum == 0, TcpHeaderN2H): verdicts,
+    the header array, the ring untouched by it, then the in-place form."""
+    exe = build("opt")
+    lines = run(exe, "receive", n, slot, 5)
+    assert lines[-1].endswith("mismatches=0"), lines
+
+
 def test_loopback_c1(built_lib):
     """Config C1: segments over UDP loopback, filled and verified through the drop-in."""
     import json

@@ -401,3 +401,52 @@ def test_batch_receive_rejects(ctx):
     with pytest.raises(tcpck.TcpckError):
         ctx.batch_receive(a, 4, ok, hdr, stride=64, length=64, mode=7)
     ctx.batch_receive(a, 0, ok, hdr, stride=64, length=64)                     # empty: no-op
+
+
+@pytest.mark.parametrize("slot", [64, 1536, 2048, 9216])
+@pytest.mark.parametrize("mis", [0, 16, 2, 6])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_batch_receive_hdr_ring(ctx, slot, mis, mode):
+    """A datagram ring through an offset list with the SORTED hint (the
+    compacted slot stream, then the header pass): 16-B aligned and unaligned
+    starts, both modes."""
+    from oracle import ref16 as R
+    rng = np.random.default_rng(slot + mis + 100 * mode)
+    n = max(1, min(40000, (32 << 20) // slot))
+    ln = (rng.integers(16, slot // 2 + 1, n) * 2).astype(np.uint32)
+    off = np.arange(n, dtype=np.uint64) * np.uint64(slot)
+    a = rng.integers(0, 256, n * slot + 64, dtype=np.uint8)
+    v = a[mis:]
+    for o, l in zip(off[::3], ln[::3]):  # a third of them valid, as sent
+        R.fill_np(v[int(o):int(o) + int(l)], mode)
+    buf = dev(a)
+    ok = torch.empty(n, dtype=torch.uint8, device="cuda")
+    hdr = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
+    ctx.batch_receive(buf.data_ptr() + mis, n, ok, hdr, offsets=dev(off), lengths=dev(ln), mode=mode,
+                      total_bytes=int(ln.sum()), min_len=int(ln.min()), max_len=int(ln.max()), sorted=True)
+    exp_ok = (R.ref16_batch_np(v, off, ln, mode) == 0).astype(np.uint8)
+    assert exp_ok.sum() >= len(off[::3])
+    np.testing.assert_array_equal(host(ok), exp_ok)
+    np.testing.assert_array_equal(host(hdr), _expect_hdr(v, off.astype(np.int64)))
+    np.testing.assert_array_equal(host(buf), a)
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2, 4, 8])
+def test_batch_receive_sstream_variants(ctx, variant):
+    """RECEIVE through tcpck_batch_var_ex(KERNEL_SSTREAM), every variant
+    (U4 / U8, block orders): VERIFY + the header pass, same bytes."""
+    import tcpck
+    from oracle import ref16 as R
+    rng = np.random.default_rng(variant)
+    n, slot = 30000, 2048
+    ln = (rng.integers(16, 1024, n) * 2).astype(np.uint32)
+    off = np.arange(n, dtype=np.uint64) * np.uint64(slot)
+    a = rng.integers(0, 256, n * slot, dtype=np.uint8)
+    buf = dev(a)
+    ok = torch.empty(n, dtype=torch.uint8, device="cuda")
+    ctx.batch_var_ex(tcpck.OP_RECEIVE, buf, dev(off), dev(ln), n, ok, tcpck.KERNEL_SSTREAM, variant,
+                     total_bytes=int(ln.sum()), sorted=True)
+    exp = a.copy()
+    exp_ok = R.receive_np(exp, off.astype(np.int64), ln)
+    np.testing.assert_array_equal(host(ok), exp_ok)
+    np.testing.assert_array_equal(host(buf), exp)
