@@ -207,6 +207,7 @@ constexpr uint64_t kFixedRunMaxLen = 4096;   // packed fixed: rstream up to here
 // profiles/r01/oversub_c5_first_step.log, split_probe.log); vvstream the
 // same with runs >= 8 KiB (C3 86.3 -> 89.5%, profiles/r01/xcd_first_step_probe.log).
 constexpr int kRstreamPolicy = 20;       // v_dot2 sums, buffer loads, XCD-chunked order, L2-kept first step
+constexpr int kRstreamDeferFill = 25;    // FILL: kRstreamPolicy's stream to out, then the 64-B block patch pass
 constexpr int kVvPolicy = 4 | 8 | 16;    // size policy, XCD-chunked order, L2-kept first step
 constexpr int kSegXcdOrder = 1 << 24;    // seg: XCD-chunked order
 // FILL of small images: nearly every line holds a checksum field, so the
@@ -235,8 +236,9 @@ static bool jumbo_on_seg(int op, uint64_t len) {
 }
 
 hipError_t run_fixed_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t stride, uint32_t len,
-                          uint64_t count, void *out, int kernel, int param, hipStream_t s) {
+                          uint64_t count, void *out, int kernel, int param, hipStream_t s, bool *patch) {
   const uint32_t num_cus = static_cast<uint32_t>(ctx->num_cus);
+  const bool auto_pick = kernel == TCPCK_KERNEL_AUTO;
   if (kernel == TCPCK_KERNEL_AUTO && mode == TCPCK_MODE_RFC1071 && stride == len && len >= 512 &&
       len <= kFixedRunMaxLen) {
     // RFC 1071 on packed fixed images: rstream's prefix is an exact u32 word
@@ -328,6 +330,13 @@ hipError_t run_fixed_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint
     }
   }
   if (op == TCPCK_OP_RECEIVE) op = TCPCK_OP_VERIFY;  // the header pass follows (run_fixed)
+  // FILL on rstream with a results buffer: the stream writes only the results,
+  // then a second pass rewrites each field's 64-B block whole -- never slower
+  // than the in-stream 2-B stores, 4-8 % faster at 512-768 B and 2.5-4 KiB
+  // (scripts/fill_defer_probe.py, profiles/r02/fill_defer_probe{,2}.log)
+  if (auto_pick && kernel == TCPCK_KERNEL_RSTREAM && op == TCPCK_OP_FILL && out && stride >= 64 &&
+      (param & 0xFF) == kRstreamPolicy)
+    param = (param & ~0xFF) | kRstreamDeferFill;
   if (kernel == TCPCK_KERNEL_RSTREAM) {
     if (stride != len || len < 16 || len > (1u << 24)) return hipErrorInvalidValue;
     tcpck::FixedStreamArgs a{};
@@ -340,7 +349,14 @@ hipError_t run_fixed_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint
     a.dbg = static_cast<uint64_t *>(ctx->dbg);
     a.blocks_per_cu = static_cast<uint32_t>(param >> 8) & 0xFFu;
     a.oversub = static_cast<uint32_t>(param >> 16) & 0xFFu;
-    return tcpck::launch_rstream(op, param & 0xFF, a, num_cus, s);
+    int variant = param & 0xFF;
+    if (variant == kRstreamDeferFill) {  // FILL: the policy's stream, the fields in a second pass
+      if (op != TCPCK_OP_FILL || !out || stride < 64) return hipErrorInvalidValue;
+      a.defer_field = 1;
+      *patch = true;
+      variant = kRstreamPolicy;
+    }
+    return tcpck::launch_rstream(op, variant, a, num_cus, s);
   }
   if (kernel == TCPCK_KERNEL_GSTREAM) {  // stride == len, a power of two in [32, 1024], 16-B aligned arena
     if (mode != TCPCK_MODE_REF || !tcpck::gstream_applies(arena, stride, len)) return hipErrorInvalidValue;
@@ -399,8 +415,20 @@ hipError_t run_fixed_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint
 // path").  hdr: host-order headers to hdr[32k, 32k + 32) instead of in place.
 hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t stride, uint32_t len,
                      uint64_t count, void *out, int kernel, int param, hipStream_t s, uint8_t *hdr = nullptr) {
-  const hipError_t e = run_fixed_impl(ctx, op, mode, arena, stride, len, count, out, kernel, param, s);
-  if (e != hipSuccess || op != TCPCK_OP_RECEIVE) return e;
+  bool patch = false;
+  const hipError_t e = run_fixed_impl(ctx, op, mode, arena, stride, len, count, out, kernel, param, s, &patch);
+  if (e != hipSuccess) return e;
+  if (patch) {
+    tcpck::PatchArgs p{};
+    p.arena = arena;
+    p.stride = stride;
+    p.count = count;
+    p.sums = static_cast<const uint16_t *>(out);
+    p.lo = 0;
+    p.hi = (count - 1) * stride + len;
+    return tcpck::launch_patch_fields(p, static_cast<uint32_t>(ctx->num_cus), s);
+  }
+  if (op != TCPCK_OP_RECEIVE) return e;
   tcpck::HeaderArgs h{};
   h.arena = arena;
   h.stride = stride;

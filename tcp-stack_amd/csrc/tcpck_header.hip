@@ -1,4 +1,5 @@
-// tcpck_header.hip -- batched header byte-order conversion, in place.
+// tcpck_header.hip -- batched header byte-order conversion (in place or into
+// a dense header array), and FILL's deferred field stores.
 //
 // The receive path verifies a packet on its network-order bytes and only then
 // converts the header to host order (ReceivePacket, include/socket-manager.h:
@@ -69,7 +70,53 @@ hipError_t launch_one(const HeaderArgs &a, uint32_t num_cus, hipStream_t s) {
   return hipGetLastError();
 }
 
+// FILL's field stores after the stream (PatchArgs): 4 lanes per image, lane j
+// owns 16 B of the 64-B block around the field; whole-block write-backs instead
+// of a masked 2-B write per image.
+__global__ void __launch_bounds__(kBlock) patch_fields_kernel(PatchArgs a) {
+  const uint64_t step = static_cast<uint64_t>(gridDim.x) * kBlock;
+  const uint64_t total = a.count * 4;
+  const uint64_t base = reinterpret_cast<uint64_t>(a.arena);
+  const uint64_t lo = base + a.lo, hi = base + a.hi;
+  for (uint64_t t = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x; t < total; t += step) {
+    const uint64_t k = t >> 2;
+    const uint32_t j = static_cast<uint32_t>(t & 3);
+    const uint64_t f = k * a.stride + 28;                             // the field, relative to arena
+    const uint16_t c = a.sums[k];
+    const uint64_t blk_abs = (base + f) & ~uint64_t{63};             // its 64-B block
+    const uint64_t blk = blk_abs - base;                              // (relative; valid when inside)
+    if (blk_abs < lo || blk_abs + 64 > hi) {
+      if (j == 0) *reinterpret_cast<uint16_t *>(a.arena + f) = c;
+      continue;
+    }
+    dev::u32x4 *p = reinterpret_cast<dev::u32x4 *>(a.arena + blk) + j;
+    dev::u32x4 v = *p;
+    const uint32_t r = static_cast<uint32_t>(f - blk) - 16 * j;  // field offset in this lane's 16 B
+    if (r < 16) {
+      const uint32_t sh = 16 * ((r >> 1) & 1);
+      const uint32_t m = ~(0xFFFFu << sh), x = static_cast<uint32_t>(c) << sh;
+      const uint32_t di = r >> 2;
+      v.x = di == 0 ? (v.x & m) | x : v.x;
+      v.y = di == 1 ? (v.y & m) | x : v.y;
+      v.z = di == 2 ? (v.z & m) | x : v.z;
+      v.w = di == 3 ? (v.w & m) | x : v.w;
+    }
+    *p = v;
+  }
+}
+
 }  // namespace
+
+hipError_t launch_patch_fields(const PatchArgs &a, uint32_t num_cus, hipStream_t stream) {
+  if (a.count == 0) return hipSuccess;
+  if (a.stride < 64) return hipErrorInvalidValue;  // two fields could share a block
+  static const uint32_t per_cu = dev::resident_blocks_per_cu(patch_fields_kernel);
+  uint64_t blocks = (a.count * 4 + kBlock - 1) / kBlock;
+  const uint64_t cap = static_cast<uint64_t>(per_cu) * num_cus * 8;
+  if (blocks > cap) blocks = cap;
+  hipLaunchKernelGGL(patch_fields_kernel, dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0, stream, a);
+  return hipGetLastError();
+}
 
 hipError_t launch_header_swap(const HeaderArgs &a, uint32_t num_cus, hipStream_t stream) {
   if (a.count == 0) return hipSuccess;

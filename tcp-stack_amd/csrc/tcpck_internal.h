@@ -74,6 +74,7 @@ struct FixedStreamArgs {
   uint64_t rem;            // wave w owns per_wave + (w < rem) images (no 64-bit division on device)
   uint32_t order;          // block order (dev::ordered_block; 0xFF default)
   int mode;                // kRef, or kRfc1071 (variant 20 only)
+  uint32_t defer_field;    // kFill: results to out only, the fields left for launch_patch_fields
 };
 
 // Fixed stride == len == S, S a power of two in [32, 1024], 16-B aligned arena
@@ -158,6 +159,20 @@ struct HeaderArgs {
   uint8_t *out;             // null: convert in place; else header k -> out[32k, 32k + 32), arena untouched
 };
 hipError_t launch_header_swap(const HeaderArgs &a, uint32_t num_cus, hipStream_t stream);
+
+// ---- FILL's field stores as a second pass (tcpck_header.hip) ----
+// For every image of a fixed-stride batch, the 64-B aligned block holding
+// bytes 28-29 is read and written back whole with the checksum sums[k] patched
+// in (stride >= 64: no two fields share a block); a block that leaves [lo, hi)
+// of the arena gets a 2-B store instead.
+struct PatchArgs {
+  uint8_t *arena;
+  uint64_t stride;          // image k at k * stride (stride >= 64)
+  uint64_t count;
+  const uint16_t *sums;
+  uint64_t lo, hi;          // byte range (relative to arena) the block writes may cover
+};
+hipError_t launch_patch_fields(const PatchArgs &a, uint32_t num_cus, hipStream_t stream);
 
 // timing-only streaming micro-kernels (tcpck_diag.hip)
 hipError_t launch_diag_stream(int variant, const uint8_t *buf, uint64_t bytes, uint32_t *out, uint32_t num_cus,

@@ -27,6 +27,9 @@
 //   * kFill zeroes each image's checksum word (bytes 28-29) in the stream, so
 //     the differences are the checksums of the zero-field images, and writes
 //     them into bytes 28-29 (tcp-header.h:177); kVerify stores checksum == 0.
+//     With FixedStreamArgs::defer_field, kFill writes only the results, and
+//     launch_patch_fields (tcpck_header.hip) stores the fields afterwards as
+//     whole 64-B blocks (the AUTO choice when there is a results buffer).
 #include "tcpck_device.h"
 
 namespace tcpck {
@@ -128,7 +131,8 @@ __global__ void __launch_bounds__(kBlock) rstream_kernel(FixedStreamArgs a) {
         static_cast<uint8_t *>(a.out)[k] = (c == 0) ? 1 : 0;
       } else {
         if (a.out) static_cast<uint16_t *>(a.out)[k] = c;
-        if (OP == kFill) dev::store16_field(rsrc, (out_rel + lane) * S + lead + 28, c);  // tcp-header.h:177
+        if (OP == kFill && !a.defer_field)
+          dev::store16_field(rsrc, (out_rel + lane) * S + lead + 28, c);  // tcp-header.h:177
       }
     }
   };

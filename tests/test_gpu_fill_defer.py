@@ -1,0 +1,73 @@
+"""FILL with the field stores deferred to a block pass (rstream variant 25:
+the stream writes only the results, then each field's 64-B block is rewritten
+whole): every arena byte and result against the oracle's FILL
+(socket-manager.cc:9-10), including the blocks at the batch's edges that fall
+back to 2-B stores."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def ctx(built_lib):
+    import tcpck
+    assert torch.cuda.is_available()
+    c = tcpck.Context(0)
+    yield c
+    c.close()
+
+
+@pytest.mark.parametrize("length", [64, 66, 100, 512, 514, 1024, 1460, 1492, 2048, 4094, 4096, 6000, 9000, 16384])
+@pytest.mark.parametrize("mis", [0, 2, 30, 36, 62])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_fill_defer_vs_oracle(ctx, oracle_c, length, mis, mode):
+    import tcpck
+    from oracle import ref16 as R
+    rng = np.random.default_rng(length * 8 + mis + mode)
+    count = max(1, min(20000, (16 << 20) // length))
+    a = rng.integers(0, 256, count * length + 128, dtype=np.uint8)
+    buf = torch.from_numpy(a).cuda()
+    out = torch.empty(count, dtype=torch.int16, device="cuda")
+    ctx.batch_fixed_ex(tcpck.OP_FILL, buf.data_ptr() + mis, length, length, count, out, tcpck.KERNEL_RSTREAM, 25,
+                       mode=mode)
+    torch.cuda.synchronize()
+    exp = a.copy()
+    v = exp[mis:]
+    want = np.array([R.fill_np(v[k * length:(k + 1) * length], mode) for k in range(count)], np.uint16)
+    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint16), want)
+    np.testing.assert_array_equal(buf.cpu().numpy(), exp)
+
+
+def test_fill_defer_rejects(ctx):
+    import tcpck
+    a = torch.zeros(1 << 16, dtype=torch.uint8, device="cuda")
+    out = torch.empty(1024, dtype=torch.int16, device="cuda")
+    with pytest.raises(tcpck.TcpckError):  # results are the pass's input: out required
+        ctx.batch_fixed_ex(tcpck.OP_FILL, a, 512, 512, 64, None, tcpck.KERNEL_RSTREAM, 25)
+    with pytest.raises(tcpck.TcpckError):  # CHECKSUM has no fields to defer
+        ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, a, 512, 512, 64, out, tcpck.KERNEL_RSTREAM, 25)
+
+
+@pytest.mark.parametrize("length", [512, 1492, 4096, 9000])
+@pytest.mark.parametrize("with_out", [True, False])
+def test_fill_auto_rstream(ctx, length, with_out):
+    """AUTO FILL on packed fixed images: with a results buffer the policy
+    defers the fields to the block pass, without one it stores them in the
+    stream -- same arena either way."""
+    import tcpck
+    from oracle import ref16 as R
+    rng = np.random.default_rng(length + with_out)
+    count = max(1, (8 << 20) // length)
+    a = rng.integers(0, 256, count * length, dtype=np.uint8)
+    buf = torch.from_numpy(a).cuda()
+    out = torch.empty(count, dtype=torch.int16, device="cuda") if with_out else None
+    ctx.batch_fixed(tcpck.OP_FILL, buf, length, length, count, out)
+    torch.cuda.synchronize()
+    exp = a.copy()
+    want = np.array([R.fill_np(exp[k * length:(k + 1) * length]) for k in range(count)], np.uint16)
+    if with_out:
+        np.testing.assert_array_equal(out.cpu().numpy().view(np.uint16), want)
+    np.testing.assert_array_equal(buf.cpu().numpy(), exp)
