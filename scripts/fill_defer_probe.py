@@ -49,6 +49,8 @@ def main():
         runs = [("CHECKSUM", lambda: ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, a, L, L, n, out, R, 20, stream=s)),
                 ("FILL in-stream", lambda: ctx.batch_fixed_ex(tcpck.OP_FILL, a, L, L, n, out, R, 20, stream=s)),
                 ("FILL + block pass", lambda: ctx.batch_fixed_ex(tcpck.OP_FILL, a, L, L, n, out, R, 25, stream=s))]
+        if L > 4096:  # jumbo: AUTO (seg's W-wave kernels from 24 KiB) for comparison
+            runs.append(("FILL AUTO", lambda: ctx.batch_fixed(tcpck.OP_FILL, a, L, L, n, out, stream=s)))
         for name, fn in runs:
             ms = b2b(fn, s)
             print(f"{L:5d} B x {n}: {name:18s} {ms * 1e3:8.1f} us  {(n * L + 2 * n) / ms / 1e6 / 80:5.1f} % of the roof",
