@@ -5,7 +5,8 @@ followed by a pass that rewrites each field's 64-B block whole (variant 25),
 with CHECKSUM for reference.  1.5 GB per size, median of back-to-back rounds.
 (The same pass after vvstream's stream on C3 and on 96-384 B fixed images
 lost 12-40 %, profiles/r02/fill_defer_vv_probe.log: the pass's cost grows with
-the image count, and there are many small images.)"""
+the image count, and there are many small images.  After sstream in fixed
+slots it was equal or slower, profiles/r02/fill_defer_slots_probe.log.)"""
 import os
 import sys
 import time
