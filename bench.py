@@ -66,6 +66,9 @@ EXTRA = {
     "receive": ("receive ring: 1M x 2048-B slots, images of 96/608/1492 B, offset list, TCPCK_LAYOUT_SORTED; "
                 "tcpck_batch_receive: verdicts + TcpHeaderN2H into a 32-B-per-image header array",
                 "receive", 1 << 20, 2048),
+    # the send path's insert (socket-manager.cc:9-10) on C2's layout: zero, compute, store in place
+    "fill": ("send-side FILL on C2's layout: 1M x 1492-B images, fixed stride, checksum field zeroed, computed "
+             "and stored in place, results also to a u16 array", "fill", 1 << 20, 1492),
     # the send path's producer: a 1.5 GB send stream cut into MSS segments
     "segment": ("send stream 1.5 GiB -> 1460-B segments in 1504-B slots (header template + payload, "
                 "checksum filled; tcpck_batch_segment)", "segment", (1460 << 20) + 2, 1460),
@@ -200,6 +203,14 @@ def main():
 
         def step(out):
             ctx.batch_segment(payload, P, seg, hdr, 1001, images, stride, out, stream=stream)
+    elif kind == "fill":
+        arena = torch.empty(count * L, dtype=torch.uint8, device="cuda")
+        tcpck.synth_fixed(arena, L, L, count, seed=42, first_index=first, stream=stream)
+        img_bytes = count * L
+        extra_bytes = 2 * count  # the fields written in place (+2 per result below)
+
+        def step(out):
+            ctx.batch_fixed(tcpck.OP_FILL, arena, L, L, count, out, stream=stream)
     elif kind == "fixed":
         arena = torch.empty(count * L, dtype=torch.uint8, device="cuda")
         tcpck.synth_fixed(arena, L, L, count, seed=42, first_index=first, stream=stream)
@@ -297,6 +308,8 @@ def main():
     metric = METRIC
     if kind == "slots":
         metric = "GiB/s device-resident TCP verify over a slotted receive arena (image bytes); % HBM roofline"
+    elif kind == "fill":
+        metric = "GiB/s device-resident TCP send-side fill (zero, checksum, store in place) over batched segments; % HBM roofline"
     elif kind == "receive":
         metric = ("GiB/s device-resident TCP receive (verify + TcpHeaderN2H into a header array) over a slotted "
                   "receive arena (image bytes); % HBM roofline (read + write)")

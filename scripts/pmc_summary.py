@@ -22,12 +22,13 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KERNELS = ("rstream_kernel", "vvstream_kernel", "seg_kernel", "jumbo_kernel", "sstream_kernel", "segment_kernel",
-           "header_swap_kernel")
+           "header_swap_kernel", "patch_fields_kernel")
 
 
 def per_launch(path: str, counter: str):
     """Mean counter value per launch of each step kernel, summed over the step's
-    kernels (one for every config but `receive`: VERIFY, then the header pass)."""
+    kernels (two for `receive`: VERIFY, then the header pass; and for `fill`:
+    the stream, then the field-block pass)."""
     vals: dict[str, list[float]] = {}
     with open(path) as f:
         for r in csv.DictReader(f):
@@ -50,7 +51,7 @@ def main(rnd: str = "r01") -> None:
             summary = json.load(f)
     except (OSError, ValueError):
         summary = {}
-    for cfg in ("c2", "c3", "c4", "slots", "segment", "receive"):
+    for cfg in ("c2", "c3", "c4", "slots", "segment", "receive", "fill"):
         fp = os.path.join(src, f"pmc_{cfg}_fetch", "run_counter_collection.csv")
         wp = os.path.join(src, f"pmc_{cfg}_write", "run_counter_collection.csv")
         if not (os.path.exists(fp) and os.path.exists(wp)):
