@@ -109,6 +109,8 @@ for s in ${STEPS:-tests smoke bench prof}; do
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-e2e ;;
     bench_receive) step bench_receive 600 python bench.py --config receive ;;
     bench_fill) step bench_fill 600 python bench.py --config fill ;;
+    bench_slots) step bench_slots 600 python bench.py --config slots ;;
+    bench_segment) step bench_segment 600 python bench.py --config segment ;;
     prof_fill) step prof_fill 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_fill -o run --output-format csv -- python3 bench.py --config fill --steps 10 --warmup 2 --no-cpu-baseline --no-e2e ;;
     prof_receive) step prof_receive 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_receive -o run --output-format csv -- python3 bench.py --config receive --steps 10 --warmup 2 --no-cpu-baseline --no-e2e ;;
     pmc_c2|pmc_c3|pmc_c4|pmc_slots|pmc_segment|pmc_receive|pmc_fill)  # separate FETCH_SIZE / WRITE_SIZE passes (TCC slots), kernel trace only

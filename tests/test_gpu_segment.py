@@ -136,6 +136,42 @@ def test_segment_full_size_verifies(ctx, oracle_c):
         assert cs[k] == exp_cs[0]
 
 
+def test_segment_stream_beyond_4gib(ctx):
+    """A 4.5 GB send stream (3M + 1 MSS segments, 4.7 GB of slots): offsets
+    and image indices past 2^32 bytes.  Every image verifies on the device,
+    and 256 sampled images across the stream -- the last ones included --
+    equal the restatement byte for byte (copied back one by one)."""
+    import tcpck
+    from oracle import ref16 as R
+    seg, stride = 1460, 1504
+    n_full = 3 << 20
+    P = seg * n_full + 2
+    assert P > (1 << 32)
+    payload = torch.empty(P, dtype=torch.uint8, device="cuda")
+    tcpck.synth_fixed(payload, 1492, 1492, P // 1492, seed=5)
+    n = (P + seg - 1) // seg
+    images = torch.empty(n * stride, dtype=torch.uint8, device="cuda")
+    out = torch.empty(n, dtype=torch.int16, device="cuda")
+    tmpl = np.arange(32, dtype=np.uint8)[::-1].copy()
+    ctx.batch_segment(payload, P, seg, tmpl, 0xFFFFF000, images, stride, out)
+    ok = torch.empty(n - 1, dtype=torch.uint8, device="cuda")
+    ctx.batch_fixed(tcpck.OP_VERIFY, images, stride, 32 + seg, n - 1, ok)
+    assert bool(ok.all().item())
+    last = torch.empty(1, dtype=torch.uint8, device="cuda")
+    ctx.batch_fixed(tcpck.OP_VERIFY, images[(n - 1) * stride:], stride, 32 + 2, 1, last)
+    assert int(last.item()) == 1
+    rng = np.random.default_rng(1)
+    picks = np.concatenate([rng.choice(n, 250, replace=False), [0, n // 2, n - 3, n - 2, n - 1, (1 << 32) // seg]])
+    cs = host(out).view(np.uint16)
+    for k in picks:
+        k = int(k)
+        sub = host(payload[k * seg:min(P, (k + 1) * seg)])
+        exp, _, exp_cs = R.segment_np(sub, seg, tmpl, (0xFFFFF000 + k * seg) & 0xFFFFFFFF, stride=stride)
+        np.testing.assert_array_equal(host(images[k * stride:(k + 1) * stride]), exp, err_msg=str(k))
+        assert cs[k] == exp_cs[0], k
+    del payload, images
+
+
 def test_segment_argument_errors(ctx):
     import tcpck
     p = torch.zeros(1 << 16, dtype=torch.uint8, device="cuda")
