@@ -116,7 +116,8 @@ uint16_t tcpck_update16(uint16_t checksum, uint16_t old_word, uint16_t new_word,
 
 /* ---- batched, device-resident: the hot path ------------------------------
  * Fixed stride: image k is d_arena[k*stride, k*stride + len).
- * stride and len even (stride >= len); count images.
+ * d_arena even (the u16 words of an image sit at even addresses, as in any
+ * malloc'd TcpPacket buffer); stride and len even (stride >= len); count images.
  * d_out: u16[count] (CHECKSUM/FILL) or u8[count] (VERIFY).
  * Asynchronous on `stream`; nothing is allocated; no host synchronisation. */
 int tcpck_batch_fixed(tcpck_ctx *ctx, int op, int mode, void *d_arena,
@@ -124,8 +125,8 @@ int tcpck_batch_fixed(tcpck_ctx *ctx, int op, int mode, void *d_arena,
                       tcpck_stream stream);
 
 /* Variable length: image k is d_arena[d_offsets[k], d_offsets[k] + d_lengths[k]).
- * Offsets and lengths must be even (precondition: the device arrays are not
- * read by the host).  `layout` may be NULL. */
+ * d_arena even; offsets and lengths must be even (precondition: the device
+ * arrays are not read by the host).  `layout` may be NULL. */
 int tcpck_batch_var(tcpck_ctx *ctx, int op, int mode, void *d_arena,
                     const uint64_t *d_offsets, const uint32_t *d_lengths,
                     uint64_t count, void *d_out, const tcpck_layout *layout,

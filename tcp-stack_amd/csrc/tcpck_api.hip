@@ -676,11 +676,13 @@ int tcpck_batch_fixed_ex(tcpck_ctx *ctx, int op, int mode, void *d_arena, uint64
                          uint64_t count, void *d_out, int kernel, int param, tcpck_stream stream) {
   if (!ctx || !valid_device_op_mode(op, mode)) return TCPCK_EINVAL;
   if (count == 0) return TCPCK_OK;
-  if (!d_arena || (len & 1) || (stride & 1) || (count > 1 && stride < len)) return TCPCK_EINVAL;
+  // images start at even addresses: the kernels pair bytes into u16 words by address
+  if (!d_arena || (reinterpret_cast<uintptr_t>(d_arena) & 1) || (len & 1) || (stride & 1) ||
+      (count > 1 && stride < len))
+    return TCPCK_EINVAL;
   if (!d_out && op != TCPCK_OP_FILL) return TCPCK_EINVAL;
   if (op == TCPCK_OP_FILL && len < 30) return TCPCK_EINVAL;
-  if (op == TCPCK_OP_RECEIVE && (len < TCPCK_HEADER_BYTES || (reinterpret_cast<uintptr_t>(d_arena) & 1)))
-    return TCPCK_EINVAL;
+  if (op == TCPCK_OP_RECEIVE && len < TCPCK_HEADER_BYTES) return TCPCK_EINVAL;
   if (count > 1 && stride > (UINT64_MAX - len) / (count - 1)) return TCPCK_EINVAL;
   if (count == 1) stride = len;  // one image: its stride is never read; the run kernels assume stride >= len
   DeviceGuard g(ctx->device);
@@ -694,8 +696,7 @@ int tcpck_batch_var_ex(tcpck_ctx *ctx, int op, int mode, void *d_arena, const ui
                        int kernel, int param, tcpck_stream stream) {
   if (!ctx || !valid_device_op_mode(op, mode)) return TCPCK_EINVAL;
   if (count == 0) return TCPCK_OK;
-  if (!d_arena || !d_offsets || !d_lengths) return TCPCK_EINVAL;
-  if (op == TCPCK_OP_RECEIVE && (reinterpret_cast<uintptr_t>(d_arena) & 1)) return TCPCK_EINVAL;
+  if (!d_arena || !d_offsets || !d_lengths || (reinterpret_cast<uintptr_t>(d_arena) & 1)) return TCPCK_EINVAL;
   if (!d_out && op != TCPCK_OP_FILL) return TCPCK_EINVAL;
   DeviceGuard g(ctx->device);
   if (g.status() != hipSuccess) return hip_status(g.status());
@@ -709,7 +710,7 @@ int tcpck_batch_set_ack(tcpck_ctx *ctx, int mode, void *d_arena, const uint64_t 
                         tcpck_stream stream) {
   if (!ctx || (mode != TCPCK_MODE_REF && mode != TCPCK_MODE_RFC1071)) return TCPCK_EINVAL;
   if (count == 0) return TCPCK_OK;
-  if (!d_arena) return TCPCK_EINVAL;
+  if (!d_arena || (reinterpret_cast<uintptr_t>(d_arena) & 1)) return TCPCK_EINVAL;
   if (!d_offsets) {
     if ((stride & 1) || (count > 1 && stride < 30)) return TCPCK_EINVAL;
     if (count > 1 && stride > (UINT64_MAX - 30) / (count - 1)) return TCPCK_EINVAL;

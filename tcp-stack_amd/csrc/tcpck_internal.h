@@ -163,8 +163,9 @@ hipError_t launch_header_swap(const HeaderArgs &a, uint32_t num_cus, hipStream_t
 // ---- FILL's field stores as a second pass (tcpck_header.hip) ----
 // For every image of a fixed-stride batch, the 64-B aligned block holding
 // bytes 28-29 is read and written back whole with the checksum sums[k] patched
-// in (stride >= 64: no two fields share a block); a block that leaves [lo, hi)
-// of the arena gets a 2-B store instead.
+// in (stride >= 64: no two fields share a block; the API's arenas are even, so
+// every field is a u16 inside one 16-B word); a block that leaves [lo, hi) of
+// the arena gets a 2-B store instead.
 struct PatchArgs {
   uint8_t *arena;
   uint64_t stride;          // image k at k * stride (stride >= 64)

@@ -51,6 +51,26 @@ def test_fill_defer_rejects(ctx):
         ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, a, 512, 512, 64, out, tcpck.KERNEL_RSTREAM, 25)
 
 
+
+@pytest.mark.parametrize("op", [0, 1, 2, 3])
+def test_odd_arena_rejected(ctx, op):
+    """An odd arena address puts every u16 word of the images at an odd
+    address; the kernels pair bytes by address, so the C ABI rejects it
+    (TCPCK_EINVAL) for every op and layout rather than compute other words."""
+    import tcpck
+    a = torch.zeros(1 << 16, dtype=torch.uint8, device="cuda")
+    out = torch.empty(1024, dtype=torch.int16, device="cuda")
+    off = torch.arange(16, dtype=torch.int64, device="cuda") * 1024
+    ln = torch.full((16,), 512, dtype=torch.int32, device="cuda")
+    with pytest.raises(tcpck.TcpckError):
+        ctx.batch_fixed(op, a.data_ptr() + 1, 512, 512, 64, out)
+    with pytest.raises(tcpck.TcpckError):
+        ctx.batch_var(op, a.data_ptr() + 1, off, ln, 16, out)
+    with pytest.raises(tcpck.TcpckError):
+        ctx.batch_set_ack(a.data_ptr() + 1, 16, stride=512)
+    assert not a.cpu().numpy().any()
+
+
 @pytest.mark.parametrize("length", [512, 1492, 4096, 9000])
 @pytest.mark.parametrize("with_out", [True, False])
 def test_fill_auto_rstream(ctx, length, with_out):
