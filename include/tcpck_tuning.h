@@ -86,6 +86,16 @@ extern "C" {
                                    XCD-chunked)
                                    | (grid oversubscription << 16: 0 = by batch
                                    size, M = M x the resident grid)             */
+/* FILL in TCPCK_MODE_REF with a results buffer, any kernel (param bits, OR'ed
+ * with the kernel's own param):
+ *   TCPCK_PARAM_FILL_UPDATE    the kernel's CHECKSUM pass, then a field pass that
+ *                              derives each zero-field checksum from the old field
+ *                              (c = ~(~C - f) mod 2^16) and stores it (AUTO's
+ *                              choice; fixed layouts need stride >= 64)
+ *   TCPCK_PARAM_FILL_INSTREAM  with TCPCK_KERNEL_AUTO: the field zeroed in the
+ *                              stream instead (the kernel AUTO picks for FILL) */
+#define TCPCK_PARAM_FILL_UPDATE (1 << 28)
+#define TCPCK_PARAM_FILL_INSTREAM (1 << 29)
 int tcpck_batch_fixed_ex(tcpck_ctx *ctx, int op, int mode, void *d_arena,
                          uint64_t stride, uint32_t len, uint64_t count, void *d_out,
                          int kernel, int param, tcpck_stream stream);

@@ -413,9 +413,42 @@ hipError_t run_fixed_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint
 // RECEIVE = the VERIFY pass, then the header pass on the same stream (fusing
 // the header work into rstream's stream measured no faster: DESIGN.md "Receive
 // path").  hdr: host-order headers to hdr[32k, 32k + 32) instead of in place.
+// FILL as CHECKSUM + field update (reference mode, a results buffer): the
+// layout's CHECKSUM kernel at its full streaming rate, then the patch pass
+// derives each zero-field checksum from the old field, c = ~(~C - f) mod 2^16,
+// and writes it into the field and out[k].  FILL's cost is the scattered field
+// writes, not the stream's field zeroing: the two forms tie at 1-4 KiB and on
+// receive slots, the update loses below 1 KiB (64 B 22 vs 40 %) and on C3 (52.7
+// vs 53.8 %), and wins only for jumbo images in slots (9000 B in 9216-B slots
+// 80.7 -> 83.9 %, in 16-KiB slots 75.9 -> 77.1 %; scripts/fill_update_probe.py,
+// profiles/r02/fill_update_probe.log) -- AUTO takes it there (gapped fixed
+// layouts, images > 4 KiB); elsewhere TCPCK_PARAM_FILL_UPDATE selects it.
+bool fill_by_update(int op, int mode, const void *out, int kernel, int param, bool fixed, uint64_t stride,
+                    uint32_t len) {
+  if (op != TCPCK_OP_FILL || mode != TCPCK_MODE_REF || !out) return false;
+  if (param & TCPCK_PARAM_FILL_UPDATE) return true;
+  return kernel == TCPCK_KERNEL_AUTO && !(param & TCPCK_PARAM_FILL_INSTREAM) && fixed && stride > len && len > 4096;
+}
+
 hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t stride, uint32_t len,
                      uint64_t count, void *out, int kernel, int param, hipStream_t s, uint8_t *hdr = nullptr) {
   bool patch = false;
+  if (stride >= 64 && fill_by_update(op, mode, out, kernel, param, true, stride, len)) {
+    const int p = param & ~(TCPCK_PARAM_FILL_UPDATE | TCPCK_PARAM_FILL_INSTREAM);
+    const hipError_t e = run_fixed_impl(ctx, TCPCK_OP_CHECKSUM, mode, arena, stride, len, count, out, kernel, p, s,
+                                        &patch);
+    if (e != hipSuccess) return e;
+    tcpck::PatchArgs pa{};
+    pa.arena = arena;
+    pa.stride = stride;
+    pa.count = count;
+    pa.sums = static_cast<uint16_t *>(out);
+    pa.lo = 0;
+    pa.hi = (count - 1) * stride + len;
+    pa.update = 1;
+    return tcpck::launch_patch_fields(pa, static_cast<uint32_t>(ctx->num_cus), s);
+  }
+  param &= ~(TCPCK_PARAM_FILL_UPDATE | TCPCK_PARAM_FILL_INSTREAM);
   const hipError_t e = run_fixed_impl(ctx, op, mode, arena, stride, len, count, out, kernel, param, s, &patch);
   if (e != hipSuccess) return e;
   if (patch) {
@@ -423,7 +456,7 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
     p.arena = arena;
     p.stride = stride;
     p.count = count;
-    p.sums = static_cast<const uint16_t *>(out);
+    p.sums = static_cast<uint16_t *>(out);
     p.lo = 0;
     p.hi = (count - 1) * stride + len;
     return tcpck::launch_patch_fields(p, static_cast<uint32_t>(ctx->num_cus), s);
@@ -527,6 +560,23 @@ hipError_t run_var(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const uint6
                    uint64_t base, uint64_t count, void *out, const tcpck_layout *layout, int kernel, int param,
                    hipStream_t s, uint8_t *hdr = nullptr) {
   if (op == TCPCK_OP_RECEIVE && base != 0) return hipErrorInvalidValue;  // device batches only
+  if (fill_by_update(op, mode, out, kernel, param, false, 0, 0)) {
+    const int p = param & ~(TCPCK_PARAM_FILL_UPDATE | TCPCK_PARAM_FILL_INSTREAM);
+    const hipError_t e =
+        run_var_impl(ctx, TCPCK_OP_CHECKSUM, mode, arena, off, len, base, count, out, layout, kernel, p, s);
+    if (e != hipSuccess) return e;
+    tcpck::PatchArgs pa{};
+    pa.arena = arena;
+    pa.offsets = off;
+    pa.lengths = len;
+    pa.base = base;
+    pa.count = count;
+    pa.sums = static_cast<uint16_t *>(out);
+    pa.update = 1;
+    pa.packed = (layout && (layout->flags & TCPCK_LAYOUT_PACKED)) ? 1u : 0u;
+    return tcpck::launch_patch_fields(pa, static_cast<uint32_t>(ctx->num_cus), s);
+  }
+  param &= ~(TCPCK_PARAM_FILL_UPDATE | TCPCK_PARAM_FILL_INSTREAM);
   const hipError_t e = run_var_impl(ctx, op, mode, arena, off, len, base, count, out, layout, kernel, param, s);
   if (e != hipSuccess || op != TCPCK_OP_RECEIVE) return e;
   tcpck::HeaderArgs h{};

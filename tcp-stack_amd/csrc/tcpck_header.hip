@@ -73,6 +73,7 @@ hipError_t launch_one(const HeaderArgs &a, uint32_t num_cus, hipStream_t s) {
 // FILL's field stores after the stream (PatchArgs): 4 lanes per image, lane j
 // owns 16 B of the 64-B block around the field; whole-block write-backs instead
 // of a masked 2-B write per image.
+template <bool VAR, bool UPDATE>
 __global__ void __launch_bounds__(kBlock) patch_fields_kernel(PatchArgs a) {
   const uint64_t step = static_cast<uint64_t>(gridDim.x) * kBlock;
   const uint64_t total = a.count * 4;
@@ -81,21 +82,51 @@ __global__ void __launch_bounds__(kBlock) patch_fields_kernel(PatchArgs a) {
   for (uint64_t t = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x; t < total; t += step) {
     const uint64_t k = t >> 2;
     const uint32_t j = static_cast<uint32_t>(t & 3);
-    const uint64_t f = k * a.stride + 28;                             // the field, relative to arena
-    const uint16_t c = a.sums[k];
-    const uint64_t blk_abs = (base + f) & ~uint64_t{63};             // its 64-B block
-    const uint64_t blk = blk_abs - base;                              // (relative; valid when inside)
-    if (blk_abs < lo || blk_abs + 64 > hi) {
-      if (j == 0) *reinterpret_cast<uint16_t *>(a.arena + f) = c;
+    uint64_t f;  // the field, relative to arena
+    bool blk_ok;
+    if constexpr (VAR) {
+      const uint32_t len = a.lengths[k];
+      if (len < 30) {  // no field: the plain checksum stays (UPDATE), nothing is written
+        continue;
+      }
+      const uint64_t start = a.offsets[k] - a.base;
+      f = start + 28;
+      // packed: fields >= 64 B apart and the block inside images k-1 .. k
+      blk_ok = a.packed && len >= 96 &&
+               (k > 0 ? a.lengths[k - 1] >= 64 : ((base + f) & ~uint64_t{63}) >= base + start);
+    } else {
+      f = k * a.stride + 28;
+      const uint64_t b = (base + f) & ~uint64_t{63};
+      blk_ok = b >= lo && b + 64 <= hi;
+    }
+    const uint16_t cin = a.sums[k];
+    if (!blk_ok) {
+      if (j == 0) {
+        uint16_t *p = reinterpret_cast<uint16_t *>(a.arena + f);
+        uint16_t c = cin;
+        if constexpr (UPDATE) {
+          c = static_cast<uint16_t>(~static_cast<uint16_t>(static_cast<uint16_t>(~cin) - *p));
+          a.sums[k] = c;
+        }
+        *p = c;
+      }
       continue;
     }
+    const uint64_t blk = ((base + f) & ~uint64_t{63}) - base;  // its 64-B block, relative
     dev::u32x4 *p = reinterpret_cast<dev::u32x4 *>(a.arena + blk) + j;
     dev::u32x4 v = *p;
     const uint32_t r = static_cast<uint32_t>(f - blk) - 16 * j;  // field offset in this lane's 16 B
     if (r < 16) {
       const uint32_t sh = 16 * ((r >> 1) & 1);
-      const uint32_t m = ~(0xFFFFu << sh), x = static_cast<uint32_t>(c) << sh;
       const uint32_t di = r >> 2;
+      const uint32_t d = di == 0 ? v.x : (di == 1 ? v.y : (di == 2 ? v.z : v.w));
+      uint16_t c = cin;
+      if constexpr (UPDATE) {
+        const uint16_t old = static_cast<uint16_t>(d >> sh);
+        c = static_cast<uint16_t>(~static_cast<uint16_t>(static_cast<uint16_t>(~cin) - old));
+        a.sums[k] = c;
+      }
+      const uint32_t m = ~(0xFFFFu << sh), x = static_cast<uint32_t>(c) << sh;
       v.x = di == 0 ? (v.x & m) | x : v.x;
       v.y = di == 1 ? (v.y & m) | x : v.y;
       v.z = di == 2 ? (v.z & m) | x : v.z;
@@ -105,17 +136,28 @@ __global__ void __launch_bounds__(kBlock) patch_fields_kernel(PatchArgs a) {
   }
 }
 
+template <bool VAR, bool UPDATE>
+hipError_t launch_patch(const PatchArgs &a, uint32_t num_cus, hipStream_t stream) {
+  static const uint32_t per_cu = dev::resident_blocks_per_cu(patch_fields_kernel<VAR, UPDATE>);
+  uint64_t blocks = (a.count * 4 + kBlock - 1) / kBlock;
+  const uint64_t cap = static_cast<uint64_t>(per_cu) * num_cus * 8;
+  if (blocks > cap) blocks = cap;
+  hipLaunchKernelGGL((patch_fields_kernel<VAR, UPDATE>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0, stream,
+                     a);
+  return hipGetLastError();
+}
+
 }  // namespace
 
 hipError_t launch_patch_fields(const PatchArgs &a, uint32_t num_cus, hipStream_t stream) {
   if (a.count == 0) return hipSuccess;
+  if (!a.sums) return hipErrorInvalidValue;
+  if (a.offsets) {
+    if (!a.lengths) return hipErrorInvalidValue;
+    return a.update ? launch_patch<true, true>(a, num_cus, stream) : launch_patch<true, false>(a, num_cus, stream);
+  }
   if (a.stride < 64) return hipErrorInvalidValue;  // two fields could share a block
-  static const uint32_t per_cu = dev::resident_blocks_per_cu(patch_fields_kernel);
-  uint64_t blocks = (a.count * 4 + kBlock - 1) / kBlock;
-  const uint64_t cap = static_cast<uint64_t>(per_cu) * num_cus * 8;
-  if (blocks > cap) blocks = cap;
-  hipLaunchKernelGGL(patch_fields_kernel, dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0, stream, a);
-  return hipGetLastError();
+  return a.update ? launch_patch<false, true>(a, num_cus, stream) : launch_patch<false, false>(a, num_cus, stream);
 }
 
 hipError_t launch_header_swap(const HeaderArgs &a, uint32_t num_cus, hipStream_t stream) {

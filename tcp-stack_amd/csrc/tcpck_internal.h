@@ -161,17 +161,31 @@ struct HeaderArgs {
 hipError_t launch_header_swap(const HeaderArgs &a, uint32_t num_cus, hipStream_t stream);
 
 // ---- FILL's field stores as a second pass (tcpck_header.hip) ----
-// For every image of a fixed-stride batch, the 64-B aligned block holding
-// bytes 28-29 is read and written back whole with the checksum sums[k] patched
-// in (stride >= 64: no two fields share a block; the API's arenas are even, so
-// every field is a u16 inside one 16-B word); a block that leaves [lo, hi) of
-// the arena gets a 2-B store instead.
+// For every image, the 64-B aligned block holding bytes 28-29 is read and
+// written back whole with the checksum patched in (no two fields may share a
+// block; the API's arenas are even, so every field is a u16 inside one 16-B
+// word); where that cannot be shown, a 2-B access instead.
+//   fixed stride (offsets == null): stride >= 64, blocks inside [lo, hi) of the arena;
+//   offset lists: PACKED (offsets[k+1] == offsets[k] + lengths[k], the API's
+//   contract for the flag) and lengths[k] >= 96, lengths[k-1] >= 64 -> block;
+//   otherwise (and always without PACKED) the 2-B access.
+// update == 0: sums[k] is the checksum to store (the stream zeroed the field).
+// update == 1 (REF mode only): sums[k] is the checksum of image k as it stands,
+// field included (a CHECKSUM pass), so the zero-field checksum follows exactly
+// from the old field f: c = ~(~C - f) mod 2^16 (tcp-header.h:252-263 is a sum
+// mod 2^16); c goes to the field and back to sums[k].  Images < 30 B keep
+// their plain checksum and are not written (seg's FILL does the same).
 struct PatchArgs {
   uint8_t *arena;
   uint64_t stride;          // image k at k * stride (stride >= 64)
+  const uint64_t *offsets;  // or image k at offsets[k] - base, lengths[k] bytes
+  const uint32_t *lengths;
+  uint64_t base;
   uint64_t count;
-  const uint16_t *sums;
-  uint64_t lo, hi;          // byte range (relative to arena) the block writes may cover
+  uint16_t *sums;
+  uint64_t lo, hi;          // fixed: byte range (relative to arena) the block writes may cover
+  uint32_t update;          // 1: sums hold CHECKSUM results, derive FILL's from the old field
+  uint32_t packed;          // offset lists: the PACKED contract holds
 };
 hipError_t launch_patch_fields(const PatchArgs &a, uint32_t num_cus, hipStream_t stream);
 
