@@ -83,7 +83,9 @@ extern "C" {
                                    policy = 4 steps in flight, scattered block
                                    order; 1: 4 steps in flight, 2: 8; + 4:
                                    default block order, + 8: scattered, else
-                                   XCD-chunked)
+                                   XCD-chunked; + 16, RECEIVE into a header
+                                   array only: the stream read with the default
+                                   cache policy)
                                    | (grid oversubscription << 16: 0 = by batch
                                    size, M = M x the resident grid)             */
 /* FILL in TCPCK_MODE_REF with a results buffer, any kernel (param bits, OR'ed
@@ -96,6 +98,10 @@ extern "C" {
  *                              stream instead (the kernel AUTO picks for FILL) */
 #define TCPCK_PARAM_FILL_UPDATE (1 << 28)
 #define TCPCK_PARAM_FILL_INSTREAM (1 << 29)
+/* RECEIVE into a header array (tcpck_batch_receive_ex): where the VERIFY kernel
+ * is sstream it writes each run's headers itself after the run's verdicts;
+ * this bit keeps the separate header pass instead (tuning). */
+#define TCPCK_PARAM_RECEIVE_TWO_PASS (1 << 30)
 int tcpck_batch_fixed_ex(tcpck_ctx *ctx, int op, int mode, void *d_arena,
                          uint64_t stride, uint32_t len, uint64_t count, void *d_out,
                          int kernel, int param, tcpck_stream stream);
@@ -120,6 +126,12 @@ int tcpck_batch_var_ex(tcpck_ctx *ctx, int op, int mode, void *d_arena,
                        const uint64_t *d_offsets, const uint32_t *d_lengths,
                        uint64_t count, void *d_out, const tcpck_layout *layout,
                        int kernel, int param, tcpck_stream stream);
+
+/* tcpck_batch_receive (tcpck.h) with an explicit kernel / param for the VERIFY
+ * pass (param may carry TCPCK_PARAM_RECEIVE_TWO_PASS). */
+int tcpck_batch_receive_ex(tcpck_ctx *ctx, int mode, void *d_arena, uint64_t stride, uint32_t len,
+                           const uint64_t *d_offsets, const uint32_t *d_lengths, uint64_t count, uint8_t *d_ok,
+                           void *d_hdr, const tcpck_layout *layout, int kernel, int param, tcpck_stream stream);
 
 #ifdef __cplusplus
 } /* extern "C" */

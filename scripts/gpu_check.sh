@@ -82,6 +82,9 @@ for s in ${STEPS:-tests smoke bench prof}; do
       step fdefer 300 python scripts/fill_defer_probe.py ;;
     fupd) step fupd_tests 600 python -u -m pytest tests/test_gpu_fill_update.py -x -q --timeout 120 --timeout-method thread &&
       step fupd 600 python scripts/fill_update_probe.py ;;
+    rfused) step rfused_tests 600 python -u -m pytest tests/test_gpu_receive.py -x -q --timeout 120 --timeout-method thread &&
+      step rfused 600 python scripts/receive_fused_probe.py ;;
+    copy) step copy 600 python scripts/copy_probe.py ;;
     fuzz) step fuzz_tests 600 python -u -m pytest tests/test_gpu_fuzz.py -x -q --timeout 120 --timeout-method thread ;;
     receive) step receive_tests 300 python -u -m pytest tests/test_gpu_receive.py -x -q --timeout 120 --timeout-method thread &&
       step receive 300 python scripts/receive_probe.py ;;

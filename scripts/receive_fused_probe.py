@@ -1,0 +1,97 @@
+#!/usr/bin/env python3
+"""RECEIVE into a header array on sstream layouts: the VERIFY pass followed by
+the separate header pass (TCPCK_PARAM_RECEIVE_TWO_PASS) against sstream
+writing each run's headers itself after the run's verdicts (one launch),
+with the stream read nt (variant 0) or with the default cache policy
+(variant 16, the header lines still in L2 when the run's end re-reads them).
+VERIFY alone for reference.  Results compared byte for byte.  Median of
+back-to-back rounds."""
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "tcp-stack_amd")]
+
+import torch  # noqa: E402
+import tcpck  # noqa: E402
+
+TWO = 1 << 30
+
+
+def b2b(fn, s, reps=20, rounds=5):
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < 0.3:
+        fn()
+        torch.cuda.synchronize()
+    t = []
+    for _ in range(rounds):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for _ in range(reps):
+            fn()
+        e1.record(s)
+        torch.cuda.synchronize()
+        t.append(e0.elapsed_time(e1) / reps)
+    return float(np.median(t))
+
+
+def case(ctx, s, name, n, slot, ln, fixed_len=None):
+    off = np.arange(n, dtype=np.uint64) * np.uint64(slot)
+    a = torch.empty(n * slot, dtype=torch.uint8, device="cuda")
+    d_off, d_ln = torch.from_numpy(off).cuda(), torch.from_numpy(ln).cuda()
+    tcpck.synth_var(a, d_off, d_ln, int(ln.max()), n, seed=42)
+    img = int(ln.astype(np.int64).sum())
+    ok = torch.empty(n, dtype=torch.uint8, device="cuda")
+    hdr = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
+    S = tcpck.KERNEL_SSTREAM
+    if fixed_len:
+        kw = dict(stride=slot, length=fixed_len, stream=s)
+    else:
+        kw = dict(offsets=d_off, lengths=d_ln, total_bytes=img, min_len=int(ln.min()), max_len=int(ln.max()),
+                  sorted=True, stream=s)
+
+    def verify():
+        if fixed_len:
+            ctx.batch_fixed(tcpck.OP_VERIFY, a, slot, fixed_len, n, ok, stream=s)
+        else:
+            ctx.batch_var(tcpck.OP_VERIFY, a, d_off, d_ln, n, ok, total_bytes=img, min_len=int(ln.min()),
+                          max_len=int(ln.max()), sorted=True, stream=s)
+
+    runs = [("VERIFY only", verify),
+            ("two passes", lambda: ctx.batch_receive(a, n, ok, hdr, kernel=S, param=TWO, **kw)),
+            ("fused nt", lambda: ctx.batch_receive(a, n, ok, hdr, kernel=S, param=0, **kw)),
+            ("fused keep", lambda: ctx.batch_receive(a, n, ok, hdr, kernel=S, param=16, **kw)),
+            ("AUTO", lambda: ctx.batch_receive(a, n, ok, hdr, **kw))]
+    res = {}
+    for label, fn in runs:
+        ms = b2b(fn, s)
+        if label != "VERIFY only":
+            torch.cuda.synchronize()
+            res[label] = (ok.clone(), hdr.clone())
+        alg = img + n + (0 if label == "VERIFY only" else 32 * n)
+        print(f"{name:28s} {label:12s} {ms * 1e3:8.1f} us  {alg / ms / 1e6 / 80:5.1f} % of the roof "
+              f"(image bytes + verdicts + headers)", flush=True)
+    ref = res["two passes"]
+    same = all(torch.equal(v[0], ref[0]) and torch.equal(v[1], ref[1]) for v in res.values())
+    print(f"{name:28s} results identical: {same}", flush=True)
+    del a, hdr
+
+
+def main():
+    ctx = tcpck.Context(0)
+    s = torch.cuda.current_stream()
+    rng = np.random.default_rng(42)
+    n = 1 << 20
+    mix = (np.asarray((64, 576, 1460), np.uint32)[rng.integers(0, 3, n)] + 32).astype(np.uint32)
+    case(ctx, s, "ring 1M x 2048 (bench mix)", n, 2048, mix)
+    case(ctx, s, "ring 1M x 1536 (bench mix)", n, 1536, mix)
+    case(ctx, s, "fixed 1492 in 2048-B slots", n, 2048, np.full(n, 1492, np.uint32), fixed_len=1492)
+    small = (rng.integers(16, 128, 4 * n) * 2).astype(np.uint32)
+    case(ctx, s, "ring 4M x 256 (32-254 B)", 4 * n, 256, small)
+
+
+if __name__ == "__main__":
+    main()

@@ -236,7 +236,8 @@ static bool jumbo_on_seg(int op, uint64_t len) {
 }
 
 hipError_t run_fixed_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t stride, uint32_t len,
-                          uint64_t count, void *out, int kernel, int param, hipStream_t s, bool *patch) {
+                          uint64_t count, void *out, int kernel, int param, hipStream_t s, bool *patch,
+                          uint8_t *hdr = nullptr, bool *hdr_done = nullptr) {
   const uint32_t num_cus = static_cast<uint32_t>(ctx->num_cus);
   const bool auto_pick = kernel == TCPCK_KERNEL_AUTO;
   if (kernel == TCPCK_KERNEL_AUTO && mode == TCPCK_MODE_RFC1071 && stride == len && len >= 512 &&
@@ -329,6 +330,13 @@ hipError_t run_fixed_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint
       param = kRstreamPolicy;
     }
   }
+  // RECEIVE into a header array: the header pass follows the VERIFY pass.
+  // sstream can instead write each run's headers after the run's verdicts
+  // (one launch), but those stores inside the other waves' read streams cost
+  // more than the separate pass (1492 B in 2048-B slots 302 vs 258 us, the
+  // receive ring 181 vs 156 us; scripts/receive_fused_probe.py,
+  // profiles/r02/receive_fused_probe.log): tuning only for fixed slots
+  const bool fuse_hdr = op == TCPCK_OP_RECEIVE && hdr && !auto_pick && !(param & TCPCK_PARAM_RECEIVE_TWO_PASS);
   if (op == TCPCK_OP_RECEIVE) op = TCPCK_OP_VERIFY;  // the header pass follows (run_fixed)
   // FILL on rstream with a results buffer: the stream writes only the results,
   // then a second pass rewrites each field's 64-B block whole -- never slower
@@ -381,6 +389,10 @@ hipError_t run_fixed_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint
     a.count = count;
     a.out = out;
     a.oversub = static_cast<uint32_t>(param >> 16) & 0xFFu;
+    if (fuse_hdr) {
+      a.hdr = hdr;
+      *hdr_done = true;
+    }
     return tcpck::launch_sstream(op, param & 0xFF, true, a, num_cus, s);
   }
   if (kernel == TCPCK_KERNEL_VVSTREAM) {  // any even length: the prefix table takes any number of ends per step
@@ -449,7 +461,9 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
     return tcpck::launch_patch_fields(pa, static_cast<uint32_t>(ctx->num_cus), s);
   }
   param &= ~(TCPCK_PARAM_FILL_UPDATE | TCPCK_PARAM_FILL_INSTREAM);
-  const hipError_t e = run_fixed_impl(ctx, op, mode, arena, stride, len, count, out, kernel, param, s, &patch);
+  bool hdr_done = false;
+  const hipError_t e =
+      run_fixed_impl(ctx, op, mode, arena, stride, len, count, out, kernel, param, s, &patch, hdr, &hdr_done);
   if (e != hipSuccess) return e;
   if (patch) {
     tcpck::PatchArgs p{};
@@ -461,7 +475,7 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
     p.hi = (count - 1) * stride + len;
     return tcpck::launch_patch_fields(p, static_cast<uint32_t>(ctx->num_cus), s);
   }
-  if (op != TCPCK_OP_RECEIVE) return e;
+  if (op != TCPCK_OP_RECEIVE || hdr_done) return e;
   tcpck::HeaderArgs h{};
   h.arena = arena;
   h.stride = stride;
@@ -472,9 +486,11 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
 
 hipError_t run_var_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const uint64_t *off, const uint32_t *len,
                         uint64_t base, uint64_t count, void *out, const tcpck_layout *layout, int kernel, int param,
-                        hipStream_t s) {
+                        hipStream_t s, uint8_t *hdr = nullptr, bool *hdr_done = nullptr) {
   const uint64_t typical = (layout && layout->total_bytes) ? layout->total_bytes / count : 1500;
   const bool packed = mode == TCPCK_MODE_REF && layout && (layout->flags & TCPCK_LAYOUT_PACKED);
+  bool fuse_small = false;  // RECEIVE into a header array on a ring of small datagrams (below)
+  const bool auto_pick = kernel == TCPCK_KERNEL_AUTO;
   // packed, reference mode: vvstream for every op (any image lengths; C3 89.1%
   // at 32x oversubscription, profiles/r01/c3_bench_r01_final.log).  The
   // packed flag must be true when set (tcpck.h); a wave whose lengths do not
@@ -504,6 +520,10 @@ hipError_t run_var_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const 
       // (41-58 % either way: the scattered field writes bound it)
       kernel = TCPCK_KERNEL_SSTREAM;
       param = 0;
+      if (op == TCPCK_OP_RECEIVE && hdr && typical <= 256) {
+        fuse_small = true;
+        param = 16;
+      }
     } else if (!packed || typical > kRunMaxLen ||
                (op == TCPCK_OP_FILL && layout->min_len != 0 && layout->min_len < 30)) {
       kernel = TCPCK_KERNEL_SEG;
@@ -513,6 +533,12 @@ hipError_t run_var_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const 
       param = kVvPolicy | (op == TCPCK_OP_FILL && typical <= kFillKeepMaxLen ? kVvKeep : 0);
     }
   }
+  // RECEIVE into a header array (as run_fixed_impl): the header pass, except
+  // for rings of small images (typical <= 256 B), where sstream writing each
+  // run's headers itself with a default-policy stream wins (4M 32-254-B
+  // datagrams in 256-B slots: 236 vs 259 us; receive_fused_probe.log)
+  bool fuse_hdr = op == TCPCK_OP_RECEIVE && hdr && !(param & TCPCK_PARAM_RECEIVE_TWO_PASS) &&
+                  (!auto_pick || fuse_small);
   if (op == TCPCK_OP_RECEIVE) op = TCPCK_OP_VERIFY;  // the header pass follows (run_var)
   if (kernel == TCPCK_KERNEL_VVSTREAM) {
     if (mode != TCPCK_MODE_REF && (param & 32)) return hipErrorInvalidValue;
@@ -540,6 +566,10 @@ hipError_t run_var_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const 
     a.out = out;
     a.oversub = static_cast<uint32_t>(param >> 16) & 0xFFu;
     a.total_bytes = layout ? layout->total_bytes : 0;
+    if (fuse_hdr) {
+      a.hdr = hdr;
+      *hdr_done = true;
+    }
     return tcpck::launch_sstream(op, param & 0xFF, false, a, static_cast<uint32_t>(ctx->num_cus), s);
   }
   if (kernel != TCPCK_KERNEL_SEG) return hipErrorInvalidValue;
@@ -577,8 +607,10 @@ hipError_t run_var(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const uint6
     return tcpck::launch_patch_fields(pa, static_cast<uint32_t>(ctx->num_cus), s);
   }
   param &= ~(TCPCK_PARAM_FILL_UPDATE | TCPCK_PARAM_FILL_INSTREAM);
-  const hipError_t e = run_var_impl(ctx, op, mode, arena, off, len, base, count, out, layout, kernel, param, s);
-  if (e != hipSuccess || op != TCPCK_OP_RECEIVE) return e;
+  bool hdr_done = false;
+  const hipError_t e =
+      run_var_impl(ctx, op, mode, arena, off, len, base, count, out, layout, kernel, param, s, hdr, &hdr_done);
+  if (e != hipSuccess || op != TCPCK_OP_RECEIVE || hdr_done) return e;
   tcpck::HeaderArgs h{};
   h.arena = arena;
   h.offsets = off;
@@ -783,10 +815,18 @@ int tcpck_batch_set_ack(tcpck_ctx *ctx, int mode, void *d_arena, const uint64_t 
 int tcpck_batch_receive(tcpck_ctx *ctx, int mode, void *d_arena, uint64_t stride, uint32_t len,
                         const uint64_t *d_offsets, const uint32_t *d_lengths, uint64_t count, uint8_t *d_ok,
                         void *d_hdr, const tcpck_layout *layout, tcpck_stream stream) {
+  return tcpck_batch_receive_ex(ctx, mode, d_arena, stride, len, d_offsets, d_lengths, count, d_ok, d_hdr, layout,
+                                TCPCK_KERNEL_AUTO, 0, stream);
+}
+
+int tcpck_batch_receive_ex(tcpck_ctx *ctx, int mode, void *d_arena, uint64_t stride, uint32_t len,
+                           const uint64_t *d_offsets, const uint32_t *d_lengths, uint64_t count, uint8_t *d_ok,
+                           void *d_hdr, const tcpck_layout *layout, int kernel, int param, tcpck_stream stream) {
   if (!d_hdr) {
-    return d_offsets ? tcpck_batch_var(ctx, TCPCK_OP_RECEIVE, mode, d_arena, d_offsets, d_lengths, count, d_ok,
-                                       layout, stream)
-                     : tcpck_batch_fixed(ctx, TCPCK_OP_RECEIVE, mode, d_arena, stride, len, count, d_ok, stream);
+    return d_offsets ? tcpck_batch_var_ex(ctx, TCPCK_OP_RECEIVE, mode, d_arena, d_offsets, d_lengths, count, d_ok,
+                                          layout, kernel, param, stream)
+                     : tcpck_batch_fixed_ex(ctx, TCPCK_OP_RECEIVE, mode, d_arena, stride, len, count, d_ok, kernel,
+                                            param, stream);
   }
   if (!ctx || !valid_device_op_mode(TCPCK_OP_VERIFY, mode)) return TCPCK_EINVAL;
   if (count == 0) return TCPCK_OK;
@@ -806,9 +846,9 @@ int tcpck_batch_receive(tcpck_ctx *ctx, int mode, void *d_arena, uint64_t stride
   auto *hdr = static_cast<uint8_t *>(d_hdr);
   const auto s = static_cast<hipStream_t>(stream);
   return hip_status(d_offsets ? run_var(ctx, TCPCK_OP_RECEIVE, mode, arena, d_offsets, d_lengths, 0, count, d_ok,
-                                        layout, TCPCK_KERNEL_AUTO, 0, s, hdr)
-                              : run_fixed(ctx, TCPCK_OP_RECEIVE, mode, arena, stride, len, count, d_ok,
-                                          TCPCK_KERNEL_AUTO, 0, s, hdr));
+                                        layout, kernel, param, s, hdr)
+                              : run_fixed(ctx, TCPCK_OP_RECEIVE, mode, arena, stride, len, count, d_ok, kernel,
+                                          param, s, hdr));
 }
 
 // ---- header byte order: TcpHeaderN2H / TcpHeaderH2N in place -----------------------

@@ -294,6 +294,71 @@ hipError_t launch_one(const uint8_t *buf, uint64_t bytes, uint32_t *out, uint32_
   return hipGetLastError();
 }
 
+// Device copy ceiling (timing only): the first half of buf copied to the
+// second half.  RUN: wave w copies one contiguous run in 1 KiB steps (lane l:
+// 16 B at 1024 t + 16 l), U steps in flight, nt loads; else a grid-stride float4
+// copy, U loads issued before their U stores.  SPOL: store aux bits (0
+// default, 2 nt, 16 sc1).  The measure segmentation's read + write rate is
+// judged against.
+template <int U, int SPOL, bool RUN>
+__global__ void __launch_bounds__(kBlock) diag_copy_kernel(uint8_t *buf, uint64_t bytes) {
+  const uint64_t half = (bytes >> 1) & ~uint64_t{127};
+  const uint8_t *src = buf;
+  uint8_t *dst = buf + half;
+  const uint64_t n16 = half >> 4;
+  typedef unsigned v4u __attribute__((ext_vector_type(4)));
+  if constexpr (RUN) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t W = static_cast<uint64_t>(gridDim.x) * kWavesPerBlock;
+    const uint64_t wid = static_cast<uint64_t>(blockIdx.x) * kWavesPerBlock + (threadIdx.x >> 6);
+    const uint64_t lines = half >> 7;
+    const uint64_t b0 = (wid * lines / W) << 7, b1 = ((wid + 1) * lines / W) << 7;
+    if (b0 >= b1) return;
+    const uint32_t span = static_cast<uint32_t>(b1 - b0);
+    const uint32_t nsteps = (span + 1023) >> 10;
+    const auto rs = dev::make_rsrc(src + b0, span);
+    const auto rd = dev::make_rsrc(dst + b0, span);
+    v4u ring[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      ring[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, static_cast<int>(lane << 4), static_cast<int>(u << 10), 2);
+    for (uint32_t g = 0; g < nsteps; g += U) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t st = g + u;
+        if (st < nsteps)
+          __builtin_amdgcn_raw_buffer_store_b128(ring[u], rd, static_cast<int>(lane << 4), static_cast<int>(st << 10), SPOL);
+        ring[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, static_cast<int>(lane << 4), static_cast<int>((st + U) << 10), 2);
+      }
+    }
+  } else {
+    const uint64_t T = static_cast<uint64_t>(gridDim.x) * kBlock;
+    const v4u *s4 = reinterpret_cast<const v4u *>(src);
+    v4u *d4 = reinterpret_cast<v4u *>(dst);
+    for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x; i < n16; i += U * T) {
+      v4u r[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) r[u] = i + u * T < n16 ? __builtin_nontemporal_load(s4 + i + u * T) : v4u{};
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (i + u * T < n16) {
+          if constexpr (SPOL == 2)
+            __builtin_nontemporal_store(r[u], d4 + i + u * T);
+          else
+            d4[i + u * T] = r[u];
+        }
+      }
+    }
+  }
+}
+
+template <int U, int SPOL, bool RUN>
+hipError_t launch_copy(uint8_t *buf, uint64_t bytes, uint32_t num_cus, hipStream_t s, uint32_t m) {
+  static const uint32_t per_cu = dev::resident_blocks_per_cu(diag_copy_kernel<U, SPOL, RUN>);
+  hipLaunchKernelGGL((diag_copy_kernel<U, SPOL, RUN>), dim3(per_cu * num_cus * m), dim3(kBlock), 0, s, buf, bytes);
+  return hipGetLastError();
+}
+
 }  // namespace
 
 // variant: LPB x U x scan: 0 = 1x4 scan, 1 = 1x4 no scan, 2 = 2x2 scan, 3 = 2x2 no scan,
@@ -303,6 +368,18 @@ hipError_t launch_one(const uint8_t *buf, uint64_t bytes, uint32_t *out, uint32_
 // image (w = 0 none, 1 2 B, 2 4 B, 3 16 B, 4 32 B, 5 64 B, 6 128 B)
 hipError_t launch_diag_stream(int variant, const uint8_t *buf, uint64_t bytes, uint32_t *out, uint32_t num_cus,
                               hipStream_t s) {
+  if (variant >= 0x5000) {  // copy ceiling: bits 0-1 U (2/4/8), 2-3 store policy (default/nt/sc1), 4 grid-stride,
+                            // 8-11 grid multiple (x resident, 0 = 1)
+    uint8_t *wb = const_cast<uint8_t *>(buf);
+    const uint32_t m = (variant >> 8) & 0xFu ? static_cast<uint32_t>((variant >> 8) & 0xFu) : 1u;
+    const int u = variant & 3, sp = (variant >> 2) & 3;
+    const bool gs = (variant & 16) != 0;
+#define TCPCK_COPY(UU, SS) (gs ? launch_copy<UU, SS, false>(wb, bytes, num_cus, s, m) : launch_copy<UU, SS, true>(wb, bytes, num_cus, s, m))
+    if (u == 0) return sp == 0 ? TCPCK_COPY(2, 0) : (sp == 1 ? TCPCK_COPY(2, 2) : TCPCK_COPY(2, 16));
+    if (u == 1) return sp == 0 ? TCPCK_COPY(4, 0) : (sp == 1 ? TCPCK_COPY(4, 2) : TCPCK_COPY(4, 16));
+    return sp == 0 ? TCPCK_COPY(8, 0) : (sp == 1 ? TCPCK_COPY(8, 2) : TCPCK_COPY(8, 16));
+#undef TCPCK_COPY
+  }
   if (variant >= 0x4000) {  // in-place FILL write cost with store cache-policy bits: 0x4000 | aux (2 B), 0x4100 | aux (64 B)
     uint8_t *wb = const_cast<uint8_t *>(buf);
     return (variant & 0x100) ? launch_fill_aux<64>(variant & 0xFF, wb, bytes, out, num_cus, s)

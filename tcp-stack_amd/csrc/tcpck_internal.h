@@ -59,6 +59,7 @@ struct RunArgs {
   uint64_t total_bytes;      // batch byte span hint (0 = unknown)
   uint32_t blocks_per_cu;    // vvstream: occupancy cap (LDS padding) and grid base, 0 = by resources
   int mode;                  // vvstream: kRef or kRfc1071
+  uint8_t *hdr;              // sstream VERIFY: host-order header k also to hdr + 32 k (receive)
 };
 
 // Fixed stride == len for rstream (tcpck_rstream.hip).
@@ -116,7 +117,9 @@ hipError_t launch_vvstream(int op, int variant, bool fixed, const RunArgs &a, ui
 // the arena -- fixed slots (fixed = true: stride % 16 == 0, stride >= len) or
 // offsets + lengths (fixed = false; runs of <= 128 images).  variant: 0 policy
 // (U4, scattered block order), 1 U4, 2 U8; + 4: default block order, + 8:
-// scattered (else XCD-chunked).  a.oversub: 0 = by size; a.total_bytes: image bytes hint.
+// scattered (else XCD-chunked); + 16 (with a.hdr): the stream read with the
+// default cache policy.  a.hdr (VERIFY only): the run's headers in host order
+// to the dense array after its verdicts (tcpck_batch_receive).  a.oversub: 0 = by size; a.total_bytes: image bytes hint.
 bool sstream_fixed_applies(uint64_t stride, uint32_t len);
 hipError_t launch_sstream(int op, int variant, bool fixed, const RunArgs &a, uint32_t num_cus, hipStream_t stream);
 // ---- segment (tcpck_segment.hip): send stream -> checksummed images ------

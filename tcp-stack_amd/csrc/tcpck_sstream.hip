@@ -42,6 +42,13 @@
 //     stores the result at the image's arena address (d_i + 16 C_i + h_i +
 //     28); images < 30 B send the run to the per-image pass, which skips
 //     them (the C ABI rejects them).
+//   * HDR (kVerify, tcpck_batch_receive with a header array): after the
+//     verdicts the wave converts its run's headers to host order
+//     (TcpHeaderN2H, include/socket-manager.h:184; tcp-header.h:208-221) into
+//     the dense array, one image per lane: the run's records leave as one
+//     burst of whole lines instead of a second launch over the batch.  The
+//     header lines were read by the stream moments before (KEEPL: with the
+//     default cache policy, so they are still in L2).
 #include <algorithm>
 #include <type_traits>
 
@@ -76,6 +83,7 @@ struct SSArgs {
   uint32_t magic, shift;    // fixed: q / nchunk == mulhi(q, magic) >> shift (magic 0: q >> shift)
   uint32_t order;           // block order (dev::ordered_block)
   int mode;                 // kRef or kRfc1071
+  uint8_t *hdr;             // HDR: host-order header k at hdr + 32 k
 };
 
 __device__ __forceinline__ u32x4 zero_word(u32x4 w, uint32_t wi) {
@@ -96,7 +104,7 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t x) {
 
 // MODE kRfc1071: exact u32 prefix tables (as tcpck_vvstream.hip), the
 // differences folded
-template <int U, int OP, bool FIXED, int MODE = kRef>
+template <int U, int OP, bool FIXED, int MODE = kRef, bool HDR = false, bool KEEPL = false>
 __global__ void __launch_bounds__(kBlock) sstream_kernel(SSArgs a) {
   __shared__ uint32_t s_end[kWavesPerBlock][FIXED ? 1 : kEnds];         // virtual ends, compacted bytes
   __shared__ uint32_t s_c[kWavesPerBlock][FIXED ? 1 : kMaxRun + 64];    // first compacted chunk, ~0 past the run
@@ -250,7 +258,15 @@ __global__ void __launch_bounds__(kBlock) sstream_kernel(SSArgs a) {
         return d + (q << 4);
       }
     };
-    auto load_step = [&](uint32_t t) -> u32x4 { return dev::load16_buf_nt(rsrc, map_step(t), 0); };
+    auto load_step = [&](uint32_t t) -> u32x4 {
+      if constexpr (KEEPL) {
+        typedef unsigned v4u __attribute__((ext_vector_type(4)));
+        const v4u v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, static_cast<int>(map_step(t)), 0, 0);
+        return u32x4{v.x, v.y, v.z, v.w};
+      } else {
+        return dev::load16_buf_nt(rsrc, map_step(t), 0);
+      }
+    };
     // arena offset (from B) of image i's checksum field
     auto field_at = [&](uint32_t i, uint32_t start) -> uint32_t {
       if constexpr (FIXED)
@@ -401,11 +417,42 @@ __global__ void __launch_bounds__(kBlock) sstream_kernel(SSArgs a) {
       if (lane == 0) store(k, sum, start);
     }
   }
+  if constexpr (HDR) {
+    // the run's headers in host order, image kb + i by lane i (mod 64): 32-B
+    // records, consecutive lanes consecutive records -- whole lines out
+    for (uint32_t i = lane; i < nimg; i += 64) {
+      const uint64_t k = kb + i;
+      const uint8_t *p = arena + (FIXED ? k * S : a.offsets[k] - a.base);
+      uint32_t hd[8];
+      const uintptr_t pa = reinterpret_cast<uintptr_t>(p);
+      if ((pa & 15u) == 0) {
+        const u32x4 x = reinterpret_cast<const u32x4 *>(p)[0], y = reinterpret_cast<const u32x4 *>(p)[1];
+        hd[0] = x.x, hd[1] = x.y, hd[2] = x.z, hd[3] = x.w, hd[4] = y.x, hd[5] = y.y, hd[6] = y.z, hd[7] = y.w;
+      } else if ((pa & 3u) == 0) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) hd[j] = reinterpret_cast<const uint32_t *>(p)[j];
+      } else {  // images are 2-B aligned
+        const uint16_t *q = reinterpret_cast<const uint16_t *>(p);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) hd[j] = static_cast<uint32_t>(q[2 * j]) | (static_cast<uint32_t>(q[2 * j + 1]) << 16);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) hd[j] = dev::n2h_dword(hd[j], dev::n2h_selector(static_cast<uint32_t>(j)));
+      uint8_t *o = a.hdr + 32 * k;
+      if ((reinterpret_cast<uintptr_t>(o) & 15u) == 0) {
+        reinterpret_cast<u32x4 *>(o)[0] = u32x4{hd[0], hd[1], hd[2], hd[3]};
+        reinterpret_cast<u32x4 *>(o)[1] = u32x4{hd[4], hd[5], hd[6], hd[7]};
+      } else {  // the API requires a 4-B aligned array
+#pragma unroll
+        for (int j = 0; j < 8; ++j) reinterpret_cast<uint32_t *>(o)[j] = hd[j];
+      }
+    }
+  }
 }
 
-template <int U, int OP, bool FIXED, int MODE = kRef>
+template <int U, int OP, bool FIXED, int MODE = kRef, bool HDR = false, bool KEEPL = false>
 hipError_t launch_one(SSArgs a, uint32_t oversub, uint64_t min_waves, uint32_t num_cus, hipStream_t stream) {
-  static const uint32_t per_cu = dev::resident_blocks_per_cu(sstream_kernel<U, OP, FIXED, MODE>);
+  static const uint32_t per_cu = dev::resident_blocks_per_cu(sstream_kernel<U, OP, FIXED, MODE, HDR, KEEPL>);
   const uint64_t resident = static_cast<uint64_t>(per_cu) * num_cus;
   uint64_t blocks = resident * oversub;
   const uint64_t need = (a.count + kWavesPerBlock - 1) / kWavesPerBlock;  // >= 1 image per wave
@@ -416,12 +463,22 @@ hipError_t launch_one(SSArgs a, uint32_t oversub, uint64_t min_waves, uint32_t n
   if (blocks > 0xFFFFFFFFull) return hipErrorInvalidValue;
   a.per_wave = a.count / (blocks * kWavesPerBlock);
   a.rem = a.count % (blocks * kWavesPerBlock);
-  hipLaunchKernelGGL((sstream_kernel<U, OP, FIXED, MODE>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0, stream, a);
+  hipLaunchKernelGGL((sstream_kernel<U, OP, FIXED, MODE, HDR, KEEPL>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0,
+                     stream, a);
   return hipGetLastError();
 }
 
 template <int U, bool FIXED>
-hipError_t dispatch(int op, const SSArgs &a, uint32_t m, uint64_t min_waves, uint32_t num_cus, hipStream_t s) {
+hipError_t dispatch(int op, const SSArgs &a, uint32_t m, uint64_t min_waves, uint32_t num_cus, hipStream_t s,
+                    bool keepl) {
+  if (a.hdr) {  // VERIFY + the run's headers into the array (tcpck_batch_receive)
+    if (op != kVerify) return hipErrorInvalidValue;
+    if (a.mode != kRef)
+      return keepl ? launch_one<U, kVerify, FIXED, kRfc1071, true, true>(a, m, min_waves, num_cus, s)
+                   : launch_one<U, kVerify, FIXED, kRfc1071, true, false>(a, m, min_waves, num_cus, s);
+    return keepl ? launch_one<U, kVerify, FIXED, kRef, true, true>(a, m, min_waves, num_cus, s)
+                 : launch_one<U, kVerify, FIXED, kRef, true, false>(a, m, min_waves, num_cus, s);
+  }
   if (a.mode != kRef) {
     switch (op) {
       case kChecksum: return launch_one<U, kChecksum, FIXED, kRfc1071>(a, m, min_waves, num_cus, s);
@@ -454,6 +511,7 @@ hipError_t launch_sstream(int op, int variant, bool fixed, const RunArgs &r, uin
   a.count = r.count;
   a.out = r.out;
   a.mode = r.mode;
+  a.hdr = r.hdr;
   // + 4: default block order; + 8: scattered (the policy's); else groups of
   // 16 blocks per XCD
   a.order = (variant & 8) ? kOrderScatter : ((variant & 4) ? dev::kOrderDefault : 4u);
@@ -495,10 +553,11 @@ hipError_t launch_sstream(int op, int variant, bool fixed, const RunArgs &r, uin
                                       fixed ? 8u << 10 : 16u << 10);
   const int u = variant & 3;  // 0: policy, 1: U4, 2: U8
   const bool u8 = u == 2;
-  if (fixed) return u8 ? dispatch<8, true>(op, a, m, min_waves, num_cus, stream)
-                       : dispatch<4, true>(op, a, m, min_waves, num_cus, stream);
-  return u8 ? dispatch<8, false>(op, a, m, min_waves, num_cus, stream)
-            : dispatch<4, false>(op, a, m, min_waves, num_cus, stream);
+  const bool keepl = (variant & 16) != 0;  // HDR: the stream read with the default cache policy
+  if (fixed) return u8 ? dispatch<8, true>(op, a, m, min_waves, num_cus, stream, keepl)
+                       : dispatch<4, true>(op, a, m, min_waves, num_cus, stream, keepl);
+  return u8 ? dispatch<8, false>(op, a, m, min_waves, num_cus, stream, keepl)
+            : dispatch<4, false>(op, a, m, min_waves, num_cus, stream, keepl);
 }
 
 }  // namespace tcpck

@@ -47,7 +47,10 @@ KERNEL_GSTREAM = 9  # fixed stride == len, len a power of two in [32, 1024], 16-
 KERNEL_SSTREAM = 10  # slotted layouts (fixed slots, stride % 16 == 0, or any offset list): param = 0 policy (U4, scattered order), 1 U4, 2 U8 (+4 default block order, +8 scattered) | oversub << 16
 SEG_SHAPES = {1: "G8/U2", 2: "G16/U6", 3: "G64/U4", 4: "G64/U2", 5: "G32/U3", 6: "G4/U8", 7: "W4/U4", 8: "W8/U4", 9: "W16/U2", 10: "W16/U4", 11: "W2/U4"}
 TUNING_EXPORTS = ("tcpck_batch_fixed_ex", "tcpck_batch_var_ex", "tcpck_ctx_set_debug", "tcpck_diag_stream",
-                  "tcpck_batch_segment_ex")
+                  "tcpck_batch_segment_ex", "tcpck_batch_receive_ex")
+PARAM_FILL_UPDATE = 1 << 28  # FILL: the kernel's CHECKSUM pass + the field-update pass
+PARAM_FILL_INSTREAM = 1 << 29  # FILL under AUTO: the field zeroed in the stream
+PARAM_RECEIVE_TWO_PASS = 1 << 30  # RECEIVE into a header array: separate header pass
 
 # Every symbol include/tcpck.h declares (checked by tests/test_abi.py).
 EXPORTS = (
@@ -116,6 +119,8 @@ def lib() -> ctypes.CDLL:
         "tcpck_batch_segment_ex": (i32, [vp, i32, vp, u64, u32, vp, u32, vp, u64, vp, i32, vp]),
         "tcpck_batch_header_swap": (i32, [vp, vp, vp, u64, u64, vp]),
         "tcpck_batch_receive": (i32, [vp, i32, vp, u64, u32, vp, vp, u64, vp, vp, ctypes.POINTER(Layout), vp]),
+        "tcpck_batch_receive_ex": (i32, [vp, i32, vp, u64, u32, vp, vp, u64, vp, vp, ctypes.POINTER(Layout), i32, i32,
+                                         vp]),
         # include/tcpck_tuning.h
         "tcpck_batch_fixed_ex": (i32, [vp, i32, i32, vp, u64, u32, u64, vp, i32, i32, vp]),
         "tcpck_batch_var_ex": (i32, [vp, i32, i32, vp, vp, vp, u64, vp, ctypes.POINTER(Layout), i32, i32, vp]),
@@ -263,15 +268,20 @@ class Context:
 
     def batch_receive(self, arena, count: int, ok, hdr=None, stride: int = 0, length: int = 0, offsets=None,
                       lengths=None, mode: int = MODE_REF, total_bytes: int = 0, min_len: int = 0, max_len: int = 0,
-                      packed: bool = False, sorted: bool = False, stream=None) -> None:
+                      packed: bool = False, sorted: bool = False, stream=None, kernel: int | None = None,
+                      param: int = 0) -> None:
         """ReceivePacket's front half for a batch (tcpck_batch_receive): ok[k] = verdict on the
         network-order image; headers in host order in place (hdr None) or into hdr (32 B per image,
-        the arena left as received).  Fixed layout (stride, length) or offsets + lengths."""
+        the arena left as received).  Fixed layout (stride, length) or offsets + lengths.
+        kernel/param: tcpck_batch_receive_ex (include/tcpck_tuning.h)."""
         lay = Layout(total_bytes, min_len, max_len,
                      (LAYOUT_PACKED if packed else 0) | (LAYOUT_SORTED if sorted else 0), 0)
-        _check(lib().tcpck_batch_receive(self._h, mode, _ptr(arena), stride, length, _ptr(offsets), _ptr(lengths),
-                                         count, _ptr(ok), _ptr(hdr), ctypes.byref(lay), _stream(stream)),
-               "tcpck_batch_receive")
+        args = (self._h, mode, _ptr(arena), stride, length, _ptr(offsets), _ptr(lengths), count, _ptr(ok), _ptr(hdr),
+                ctypes.byref(lay))
+        if kernel is None:
+            _check(lib().tcpck_batch_receive(*args, _stream(stream)), "tcpck_batch_receive")
+        else:
+            _check(lib().tcpck_batch_receive_ex(*args, kernel, param, _stream(stream)), "tcpck_batch_receive_ex")
 
     def batch_segment(self, payload, payload_bytes: int, seg: int, hdr, seq0: int, images, stride: int,
                       out=None, mode: int = MODE_REF, param: int | None = None, stream=None) -> int:

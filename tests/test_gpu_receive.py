@@ -450,3 +450,66 @@ def test_batch_receive_sstream_variants(ctx, variant):
     exp_ok = R.receive_np(exp, off.astype(np.int64), ln)
     np.testing.assert_array_equal(host(ok), exp_ok)
     np.testing.assert_array_equal(host(buf), exp)
+
+
+# ---- RECEIVE with the headers written by sstream itself (one launch) -------------------
+
+@pytest.mark.parametrize("variant", [0, 1, 2, 4, 8, 16, 17, 18, 1 << 30])
+@pytest.mark.parametrize("layout", ["ring", "ring-mis", "unordered", "fixed-slots", "fixed-mis"])
+@pytest.mark.parametrize("hdr_mis", [0, 4])
+def test_batch_receive_fused_hdr(ctx, variant, layout, hdr_mis):
+    """tcpck_batch_receive_ex on KERNEL_SSTREAM: each wave writes its run's
+    host-order headers after its verdicts (variant + 16: the stream read with
+    the default cache policy; 1 << 30: the separate header pass instead).
+    Rings (16-B and 2-B aligned starts), unordered offsets (the per-image
+    fallback), fixed slots; header arrays 16-B and only 4-B aligned; both
+    modes.  Verdicts, every header byte, the arena unchanged."""
+    import tcpck
+    from oracle import ref16 as R
+    rng = np.random.default_rng(variant % 97 + 10 * len(layout) + hdr_mis)
+    mode = int(rng.random() < 0.5)
+    n, slot = 20000, 2048
+    mis = 6 if layout.endswith("mis") else 0
+    ln = (rng.integers(16, 1000, n) * 2).astype(np.uint32)
+    off = np.arange(n, dtype=np.uint64) * np.uint64(slot)
+    if layout == "unordered":
+        off = off[rng.permutation(n)].copy()
+    if layout.startswith("fixed"):
+        ln[:] = 1492
+    a = rng.integers(0, 256, n * slot + 64, dtype=np.uint8)
+    v = a[mis:]
+    for o, l in zip(off[::3], ln[::3]):
+        R.fill_np(v[int(o):int(o) + int(l)], mode)
+    buf = dev(a)
+    ok = torch.empty(n, dtype=torch.uint8, device="cuda")
+    hbuf = torch.full((n * 32 + 16,), 0xEE, dtype=torch.uint8, device="cuda")
+    hdr = hbuf.data_ptr() + hdr_mis
+    if layout.startswith("fixed"):
+        ctx.batch_receive(buf.data_ptr() + mis, n, ok, hdr, stride=slot, length=1492, mode=mode,
+                          kernel=tcpck.KERNEL_SSTREAM, param=variant)
+    else:
+        ctx.batch_receive(buf.data_ptr() + mis, n, ok, hdr, offsets=dev(off), lengths=dev(ln), mode=mode,
+                          total_bytes=int(ln.sum()), min_len=int(ln.min()), max_len=int(ln.max()),
+                          sorted=layout != "unordered", kernel=tcpck.KERNEL_SSTREAM, param=variant)
+    exp_ok = (R.ref16_batch_np(v, off, ln, mode) == 0).astype(np.uint8)
+    np.testing.assert_array_equal(host(ok), exp_ok)
+    h = host(hbuf)
+    np.testing.assert_array_equal(h[hdr_mis:hdr_mis + 32 * n], _expect_hdr(v, off.astype(np.int64)))
+    assert (h[:hdr_mis] == 0xEE).all() and (h[hdr_mis + 32 * n:] == 0xEE).all()
+    np.testing.assert_array_equal(host(buf), a)
+
+
+def test_batch_receive_fused_rejects_other_ops(ctx):
+    """The fused header write exists for RECEIVE only: a plain VERIFY through
+    sstream never touches a header array (there is none to pass), and a
+    CHECKSUM/FILL never reaches it."""
+    import tcpck
+    rng = np.random.default_rng(5)
+    n, slot = 1000, 2048
+    a = rng.integers(0, 256, n * slot, dtype=np.uint8)
+    buf = dev(a)
+    out = torch.empty(n, dtype=torch.int16, device="cuda")
+    ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, buf, slot, 1492, n, out, tcpck.KERNEL_SSTREAM, 16)
+    from oracle import ref16 as R
+    np.testing.assert_array_equal(host(out).view(np.uint16),
+                                  R.ref16_batch_np(a, np.arange(n) * slot, np.full(n, 1492)))
