@@ -88,6 +88,13 @@ extern "C" {
                                    cache policy)
                                    | (grid oversubscription << 16: 0 = by batch
                                    size, M = M x the resident grid)             */
+#define TCPCK_KERNEL_BSTREAM 11 /* experiment, MODE_REF, CHECKSUM/VERIFY, fixed
+                                   stride == len: byte runs across image edges,
+                                   cut images combined with one atomic per part
+                                   in a workspace = the ctx debug buffer
+                                   (tcpck_ctx_set_debug: count u64s, zeroed;
+                                   left zeroed); param = log2 run bytes (0 = 8
+                                   KiB) | 256: 8 steps in flight             */
 /* FILL in TCPCK_MODE_REF with a results buffer, any kernel (param bits, OR'ed
  * with the kernel's own param):
  *   TCPCK_PARAM_FILL_UPDATE    the kernel's CHECKSUM pass, then a field pass that
