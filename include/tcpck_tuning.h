@@ -22,7 +22,8 @@ extern "C" {
                                | (grid oversubscription << 16)
                                | (1 << 24: each XCD takes groups of 16 blocks)  */
 /* 2, 3, 4, 6, 7: span, stream, fstream, rvstream and vstream, measured in
-   round 1 and removed; the numbers are not reused. */
+   round 1 and removed; 11: bstream (byte runs across
+   image edges, round 2, removed); the numbers are not reused. */
 #define TCPCK_KERNEL_RSTREAM 5 /* fixed stride == len only, MODE_REF: one run per
                                   wave, scalar boundary walk; param = variant
                                   (0: 4 loads in flight, 1: 2, 2: 8, 3: 4 with
@@ -88,13 +89,6 @@ extern "C" {
                                    cache policy)
                                    | (grid oversubscription << 16: 0 = by batch
                                    size, M = M x the resident grid)             */
-#define TCPCK_KERNEL_BSTREAM 11 /* experiment, MODE_REF, CHECKSUM/VERIFY, fixed
-                                   stride == len: byte runs across image edges,
-                                   cut images combined with one atomic per part
-                                   in a workspace = the ctx debug buffer
-                                   (tcpck_ctx_set_debug: count u64s, zeroed;
-                                   left zeroed); param = log2 run bytes (0 = 8
-                                   KiB) | 256: 8 steps in flight             */
 /* FILL in TCPCK_MODE_REF with a results buffer, any kernel (param bits, OR'ed
  * with the kernel's own param):
  *   TCPCK_PARAM_FILL_UPDATE    the kernel's CHECKSUM pass, then a field pass that

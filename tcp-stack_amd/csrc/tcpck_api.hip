@@ -366,16 +366,6 @@ hipError_t run_fixed_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint
     }
     return tcpck::launch_rstream(op, variant, a, num_cus, s);
   }
-  if (kernel == TCPCK_KERNEL_BSTREAM) {  // experiment: the workspace is the ctx's debug buffer (count zeroed u64s)
-    if (mode != TCPCK_MODE_REF || stride != len || !ctx->dbg) return hipErrorInvalidValue;
-    tcpck::ByteRunArgs a{};
-    a.arena = arena;
-    a.stride = stride;
-    a.count = count;
-    a.out = out;
-    a.ws = static_cast<uint64_t *>(ctx->dbg);
-    return tcpck::launch_bstream(op, param & 0xFFFF, a, s);
-  }
   if (kernel == TCPCK_KERNEL_GSTREAM) {  // stride == len, a power of two in [32, 1024], 16-B aligned arena
     if (mode != TCPCK_MODE_REF || !tcpck::gstream_applies(arena, stride, len)) return hipErrorInvalidValue;
     tcpck::GroupStreamArgs a{};

@@ -122,21 +122,6 @@ hipError_t launch_vvstream(int op, int variant, bool fixed, const RunArgs &a, ui
 // to the dense array after its verdicts (tcpck_batch_receive).  a.oversub: 0 = by size; a.total_bytes: image bytes hint.
 bool sstream_fixed_applies(uint64_t stride, uint32_t len);
 hipError_t launch_sstream(int op, int variant, bool fixed, const RunArgs &a, uint32_t num_cus, hipStream_t stream);
-// ---- bstream (experiment): fixed stride == len, byte runs across image edges,
-// cut images combined through a zeroed u64 workspace (tcpck_bstream.hip) ----
-struct ByteRunArgs {
-  uint8_t *arena;
-  uint64_t stride;     // == image length
-  uint64_t count;
-  void *out;           // u16 (CHECKSUM) or u8 (VERIFY)
-  uint64_t *ws;        // count u64s, all zero (left zero by every launch)
-  uint64_t nruns;      // set by the launcher
-  uint32_t run_shift;  // run bytes = 1 << run_shift
-  uint32_t off0;       // arena & 127
-  uint32_t order;      // block order
-};
-// variant bits 0-4: log2 run bytes (0 = 8 KiB), bit 8: 8 steps in flight
-hipError_t launch_bstream(int op, int variant, ByteRunArgs a, hipStream_t stream);
 // ---- segment (tcpck_segment.hip): send stream -> checksummed images ------
 struct SegmentArgs {
   const uint8_t *payload;    // the send stream (4-B aligned)
