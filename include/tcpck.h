@@ -220,6 +220,18 @@ int tcpck_host_batch_fixed(tcpck_ctx *ctx, int op, int mode, void *h_arena,
 int tcpck_host_batch_var(tcpck_ctx *ctx, int op, int mode, void *h_arena,
                          const uint64_t *h_offsets, const uint32_t *h_lengths,
                          uint64_t count, void *h_out);
+/* The same host batch over several contexts at once -- one per GPU of the
+ * node, each with its own PCIe link (independent segments, no
+ * exchange step): contiguous shards, equal image counts (fixed) or balanced by
+ * bytes (variable, over h_lengths), each run by tcpck_host_batch_* on its own
+ * host thread (the first on the calling thread).  Results land in h_out by
+ * index as from one context.  Synchronous; returns the first failing shard's
+ * status.  A context listed twice runs its shards one after the other. */
+int tcpck_host_batch_fixed_multi(tcpck_ctx *const *ctxs, int n_ctx, int op, int mode, void *h_arena,
+                                 uint64_t stride, uint32_t len, uint64_t count, void *h_out);
+int tcpck_host_batch_var_multi(tcpck_ctx *const *ctxs, int n_ctx, int op, int mode, void *h_arena,
+                               const uint64_t *h_offsets, const uint32_t *h_lengths, uint64_t count,
+                               void *h_out);
 /* Bytes of device staging per chunk used by the host batch functions. */
 int tcpck_ctx_set_chunk_bytes(tcpck_ctx *ctx, uint64_t bytes);
 

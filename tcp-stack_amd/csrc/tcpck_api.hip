@@ -17,6 +17,7 @@
 #include <cstring>
 #include <mutex>
 #include <new>
+#include <thread>
 #include <vector>
 
 #include "tcpck.h"
@@ -632,6 +633,39 @@ void patch_fields(uint8_t *arena, uint64_t k0, uint64_t n, const uint16_t *res,
 
 }  // namespace
 
+// helpers of tcpck_host_batch_*_multi
+namespace {
+
+// Runs shard i of n as job(i) -- shards 1.. on their own threads, shard 0 on the
+// caller's -- and returns the first nonzero status in shard order.
+template <typename Job>
+int run_shards(int n, Job job) {
+  std::vector<int> rc(static_cast<size_t>(n), TCPCK_OK);
+  std::vector<std::thread> th;
+  th.reserve(static_cast<size_t>(n));
+  for (int i = 1; i < n; ++i) {
+    try {
+      th.emplace_back([&rc, &job, i] { rc[static_cast<size_t>(i)] = job(i); });
+    } catch (...) {  // no thread: run it here
+      rc[static_cast<size_t>(i)] = job(i);
+    }
+  }
+  rc[0] = job(0);
+  for (auto &t : th) t.join();
+  for (int r : rc)
+    if (r != TCPCK_OK) return r;
+  return TCPCK_OK;
+}
+
+bool valid_ctx_list(tcpck_ctx *const *ctxs, int n_ctx) {
+  if (!ctxs || n_ctx < 1) return false;
+  for (int i = 0; i < n_ctx; ++i)
+    if (!ctxs[i]) return false;
+  return true;
+}
+
+}  // namespace
+
 extern "C" {
 
 int tcpck_abi_version(void) { return TCPCK_ABI_VERSION; }
@@ -1029,6 +1063,55 @@ int tcpck_host_batch_var(tcpck_ctx *ctx, int op, int mode, void *h_arena, const 
     patch_fields(arena, 0, count, reinterpret_cast<const uint16_t *>(out_bytes), h_offsets, h_lengths,
                  0, 0);
   return TCPCK_OK;
+}
+
+// ---- host batches over several contexts (one per GPU) ---------------------------
+
+int tcpck_host_batch_fixed_multi(tcpck_ctx *const *ctxs, int n_ctx, int op, int mode, void *h_arena,
+                                 uint64_t stride, uint32_t len, uint64_t count, void *h_out) {
+  if (!valid_ctx_list(ctxs, n_ctx) || !valid_op_mode(op, mode)) return TCPCK_EINVAL;
+  if (count == 0) return TCPCK_OK;
+  if (!h_arena || (!h_out && op != TCPCK_OP_FILL)) return TCPCK_EINVAL;
+  if (count > 1 && stride > (UINT64_MAX - len) / (count - 1)) return TCPCK_EINVAL;
+  const uint64_t n = std::min<uint64_t>(static_cast<uint64_t>(n_ctx), count);
+  const size_t es = out_elem(op);
+  auto *arena = static_cast<uint8_t *>(h_arena);
+  auto *out = static_cast<uint8_t *>(h_out);
+  return run_shards(static_cast<int>(n), [&](int i) {
+    const uint64_t q = count / n, r = count % n, ui = static_cast<uint64_t>(i);
+    const uint64_t k0 = ui * q + std::min(ui, r), k1 = k0 + q + (ui < r ? 1 : 0);
+    return tcpck_host_batch_fixed(ctxs[i], op, mode, arena + k0 * stride, stride, len, k1 - k0,
+                                  out ? out + k0 * es : nullptr);
+  });
+}
+
+int tcpck_host_batch_var_multi(tcpck_ctx *const *ctxs, int n_ctx, int op, int mode, void *h_arena,
+                               const uint64_t *h_offsets, const uint32_t *h_lengths, uint64_t count,
+                               void *h_out) {
+  if (!valid_ctx_list(ctxs, n_ctx) || !valid_op_mode(op, mode)) return TCPCK_EINVAL;
+  if (count == 0) return TCPCK_OK;
+  if (!h_arena || !h_offsets || !h_lengths || (!h_out && op != TCPCK_OP_FILL)) return TCPCK_EINVAL;
+  const uint64_t n = std::min<uint64_t>(static_cast<uint64_t>(n_ctx), count);
+  // shard starts balanced by bytes: shard i begins at the first image whose
+  // byte prefix reaches i/n of the total (a 1492-B image is 15.5x a 96-B one)
+  uint64_t total = 0;
+  for (uint64_t k = 0; k < count; ++k) total += h_lengths[k];
+  std::vector<uint64_t> cut(n + 1, count);
+  cut[0] = 0;
+  uint64_t pre = 0, k = 0;
+  for (uint64_t i = 1; i < n; ++i) {
+    const uint64_t target = static_cast<uint64_t>((static_cast<unsigned __int128>(total) * i) / n);
+    while (k < count && pre < target) pre += h_lengths[k++];
+    cut[i] = std::max(k, cut[i - 1]);
+  }
+  const size_t es = out_elem(op);
+  auto *out = static_cast<uint8_t *>(h_out);
+  return run_shards(static_cast<int>(n), [&](int i) {
+    const uint64_t k0 = cut[static_cast<size_t>(i)], k1 = cut[static_cast<size_t>(i) + 1];
+    if (k1 <= k0) return TCPCK_OK;
+    return tcpck_host_batch_var(ctxs[i], op, mode, h_arena, h_offsets + k0, h_lengths + k0, k1 - k0,
+                                out ? out + k0 * es : nullptr);
+  });
 }
 
 // ---- memory helpers -----------------------------------------------------------

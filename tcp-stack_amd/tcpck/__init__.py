@@ -62,7 +62,7 @@ EXPORTS = (
     "tcpck_host_alloc", "tcpck_host_free", "tcpck_device_alloc", "tcpck_device_free",
     "tcpck_memcpy_h2d", "tcpck_memcpy_d2h", "tcpck_stream_sync",
     "tcpck_synth_fixed", "tcpck_synth_var", "tcpck_batch_segment", "tcpck_batch_header_swap",
-    "tcpck_batch_receive",
+    "tcpck_batch_receive", "tcpck_host_batch_fixed_multi", "tcpck_host_batch_var_multi",
 )
 
 
@@ -105,6 +105,8 @@ def lib() -> ctypes.CDLL:
         "tcpck_batch_set_ack": (i32, [vp, i32, vp, vp, u64, u64, vp, u32, vp, vp]),
         "tcpck_host_batch_fixed": (i32, [vp, i32, i32, vp, u64, u32, u64, vp]),
         "tcpck_host_batch_var": (i32, [vp, i32, i32, vp, vp, vp, u64, vp]),
+        "tcpck_host_batch_fixed_multi": (i32, [ctypes.POINTER(vp), i32, i32, i32, vp, u64, u32, u64, vp]),
+        "tcpck_host_batch_var_multi": (i32, [ctypes.POINTER(vp), i32, i32, i32, vp, vp, vp, u64, vp]),
         "tcpck_ctx_set_chunk_bytes": (i32, [vp, u64]),
         "tcpck_host_alloc": (i32, [sz, ctypes.POINTER(vp)]),
         "tcpck_host_free": (i32, [vp]),
@@ -336,3 +338,25 @@ class Context:
 
     def set_chunk_bytes(self, n: int) -> None:
         _check(lib().tcpck_ctx_set_chunk_bytes(self._h, n), "tcpck_ctx_set_chunk_bytes")
+
+
+def _ctx_array(ctxs):
+    arr = (ctypes.c_void_p * len(ctxs))(*[c._h.value for c in ctxs])
+    return ctypes.cast(arr, ctypes.POINTER(ctypes.c_void_p)), arr
+
+
+def host_batch_fixed_multi(ctxs, op: int, arena, stride: int, length: int, count: int, out,
+                           mode: int = MODE_REF) -> None:
+    """tcpck_host_batch_fixed over several contexts (one per GPU): contiguous equal shards, one host thread each."""
+    p, keep = _ctx_array(ctxs)
+    _check(lib().tcpck_host_batch_fixed_multi(p, len(ctxs), op, mode, _ptr(arena), stride, length, count, _ptr(out)),
+           "tcpck_host_batch_fixed_multi")
+    del keep
+
+
+def host_batch_var_multi(ctxs, op: int, arena, offsets, lengths, count: int, out, mode: int = MODE_REF) -> None:
+    """tcpck_host_batch_var over several contexts: contiguous shards balanced by bytes."""
+    p, keep = _ctx_array(ctxs)
+    _check(lib().tcpck_host_batch_var_multi(p, len(ctxs), op, mode, _ptr(arena), _ptr(offsets), _ptr(lengths), count,
+                                            _ptr(out)), "tcpck_host_batch_var_multi")
+    del keep

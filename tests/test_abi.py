@@ -118,3 +118,22 @@ def test_ctx_create_without_gpu_fails_cleanly(built_lib):
     with pytest.raises(tcpck.TcpckError) as e:
         tcpck.Context(0)
     assert e.value.status in (tcpck.ENODEV,) or e.value.status <= tcpck.EHIP
+
+
+def test_multi_ctx_rejects_bad_lists(built_lib):
+    """tcpck_host_batch_*_multi validate the context list before any shard runs
+    (no GPU needed): NULL list, zero contexts, a NULL entry."""
+    import ctypes
+    import tcpck
+    L = tcpck.lib()
+    img = np.zeros(1492 * 4, np.uint8)
+    out = np.zeros(4, np.uint16)
+    off = np.arange(4, dtype=np.uint64) * 1492
+    ln = np.full(4, 1492, np.uint32)
+    assert L.tcpck_host_batch_fixed_multi(None, 1, 0, 0, img.ctypes.data, 1492, 1492, 4, out.ctypes.data) == tcpck.EINVAL
+    arr = (ctypes.c_void_p * 2)(None, None)
+    p = ctypes.cast(arr, ctypes.POINTER(ctypes.c_void_p))
+    assert L.tcpck_host_batch_fixed_multi(p, 0, 0, 0, img.ctypes.data, 1492, 1492, 4, out.ctypes.data) == tcpck.EINVAL
+    assert L.tcpck_host_batch_fixed_multi(p, 2, 0, 0, img.ctypes.data, 1492, 1492, 4, out.ctypes.data) == tcpck.EINVAL
+    assert L.tcpck_host_batch_var_multi(p, 2, 0, 0, img.ctypes.data, off.ctypes.data, ln.ctypes.data, 4,
+                                        out.ctypes.data) == tcpck.EINVAL
