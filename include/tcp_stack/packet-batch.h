@@ -15,8 +15,10 @@
 // packet costs ~0.1 us instead of a launch.
 //
 // Results are identical to calling CalculateChecksum per packet.  Not
-// thread-safe: one PacketBatch per thread (each owns a tcpck context and a
-// staging arena).
+// thread-safe: one PacketBatch per thread (each owns its tcpck contexts and a
+// staging arena).  Given several devices, a batch is split over all of them
+// (tcpck_host_batch_var_multi: contiguous shards balanced by bytes, one host
+// thread and PCIe link per GPU).
 #ifndef TCP_STACK_AMD_PACKET_BATCH_H_
 #define TCP_STACK_AMD_PACKET_BATCH_H_
 
@@ -52,13 +54,21 @@ class PacketBatch {
   };
 
   explicit PacketBatch(int device = 0) : PacketBatch(device, Thresholds()) {}
-  PacketBatch(int device, Thresholds t) : thresholds_(t) {
-    Check(tcpck_ctx_create(device, &ctx_), "tcpck_ctx_create");
+  PacketBatch(int device, Thresholds t) : PacketBatch(std::vector<int>{device}, t) {}
+  // One context per listed device (a device may appear more than once).
+  PacketBatch(const std::vector<int> &devices, Thresholds t) : thresholds_(t) {
+    if (devices.empty()) throw std::invalid_argument("PacketBatch: no device");
+    for (int d : devices) {
+      tcpck_ctx *c = nullptr;
+      const int st = tcpck_ctx_create(d, &c);
+      if (st != TCPCK_OK) {
+        Release();
+        Check(st, "tcpck_ctx_create");
+      }
+      ctxs_.push_back(c);
+    }
   }
-  ~PacketBatch() {
-    if (arena_) tcpck_host_free(arena_);
-    if (ctx_) tcpck_ctx_destroy(ctx_);
-  }
+  ~PacketBatch() { Release(); }
   PacketBatch(const PacketBatch &) = delete;
   PacketBatch &operator=(const PacketBatch &) = delete;
 
@@ -118,9 +128,9 @@ class PacketBatch {
       Reserve(bytes);
       for (size_t j = 0; j < idx_.size(); ++j) std::memcpy(arena_ + offsets_[j], Image(*pkts[idx_[j]]), lengths_[j]);
       out_.resize(idx_.size());
-      Check(tcpck_host_batch_var(ctx_, op, TCPCK_MODE_REF, arena_, offsets_.data(), lengths_.data(), idx_.size(),
-                                 out_.data()),
-            "tcpck_host_batch_var");
+      Check(tcpck_host_batch_var_multi(ctxs_.data(), static_cast<int>(ctxs_.size()), op, TCPCK_MODE_REF, arena_,
+                                       offsets_.data(), lengths_.data(), idx_.size(), out_.data()),
+            "tcpck_host_batch_var_multi");
       for (size_t j = 0; j < idx_.size(); ++j) sums_[idx_[j]] = out_[j];
       last_gpu_ = idx_.size();
     }
@@ -136,6 +146,13 @@ class PacketBatch {
     }
   }
 
+  void Release() {
+    if (arena_) tcpck_host_free(arena_);
+    arena_ = nullptr;
+    for (tcpck_ctx *c : ctxs_) tcpck_ctx_destroy(c);
+    ctxs_.clear();
+  }
+
   void Reserve(uint64_t bytes) {
     if (bytes <= cap_) return;
     if (arena_) tcpck_host_free(arena_);
@@ -147,7 +164,7 @@ class PacketBatch {
     cap_ = bytes + (bytes >> 2);
   }
 
-  tcpck_ctx *ctx_ = nullptr;
+  std::vector<tcpck_ctx *> ctxs_;
   Thresholds thresholds_;
   char *arena_ = nullptr;
   uint64_t cap_ = 0;

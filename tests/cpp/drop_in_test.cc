@@ -8,7 +8,8 @@
 //                   prints the stored value, then CalculateChecksum of the result
 //       verify   -> CalculateChecksum(...) == 0                      (socket-manager.h:182)
 //   drop_in_test layout                      header field layout / H2N / flags / operator<<
-//   drop_in_test batch <n> <seed>            PacketBatch (GPU) vs per-packet CalculateChecksum
+//   drop_in_test batch <n> <seed> [ctxs]     PacketBatch (GPU, ctxs contexts on device 0) vs per-packet
+//                                            CalculateChecksum
 //   drop_in_test segment <bytes> <win> <seed> tcpck_batch_segment (GPU) vs the per-packet send path
 //   drop_in_test receive <n> <slot> <seed>    tcpck_batch_receive (GPU) vs ReceivePacket's verdict + N2H
 #include <tcp_stack/packet-batch.h>
@@ -115,7 +116,7 @@ static int Layout() {
   return 0;
 }
 
-static int Batch(size_t n, unsigned seed) {
+static int Batch(size_t n, unsigned seed, size_t ctxs) {
   std::mt19937_64 rng(seed);
   const size_t lens[] = {0, 64, 576, 1460, 1461, 7, 4000};
   std::vector<std::shared_ptr<TcpPacket>> pkts, copy;
@@ -140,7 +141,7 @@ static int Batch(size_t n, unsigned seed) {
     copy.push_back(MakeNetPacket(b.first, b.second));
     pkts.push_back(std::move(p));
   }
-  PacketBatch batch(0, PacketBatch::Thresholds{1, 1});
+  PacketBatch batch(std::vector<int>(ctxs, 0), PacketBatch::Thresholds{1, 1});
   // checksums as-is
   const std::vector<uint16_t> sums = batch.Checksums(pkts);
   size_t bad = 0;
@@ -321,8 +322,10 @@ int main(int argc, char **argv) {
     return Segment(std::strtoull(argv[2], nullptr, 10), static_cast<uint32_t>(std::atoi(argv[3])), std::atoi(argv[4]));
   if (argc >= 4 && !std::strcmp(argv[1], "golden")) return Golden(argv[2], argv[3]);
   if (argc >= 2 && !std::strcmp(argv[1], "layout")) return Layout();
-  if (argc >= 4 && !std::strcmp(argv[1], "batch")) return Batch(std::strtoull(argv[2], nullptr, 10), std::atoi(argv[3]));
-  std::fprintf(stderr, "usage: %s golden <blob> <manifest> | layout | batch <n> <seed> | segment <bytes> <window> <seed> | receive <n> <slot> <seed>\n",
+  if (argc >= 4 && !std::strcmp(argv[1], "batch"))
+    return Batch(std::strtoull(argv[2], nullptr, 10), std::atoi(argv[3]),
+                 argc >= 5 ? std::strtoull(argv[4], nullptr, 10) : 1);
+  std::fprintf(stderr, "usage: %s golden <blob> <manifest> | layout | batch <n> <seed> [ctxs] | segment <bytes> <window> <seed> | receive <n> <slot> <seed>\n",
                argv[0]);
   return 2;
 }

@@ -85,9 +85,13 @@ def test_layout_and_known_answer(exe, golden):
 
 
 @pytest.mark.gpu
-def test_packet_batch_gpu(built_lib):
+@pytest.mark.parametrize("ctxs", [1, 3])
+def test_packet_batch_gpu(built_lib, ctxs):
+    """PacketBatch over one context, or over three (tcpck_host_batch_var_multi;
+    on a one-GPU box all on device 0): checksums, send-path fill and
+    receive-path verdicts equal the per-packet reference calls."""
     exe = build("opt")
-    lines = run(exe, "batch", 20000, 7)
+    lines = run(exe, "batch", 20000, 7, ctxs)
     assert lines[-1].endswith("mismatches=0"), lines
     assert "gpu_images=0" not in lines[-1]
 
