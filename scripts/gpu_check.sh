@@ -121,7 +121,7 @@ for s in ${STEPS:-tests smoke bench prof}; do
     bench_segment) step bench_segment 600 python bench.py --config segment ;;
     prof_fill) step prof_fill 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_fill -o run --output-format csv -- python3 bench.py --config fill --steps 10 --warmup 2 --no-cpu-baseline --no-e2e ;;
     prof_receive) step prof_receive 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_receive -o run --output-format csv -- python3 bench.py --config receive --steps 10 --warmup 2 --no-cpu-baseline --no-e2e ;;
-    pmc_c2|pmc_c3|pmc_c4|pmc_slots|pmc_segment|pmc_receive|pmc_fill)  # separate FETCH_SIZE / WRITE_SIZE passes (TCC slots), kernel trace only
+    pmc_c2|pmc_c3|pmc_c4|pmc_c5|pmc_slots|pmc_segment|pmc_receive|pmc_fill)  # separate FETCH_SIZE / WRITE_SIZE passes (TCC slots), kernel trace only
       c=${s#pmc_}
       step ${s}_fetch 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d gpurun_out/pmc_${c}_fetch -o run --output-format csv -- python3 bench.py --config $c --steps 3 --warmup 1 --settle-ms 0 --no-cpu-baseline --no-e2e
       step ${s}_write 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d gpurun_out/pmc_${c}_write -o run --output-format csv -- python3 bench.py --config $c --steps 3 --warmup 1 --settle-ms 0 --no-cpu-baseline --no-e2e ;;

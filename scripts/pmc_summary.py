@@ -51,7 +51,7 @@ def main(rnd: str = "r01") -> None:
             summary = json.load(f)
     except (OSError, ValueError):
         summary = {}
-    for cfg in ("c2", "c3", "c4", "slots", "segment", "receive", "fill"):
+    for cfg in ("c2", "c3", "c4", "c5", "slots", "segment", "receive", "fill"):
         fp = os.path.join(src, f"pmc_{cfg}_fetch", "run_counter_collection.csv")
         wp = os.path.join(src, f"pmc_{cfg}_write", "run_counter_collection.csv")
         if not (os.path.exists(fp) and os.path.exists(wp)):
