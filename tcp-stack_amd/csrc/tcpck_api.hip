@@ -639,7 +639,17 @@ namespace {
 // Runs shard i of n as job(i) -- shards 1.. on their own threads, shard 0 on the
 // caller's -- and returns the first nonzero status in shard order.
 template <typename Job>
-int run_shards(int n, Job job) {
+int run_shards(int n, Job job_raw) {
+  // nothing may escape a shard's thread (std::terminate) or the C ABI
+  auto job = [&job_raw](int i) -> int {
+    try {
+      return job_raw(i);
+    } catch (const std::bad_alloc &) {
+      return TCPCK_ENOMEM;
+    } catch (...) {
+      return TCPCK_EINVAL;
+    }
+  };
   std::vector<int> rc(static_cast<size_t>(n), TCPCK_OK);
   std::vector<std::thread> th;
   th.reserve(static_cast<size_t>(n));
