@@ -650,9 +650,14 @@ int run_shards(int n, Job job_raw) {
       return TCPCK_EINVAL;
     }
   };
-  std::vector<int> rc(static_cast<size_t>(n), TCPCK_OK);
+  std::vector<int> rc;
   std::vector<std::thread> th;
-  th.reserve(static_cast<size_t>(n));
+  try {
+    rc.assign(static_cast<size_t>(n), TCPCK_OK);
+    th.reserve(static_cast<size_t>(n));
+  } catch (...) {
+    return TCPCK_ENOMEM;
+  }
   for (int i = 1; i < n; ++i) {
     try {
       th.emplace_back([&rc, &job, i] { rc[static_cast<size_t>(i)] = job(i); });
@@ -1106,7 +1111,12 @@ int tcpck_host_batch_var_multi(tcpck_ctx *const *ctxs, int n_ctx, int op, int mo
   // byte prefix reaches i/n of the total (a 1492-B image is 15.5x a 96-B one)
   uint64_t total = 0;
   for (uint64_t k = 0; k < count; ++k) total += h_lengths[k];
-  std::vector<uint64_t> cut(n + 1, count);
+  std::vector<uint64_t> cut;
+  try {
+    cut.assign(n + 1, count);
+  } catch (...) {
+    return TCPCK_ENOMEM;
+  }
   cut[0] = 0;
   uint64_t pre = 0, k = 0;
   for (uint64_t i = 1; i < n; ++i) {
