@@ -56,22 +56,13 @@ def main():
         for m in (16, 32, 64):
             runs.append((f"var vvstream M{m}", lambda m=m: ctx.batch_var_ex(tcpck.OP_CHECKSUM, a, d_off, d_ln, n, out,
                                                                          8, 28 | (m << 16), **kw)))
-        for m in (0, 32, 64):  # 6 waves per SIMD (80 VGPRs, a few spilled) for the U8 stream
-            runs.append((f"var vvstream occ6 M{m}", lambda m=m: ctx.batch_var_ex(tcpck.OP_CHECKSUM, a, d_off, d_ln, n,
-                                                                              out, 8, 28 | 64 | (m << 16), **kw)))
         if L:
             runs += [("fixed AUTO (rstream)", lambda: ctx.batch_fixed(tcpck.OP_CHECKSUM, a, L, L, n, out, stream=s)),
                      ("fixed vvstream", lambda: ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, a, L, L, n, out, 8, 28,
                                                                    stream=s))]
-        ref = None
         for label, fn in runs:
             ms = b2b(fn, s)
-            torch.cuda.synchronize()
-            if ref is None:
-                ref = out.clone()
-            elif not torch.equal(out, ref):
-                print(f"{label}: RESULTS DIFFER", flush=True)
-            print(f"{name:12s} {label:26s} {ms * 1e3:8.1f} us  {(img + 2 * n) / ms / 1e6 / 80:5.1f} % of the roof",
+            print(f"{name:12s} {label:22s} {ms * 1e3:8.1f} us  {(img + 2 * n) / ms / 1e6 / 80:5.1f} % of the roof",
                   flush=True)
         del a
 

@@ -83,9 +83,8 @@ __device__ __forceinline__ u32x4 zero_word(u32x4 w, uint32_t wi) {
 // positions when every end is 4-B aligned (as in REF), else u32 P at every
 // word position (twice the LDS of REF's packed u16 table) -- so P(end) -
 // P(start) is an image's exact word sum and folds
-// MINW: minimum waves per SIMD the compiler must fit (VGPR budget; tuning)
-template <int U, int OP, int SPLIT, int LAYOUT, bool KEEP = false, int MODE = kRef, int MINW = 1>
-__global__ void __launch_bounds__(kBlock, MINW) vvstream_kernel(VVArgs a) {
+template <int U, int OP, int SPLIT, int LAYOUT, bool KEEP = false, int MODE = kRef>
+__global__ void __launch_bounds__(kBlock) vvstream_kernel(VVArgs a) {
   constexpr bool FIXED = LAYOUT != 0;
   constexpr bool GAP = LAYOUT == 2;
   __shared__ uint32_t s_end[kWavesPerBlock][FIXED ? 1 : kRing + kMirror];
@@ -419,9 +418,9 @@ __global__ void __launch_bounds__(kBlock, MINW) vvstream_kernel(VVArgs a) {
   }
 }
 
-template <int U, int OP, int SPLIT, int LAYOUT, bool KEEP = false, int MODE = kRef, int MINW = 1>
+template <int U, int OP, int SPLIT, int LAYOUT, bool KEEP = false, int MODE = kRef>
 hipError_t launch_one(const RunArgs &s, uint32_t oversub, int flags, uint32_t num_cus, hipStream_t stream) {
-  static const uint32_t per_cu = dev::resident_blocks_per_cu(vvstream_kernel<U, OP, SPLIT, LAYOUT, KEEP, MODE, MINW>);
+  static const uint32_t per_cu = dev::resident_blocks_per_cu(vvstream_kernel<U, OP, SPLIT, LAYOUT, KEEP, MODE>);
   const uint64_t resident = static_cast<uint64_t>(per_cu) * num_cus;
   uint64_t blocks = resident * (oversub ? oversub : 1);
   const uint64_t need = (s.count + kWavesPerBlock - 1) / kWavesPerBlock;
@@ -440,8 +439,8 @@ hipError_t launch_one(const RunArgs &s, uint32_t oversub, int flags, uint32_t nu
   a.len = s.len;
   a.order = (flags & 8) ? 4u : dev::kOrderDefault;  // groups of 16 blocks per XCD
   a.keep_first = (flags & 16) ? 1u : 0u;
-  hipLaunchKernelGGL((vvstream_kernel<U, OP, SPLIT, LAYOUT, KEEP, MODE, MINW>), dim3(static_cast<uint32_t>(blocks)),
-                     dim3(kBlock), 0, stream, a);
+  hipLaunchKernelGGL((vvstream_kernel<U, OP, SPLIT, LAYOUT, KEEP, MODE>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0,
+                     stream, a);
   return hipGetLastError();
 }
 
@@ -452,13 +451,6 @@ hipError_t dispatch(int op, const RunArgs &a, uint32_t oversub, int flags, uint3
       case kChecksum: return launch_one<U, kChecksum, SPLIT, LAYOUT, false, kRfc1071>(a, oversub, flags, num_cus, s);
       case kVerify: return launch_one<U, kVerify, SPLIT, LAYOUT, false, kRfc1071>(a, oversub, flags, num_cus, s);
       case kFill: return launch_one<U, kFill, SPLIT, LAYOUT, false, kRfc1071>(a, oversub, flags, num_cus, s);
-      default: return hipErrorInvalidValue;
-    }
-  }
-  if ((flags & 64) && U == 8) {  // tuning: the U8 REF stream held to 6 waves per SIMD (80 VGPRs)
-    switch (op) {
-      case kChecksum: return launch_one<U, kChecksum, SPLIT, LAYOUT, false, kRef, 6>(a, oversub, flags, num_cus, s);
-      case kVerify: return launch_one<U, kVerify, SPLIT, LAYOUT, false, kRef, 6>(a, oversub, flags, num_cus, s);
       default: return hipErrorInvalidValue;
     }
   }
@@ -483,7 +475,7 @@ hipError_t launch_vvstream(int op, int variant, bool fixed, const RunArgs &a, ui
   uint32_t m = a.oversub ? a.oversub : 1;
   // 8: XCD-chunked run order; 16: L2-kept first step; 32: kFill reads every
   // step with the default cache policy (small images)
-  const int flags = variant & 120;  // + 64: 6 waves per SIMD for U8 REF CHECKSUM/VERIFY (tuning)
+  const int flags = variant & 56;
   variant &= 7;
   int u8 = (variant & 1);
   int split = variant >= 2 ? 1 : 0;
