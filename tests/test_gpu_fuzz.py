@@ -5,9 +5,16 @@ unordered offset lists, empty and jumbo images, misaligned arenas, both modes,
 every op (RECEIVE in place and into a header array too), right and wrong SORTED
 hints -- each checked against the oracle (oracle/ref16.c, pinned to the
 reference's golden vectors).  Sizes stay small (<= 16 MB per case); the seeds
-are fixed, so a failure names a reproducible case."""
+are fixed, so a failure names a reproducible case.  TCPCK_FUZZ_BASE /
+TCPCK_FUZZ_SEEDS (environment) shift and widen the seed range for longer bug
+hunts (defaults: 0 and 200 / 200 / 80)."""
+import os
+
 import numpy as np
 import pytest
+
+BASE = int(os.environ.get("TCPCK_FUZZ_BASE", "0"))
+NSEEDS = int(os.environ.get("TCPCK_FUZZ_SEEDS", "0"))
 
 pytestmark = pytest.mark.gpu
 
@@ -69,7 +76,7 @@ def check_receive(ctx, arena_np, mis, offs, lens, mode, seed, layout):
     np.testing.assert_array_equal(host(ok), exp_ok)
 
 
-@pytest.mark.parametrize("seed", range(200))
+@pytest.mark.parametrize("seed", range(BASE, BASE + (NSEEDS or 200)))
 def test_fuzz_fixed(ctx, oracle_c, seed):
     import tcpck
     rng = np.random.default_rng(1000 + seed)
@@ -110,7 +117,7 @@ def test_fuzz_fixed(ctx, oracle_c, seed):
                       mode, seed, dict(stride=stride, length=length))
 
 
-@pytest.mark.parametrize("seed", range(200))
+@pytest.mark.parametrize("seed", range(BASE, BASE + (NSEEDS or 200)))
 def test_fuzz_var(ctx, oracle_c, seed):
     import tcpck
     rng = np.random.default_rng(2000 + seed)
@@ -173,7 +180,7 @@ def test_fuzz_var(ctx, oracle_c, seed):
                       dict(offsets=d_off, lengths=d_ln, **hints))
 
 
-@pytest.mark.parametrize("seed", range(80))
+@pytest.mark.parametrize("seed", range(BASE, BASE + (NSEEDS or 80)))
 def test_fuzz_segment(ctx, seed):
     from oracle import ref16 as R
     rng = np.random.default_rng(3000 + seed)
