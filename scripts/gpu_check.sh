@@ -88,6 +88,7 @@ for s in ${STEPS:-tests smoke bench prof}; do
     multi) step multi_tests 600 python -u -m pytest tests/test_gpu_multi_ctx.py -x -q --timeout 120 --timeout-method thread &&
       step multi 300 python scripts/e2e_multi_probe.py ;;
     c4shape) step c4shape 600 python scripts/c4_shape_probe.py ;;
+    recheck) step recheck 600 python scripts/slots_seg_recheck.py ;;
     copy) step copy 600 python scripts/copy_probe.py ;;
     fuzz) step fuzz_tests 600 python -u -m pytest tests/test_gpu_fuzz.py -x -q --timeout 120 --timeout-method thread ;;
     receive) step receive_tests 300 python -u -m pytest tests/test_gpu_receive.py -x -q --timeout 120 --timeout-method thread &&
