@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """bench.py -- device-resident batched TCP checksum on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5|...]
 
 A step = one pass of the hot path (one tcpck_batch_* CHECKSUM launch) over one
 batch of synthetic segments already resident in HBM.  Default workload (N=1)
@@ -10,8 +10,8 @@ payload = 1492-B checksummed images (32-B pseudo+TCP header + payload,
 SURVEY.md fact 3), fixed stride.  With N>1 GPUs (one process per GPU via
 torch.distributed.run) every rank checksums its own 1M-image shard
 (first_index = rank * count, shard-reproducible generator), no data-path
-collective: at N=8 this is configs[4] (C5, 8M segments over 8 GPUs), weak
-scaling.  Rank 0 prints ONE JSON line with the driver's fields plus:
+collective: weak scaling, so SCALE's N=1 line is BENCH's line.  Rank 0 prints
+ONE JSON line with the driver's fields plus:
 
   roofline      dominant kernel vs the HBM-read roof (8.0 TB/s): achieved =
                 algorithmic bytes per launch (sum of image bytes + 2 B written
@@ -19,10 +19,18 @@ scaling.  Rank 0 prints ONE JSON line with the driver's fields plus:
                 stream around the K launches, / K); traffic = PMC HBM bytes
                 per launch from the committed rocprofv3 pass
                 (profiles/pmc_summary.json), else null
+  c3, c4        (default C2 run only) BASELINE configs[2] and [3] timed the same
+                way in the same process, after C2: each rank its own batch
+  c5_strong     (default C2 run only) BASELINE configs[4]: ONE 8M x 1492-B batch
+                split over the N ranks with shard_range (8M images on one GPU
+                at N=1, 1M per GPU at N=8); value = all ranks' bytes / the
+                slowest rank's wall time per step, kernel_GiBs = / the slowest
+                rank's kernel time, per_gpu_frac = each GPU's roofline fraction
   cpu_baseline  the reference's own CalculateChecksum (oracle/_ref, built from
-                /root/reference/include/tcp-header.h) on the host cores, on a
-                bounded sample of the same images (rank 0, N=1 only); falls back
-                to the in-repo C restatement ("port") where oracle/_ref is absent
+                /root/reference/include/tcp-header.h) on the host cores over the
+                whole C2 arena (DRAM-sized: 6x the host L3), median of 5 passes
+                (rank 0, N=1 only); falls back to the in-repo C restatement
+                ("port") where oracle/_ref is absent
   e2e           host-memory rate incl. pinned hipMemcpyAsync H2D + D2H (not `value`)
   settle        untimed launches run before the W warm-up steps until --settle-ms
                 has passed (the idle GPU's clock ramp, scripts/transient.py)
@@ -32,6 +40,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import statistics
 import sys
 import time
 
@@ -57,6 +66,8 @@ CONFIGS = {
            "fixed", 8 << 20, 1492),
 }
 STRONG = {"c5"}  # configs whose total work is fixed as N grows; the rest are per-GPU (weak)
+# the other BASELINE configs timed inside the default (C2) run, and their keys in its line
+EXTRAS = (("c3", "c3"), ("c4", "c4"), ("c5", "c5_strong"))
 # round-2 ops (not BASELINE configs; same contract, their own metric):
 EXTRA = {
     # the device-resident receive arena: 1M 2048-B slots, one datagram per slot
@@ -89,9 +100,10 @@ def parse():
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--config", default="c2", choices=sorted(CONFIGS) + ["c1"] + sorted(EXTRA))
-    p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline time budget")
+    p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline time budget (5 passes)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-e2e", action="store_true")
+    p.add_argument("--no-extras", action="store_true", help="default run: skip the c3/c4/c5_strong keys")
     p.add_argument("--settle-ms", type=float, default=250.0,
                    help="untimed back-to-back launches before the warm-up steps (clock ramp)")
     p.add_argument("--per-launch-events", action="store_true",
@@ -132,6 +144,202 @@ def bench_c1(args):
     print(json.dumps(rec), flush=True)
 
 
+class Workload:
+    """One config's device-resident batch on this rank and its step function."""
+
+    def __init__(self, name, ctx, stream, rank, world):
+        import torch
+        import tcpck
+        from tcpck.shard import shard_range
+        desc, kind, count, L = CONFIGS[name] if name in CONFIGS else EXTRA[name]
+        self.name, self.desc, self.kind, self.L = name, desc, kind, L
+        self.strong = name in STRONG
+        if self.strong:
+            first, stop = shard_range(count, world, rank)  # independent contiguous shard, no exchange
+            count = stop - first
+        else:
+            first = rank * count  # weak: every rank checksums its own batch of the config's size
+        self.extra_bytes = 0  # algorithmic bytes per launch beyond the image bytes read (+2 per result)
+        self.layout = None
+        self.arena = None
+        if kind in ("slots", "receive"):
+            rng = np.random.default_rng(42 + rank)
+            ln = (np.asarray((64, 576, 1460), np.uint32)[rng.integers(0, 3, count)] + 32).astype(np.uint32)
+            off = np.arange(count, dtype=np.uint64) * np.uint64(L)
+            arena = torch.empty(count * L, dtype=torch.uint8, device="cuda")
+            d_off, d_ln = torch.from_numpy(off).cuda(), torch.from_numpy(ln).cuda()
+            tcpck.synth_var(arena, d_off, d_ln, 1492, count, seed=42, first_index=first, stream=stream)
+            img_bytes = int(ln.astype(np.int64).sum())
+            lmin, lmax = int(ln.min()), int(ln.max())
+
+            if kind == "slots":
+                def step(out):
+                    ctx.batch_var(tcpck.OP_VERIFY, arena, d_off, d_ln, count, out, total_bytes=img_bytes,
+                                  min_len=lmin, max_len=lmax, sorted=True, stream=stream)
+            else:
+                hdr_out = torch.empty(count * 32, dtype=torch.uint8, device="cuda")
+                self.extra_bytes = 32 * count  # the header array written
+
+                def step(out):
+                    ctx.batch_receive(arena, count, out, hdr_out, offsets=d_off, lengths=d_ln,
+                                      total_bytes=img_bytes, min_len=lmin, max_len=lmax, sorted=True,
+                                      stream=stream)
+        elif kind == "segment":
+            P, seg, stride = count, L, 1504
+            payload = torch.empty(P, dtype=torch.uint8, device="cuda")
+            tcpck.synth_fixed(payload, 1492, 1492, P // 1492, seed=42, first_index=first, stream=stream)
+            count = (P + seg - 1) // seg
+            images = torch.empty(count * stride, dtype=torch.uint8, device="cuda")
+            hdr = np.zeros(32, np.uint8)
+            hdr[0:4], hdr[4:8], hdr[12:14], hdr[14:16] = [127, 0, 0, 1], [127, 0, 0, 1], [0x3C, 0x8C], [0x3C, 0x8D]
+            hdr[20:24], hdr[25] = [0, 0, 0x1E, 0x61], 0x08  # ack 7777, ACK (state.cc:178-180)
+            img_bytes = P  # the stream read
+            self.extra_bytes = P + 32 * count  # the images written (header + payload; slot padding excluded)
+
+            def step(out):
+                ctx.batch_segment(payload, P, seg, hdr, 1001, images, stride, out, stream=stream)
+        elif kind == "fill":
+            arena = torch.empty(count * L, dtype=torch.uint8, device="cuda")
+            tcpck.synth_fixed(arena, L, L, count, seed=42, first_index=first, stream=stream)
+            img_bytes = count * L
+            self.extra_bytes = 2 * count  # the fields written in place (+2 per result below)
+
+            def step(out):
+                ctx.batch_fixed(tcpck.OP_FILL, arena, L, L, count, out, stream=stream)
+        elif kind == "fixed":
+            arena = torch.empty(count * L, dtype=torch.uint8, device="cuda")
+            tcpck.synth_fixed(arena, L, L, count, seed=42, first_index=first, stream=stream)
+            img_bytes = count * L
+
+            def step(out):
+                ctx.batch_fixed(tcpck.OP_CHECKSUM, arena, L, L, count, out, stream=stream)
+        else:
+            from synth_np import mixed_layout
+            off, ln, total = mixed_layout(count, seed=42 + rank)
+            arena = torch.empty(total, dtype=torch.uint8, device="cuda")
+            d_off = torch.from_numpy(off).cuda()
+            d_ln = torch.from_numpy(ln).cuda()
+            tcpck.synth_var(arena, d_off, d_ln, 1492, count, seed=42, first_index=first, stream=stream)
+            img_bytes = int(ln.astype(np.int64).sum())
+            lmin, lmax = int(ln.min()), int(ln.max())  # host-side layout hint, computed once
+            self.layout = (off, ln)
+
+            def step(out):
+                ctx.batch_var(tcpck.OP_CHECKSUM, arena, d_off, d_ln, count, out, total_bytes=img_bytes,
+                              min_len=lmin, max_len=lmax, packed=True, stream=stream)
+        self.arena = arena if kind in ("fixed", "mixed", "fill", "slots", "receive") else None
+        self.count, self.first, self.img_bytes = count, first, img_bytes
+        self.verdicts = kind in ("slots", "receive")  # u8 results
+        self.out = torch.empty(count, dtype=torch.uint8 if self.verdicts else torch.int16, device="cuda")
+        self._step = step
+        torch.cuda.synchronize()
+
+    def step(self):
+        self._step(self.out)
+
+    @property
+    def algo_bytes(self) -> int:
+        """Algorithmic bytes per launch: image bytes read + other bytes written + the results."""
+        return self.img_bytes + self.extra_bytes + (1 if self.verdicts else 2) * self.count
+
+    def results(self) -> np.ndarray:
+        import torch
+        res = self.out.cpu().numpy()
+        return res.view(np.uint16) if self.out.dtype == torch.int16 else res
+
+
+def measure(w: Workload, args, world, stream, coll_dev):
+    """Settle, warm up, then time exactly K steps between barrier + synchronize
+    brackets.  Returns (slowest rank's wall seconds, this rank's per-launch ms,
+    every rank's per-launch ms, the bytes all ranks read per step, settle info)."""
+    import torch
+    import torch.distributed as dist
+    from tcpck.shard import gather_ranks, max_over_ranks
+    # Settle: an idle MI355X takes 10-50 ms of back-to-back HBM streaming to
+    # reach its steady clocks (scripts/transient.py, profiles/r01/transient.log:
+    # C3 launches run at 54-79% of the roof for the first ~50 ms, then 83-84%).
+    # Untimed launches of the same step until settle_ms have passed, then the W
+    # warm-up steps; neither is in the timed region.
+    settled, t_set = 0, time.perf_counter()
+    while (time.perf_counter() - t_set) * 1e3 < args.settle_ms:
+        for _ in range(8):
+            w.step()
+        torch.cuda.synchronize()
+        settled += 8
+    settle_ms = (time.perf_counter() - t_set) * 1e3
+    for _ in range(args.warmup):
+        w.step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    # HIP events on the launch stream bracket the K launches.  An event recorded
+    # between two launches costs ~10 us of idle GPU per step on ROCm (rocprof
+    # trace: 0 us between back-to-back launches, 10-11 us with per-launch
+    # events), so the per-launch average is the bracket / K; it includes the
+    # (near-zero) kernel boundaries, so it can only under-state the kernel rate.
+    # --per-launch-events restores one event pair per launch (diagnostics).
+    n_ev = args.steps if args.per_launch_events else 1
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(n_ev)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(n_ev)]
+    t0 = time.perf_counter()
+    if not args.per_launch_events:
+        starts[0].record(stream)
+    for i in range(args.steps):
+        if args.per_launch_events:
+            starts[i].record(stream)
+        w.step()
+        if args.per_launch_events:
+            ends[i].record(stream)
+    if not args.per_launch_events:
+        ends[0].record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    launch_ms = float(np.sum([s.elapsed_time(e) for s, e in zip(starts, ends)])) / args.steps
+    tmax = max_over_ranks(elapsed, device=coll_dev)
+    launch_ms_all = gather_ranks(launch_ms, device=coll_dev)  # per-GPU kernel time (ranks start together)
+    shard_bytes = torch.tensor([w.img_bytes], dtype=torch.int64, device=coll_dev)
+    if world > 1:
+        dist.all_reduce(shard_bytes)  # bytes all ranks processed per step (shards may differ by one image)
+    settle = {"ms": round(settle_ms, 1), "launches": settled,
+              "why": "untimed launches before the W warm-ups: the idle GPU's clock ramp lasts 10-50 ms"}
+    return tmax, launch_ms, launch_ms_all, int(shard_bytes.item()), settle
+
+
+def roofline(w: Workload, launch_ms, launch_ms_all, traffic_key, world):
+    algo = w.algo_bytes
+    achieved = algo / (launch_ms * 1e-3) / 1e9
+    r = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(traffic_key) if world == 1 else None,
+         "algorithmic_bytes_per_launch": algo, "avg_launch_ms": round(launch_ms, 5)}
+    if world > 1:  # rank 0's kernel above; every GPU's fraction here (equal shards)
+        r["per_gpu_frac"] = [round(algo / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) for ms in launch_ms_all]
+    return r
+
+
+def extra_config(name, key, ctx, stream, rank, world, args, coll_dev):
+    """Another BASELINE config timed in the default run; its record for rank 0's line."""
+    import torch
+    w = Workload(name, ctx, stream, rank, world)
+    tmax, launch_ms, launch_ms_all, step_bytes, settle = measure(w, args, world, stream, coll_dev)
+    rec = {"workload": w.desc, "value": round(step_bytes * args.steps / tmax / GIB, 2), "unit": "GiB/s",
+           "ms_per_step": round(tmax / args.steps * 1e3, 5), "scaling": "strong" if w.strong else "weak",
+           "images_per_gpu": w.count, "bytes_per_gpu": w.img_bytes,
+           "roofline": roofline(w, launch_ms, launch_ms_all, name, world), "settle": settle}
+    if w.strong:
+        # the 8M-image batch's bytes over the slowest GPU's kernel time (SURVEY.md §8e)
+        rec["kernel_GiBs"] = round(step_bytes / (max(launch_ms_all) * 1e-3) / GIB, 2)
+        rec["images_total"] = CONFIGS[name][2]
+        rec["parallelism"] = f"shard{world}: one batch split by tcpck.shard.shard_range, no collective"
+    del w
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return key, rec
+
+
 def main():
     args = parse()
     if args.config == "c1":
@@ -158,199 +366,76 @@ def main():
         else:
             dist.init_process_group(backend)
 
-    from tcpck.shard import gather_ranks, max_over_ranks, shard_range
-    desc, kind, count, L = CONFIGS[args.config] if args.config in CONFIGS else EXTRA[args.config]
+    from tcpck.shard import gather_ranks, max_over_ranks
     ctx = tcpck.Context(local)
     stream = torch.cuda.current_stream()
-    if args.config in STRONG:
-        first, stop = shard_range(count, world, rank)  # independent contiguous shard, no exchange
-        count = stop - first
-    else:
-        first = rank * count  # weak: every rank checksums its own batch of the config's size
-    extra_bytes = 0  # algorithmic bytes per launch beyond the image bytes read (+2 per result)
-    if kind in ("slots", "receive"):
-        rng = np.random.default_rng(42 + rank)
-        ln = (np.asarray((64, 576, 1460), np.uint32)[rng.integers(0, 3, count)] + 32).astype(np.uint32)
-        off = np.arange(count, dtype=np.uint64) * np.uint64(L)
-        arena = torch.empty(count * L, dtype=torch.uint8, device="cuda")
-        d_off, d_ln = torch.from_numpy(off).cuda(), torch.from_numpy(ln).cuda()
-        tcpck.synth_var(arena, d_off, d_ln, 1492, count, seed=42, first_index=first, stream=stream)
-        img_bytes = int(ln.astype(np.int64).sum())
-        lmin, lmax = int(ln.min()), int(ln.max())
-
-        if kind == "slots":
-            def step(out):
-                ctx.batch_var(tcpck.OP_VERIFY, arena, d_off, d_ln, count, out, total_bytes=img_bytes,
-                              min_len=lmin, max_len=lmax, sorted=True, stream=stream)
-        else:
-            hdr_out = torch.empty(count * 32, dtype=torch.uint8, device="cuda")
-            extra_bytes = 32 * count  # the header array written
-
-            def step(out):
-                ctx.batch_receive(arena, count, out, hdr_out, offsets=d_off, lengths=d_ln, total_bytes=img_bytes,
-                                  min_len=lmin, max_len=lmax, sorted=True, stream=stream)
-    elif kind == "segment":
-        P, seg, stride = count, L, 1504
-        payload = torch.empty(P, dtype=torch.uint8, device="cuda")
-        tcpck.synth_fixed(payload, 1492, 1492, P // 1492, seed=42, first_index=first, stream=stream)
-        count = (P + seg - 1) // seg
-        images = torch.empty(count * stride, dtype=torch.uint8, device="cuda")
-        hdr = np.zeros(32, np.uint8)
-        hdr[0:4], hdr[4:8], hdr[12:14], hdr[14:16] = [127, 0, 0, 1], [127, 0, 0, 1], [0x3C, 0x8C], [0x3C, 0x8D]
-        hdr[20:24], hdr[25] = [0, 0, 0x1E, 0x61], 0x08  # ack 7777, ACK (state.cc:178-180)
-        img_bytes = P  # the stream read
-        extra_bytes = P + 32 * count  # the images written (header + payload; slot padding excluded)
-
-        def step(out):
-            ctx.batch_segment(payload, P, seg, hdr, 1001, images, stride, out, stream=stream)
-    elif kind == "fill":
-        arena = torch.empty(count * L, dtype=torch.uint8, device="cuda")
-        tcpck.synth_fixed(arena, L, L, count, seed=42, first_index=first, stream=stream)
-        img_bytes = count * L
-        extra_bytes = 2 * count  # the fields written in place (+2 per result below)
-
-        def step(out):
-            ctx.batch_fixed(tcpck.OP_FILL, arena, L, L, count, out, stream=stream)
-    elif kind == "fixed":
-        arena = torch.empty(count * L, dtype=torch.uint8, device="cuda")
-        tcpck.synth_fixed(arena, L, L, count, seed=42, first_index=first, stream=stream)
-        img_bytes = count * L
-
-        def step(out):
-            ctx.batch_fixed(tcpck.OP_CHECKSUM, arena, L, L, count, out, stream=stream)
-    else:
-        from synth_np import mixed_layout
-        off, ln, total = mixed_layout(count, seed=42 + rank)
-        arena = torch.empty(total, dtype=torch.uint8, device="cuda")
-        d_off = torch.from_numpy(off).cuda()
-        d_ln = torch.from_numpy(ln).cuda()
-        tcpck.synth_var(arena, d_off, d_ln, 1492, count, seed=42, first_index=first, stream=stream)
-        img_bytes = int(ln.astype(np.int64).sum())
-        lmin, lmax = int(ln.min()), int(ln.max())  # host-side layout hint, computed once
-
-        def step(out):
-            ctx.batch_var(tcpck.OP_CHECKSUM, arena, d_off, d_ln, count, out, total_bytes=img_bytes,
-                          min_len=lmin, max_len=lmax, packed=True, stream=stream)
-    verdicts = kind in ("slots", "receive")  # u8 results
-    out = torch.empty(count, dtype=torch.uint8 if verdicts else torch.int16, device="cuda")
-    torch.cuda.synchronize()
-
-    # Settle: an idle MI355X takes 10-50 ms of back-to-back HBM streaming to
-    # reach its steady clocks (scripts/transient.py, profiles/r01/transient.log:
-    # C3 launches run at 54-79% of the roof for the first ~50 ms, then 83-84%).
-    # Untimed launches of the same step until settle_ms have passed, then the W
-    # warm-up steps; neither is in the timed region.
-    settled, t_set = 0, time.perf_counter()
-    while (time.perf_counter() - t_set) * 1e3 < args.settle_ms:
-        for _ in range(8):
-            step(out)
-        torch.cuda.synchronize()
-        settled += 8
-    settle_ms = (time.perf_counter() - t_set) * 1e3
-    for _ in range(args.warmup):
-        step(out)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    # HIP events on the launch stream bracket the K launches.  An event recorded
-    # between two launches costs ~10 us of idle GPU per step on ROCm (rocprof
-    # trace: 0 us between back-to-back launches, 10-11 us with per-launch
-    # events), so the per-launch average is the bracket / K; it includes the
-    # (near-zero) kernel boundaries, so it can only under-state the kernel rate.
-    # --per-launch-events restores one event pair per launch (diagnostics).
-    n_ev = args.steps if args.per_launch_events else 1
-    starts = [torch.cuda.Event(enable_timing=True) for _ in range(n_ev)]
-    ends = [torch.cuda.Event(enable_timing=True) for _ in range(n_ev)]
-    t0 = time.perf_counter()
-    if not args.per_launch_events:
-        starts[0].record(stream)
-    for i in range(args.steps):
-        if args.per_launch_events:
-            starts[i].record(stream)
-        step(out)
-        if args.per_launch_events:
-            ends[i].record(stream)
-    if not args.per_launch_events:
-        ends[0].record(stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    launch_ms = float(np.sum([s.elapsed_time(e) for s, e in zip(starts, ends)])) / args.steps
-
-    tmax = max_over_ranks(elapsed, device=coll_dev)
-    launch_ms_all = gather_ranks(launch_ms, device=coll_dev)  # per-GPU kernel time (ranks start together)
-    shard_bytes = torch.tensor([img_bytes], dtype=torch.int64, device=coll_dev)
-    if world > 1:
-        dist.all_reduce(shard_bytes)  # bytes all ranks processed per step (shards may differ by one image)
-    total_bytes = int(shard_bytes.item()) * args.steps
-    value = total_bytes / tmax / GIB
-
-    # Checksum digest of this rank's results (parity spot-check on the host below).
-    res = out.cpu().numpy().view(np.uint16) if out.dtype == torch.int16 else out.cpu().numpy()
+    w = Workload(args.config, ctx, stream, rank, world)
+    tmax, launch_ms, launch_ms_all, step_bytes, settle = measure(w, args, world, stream, coll_dev)
+    value = step_bytes * args.steps / tmax / GIB
+    res = w.results()  # checksum results of this rank (the CPU baseline compares them)
 
     # End to end through PCIe (never `value`): every rank at once, so the
     # driver's N-GPU runs also record the host-memory path's aggregate rate
     e2e = None
-    if not args.no_e2e and kind == "fixed" and args.config not in STRONG:
+    if not args.no_e2e and w.kind == "fixed" and not w.strong:
         if world > 1:
             dist.barrier()
-        dt, ok = e2e_seconds(ctx, arena, res, count, L)
+        dt, ok = e2e_seconds(ctx, w.arena, res, w.count, w.L)
         dt_max = max_over_ranks(dt, device=coll_dev)
         ok_all = min(gather_ranks(1.0 if ok else 0.0, device=coll_dev)) > 0
         if np.isfinite(dt_max):
-            e2e = {"value": round(world * count * L / dt_max / GIB, 2), "unit": "GiB/s",
+            e2e = {"value": round(world * w.count * w.L / dt_max / GIB, 2), "unit": "GiB/s",
                    "what": "pinned host arena -> 64 MiB chunks H2D on 2 streams -> kernel -> u16 results D2H, "
                            f"all {world} rank(s) at once, whole-job bytes / slowest rank",
                    "results_match_device_path": ok_all}
 
-    if rank != 0:
-        if world > 1:
-            dist.barrier()
-            dist.destroy_process_group()
-        return
-
-    algo_bytes = img_bytes + extra_bytes + (1 if verdicts else 2) * count  # + the results written
-    achieved = algo_bytes / (launch_ms * 1e-3) / 1e9
-    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(args.config),
-                "algorithmic_bytes_per_launch": algo_bytes, "avg_launch_ms": round(launch_ms, 5)}
-    if world > 1:  # rank 0's kernel above; every GPU's fraction here (equal shards)
-        roofline["per_gpu_frac"] = [round(algo_bytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) for ms in launch_ms_all]
-
-    metric = METRIC
-    if kind == "slots":
-        metric = "GiB/s device-resident TCP verify over a slotted receive arena (image bytes); % HBM roofline"
-    elif kind == "fill":
-        metric = "GiB/s device-resident TCP send-side fill (zero, checksum, store in place) over batched segments; % HBM roofline"
-    elif kind == "receive":
-        metric = ("GiB/s device-resident TCP receive (verify + TcpHeaderN2H into a header array) over a slotted "
-                  "receive arena (image bytes); % HBM roofline (read + write)")
-    elif kind == "segment":
-        metric = "GiB/s of device-resident send stream segmented into checksummed images; % HBM roofline (read + write)"
+    want_cpu = rank == 0 and world == 1 and not args.no_cpu_baseline and w.kind in ("fixed", "mixed")
+    host_arena = w.arena.cpu().numpy() if want_cpu else None
     rec = {
-        "metric": metric, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world,
+        "metric": metric_for(w.kind), "value": round(value, 2), "unit": "GiB/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(tmax / args.steps * 1e3, 5),
         "higher_is_better": True,
-        "scaling": "strong" if args.config in STRONG else "weak", "vs_baseline": None, "dtype": "u16",
+        "scaling": "strong" if w.strong else "weak", "vs_baseline": None, "dtype": "u16",
         "data": "synthetic (device-generated: send-path headers + splitmix64 payloads, seed 42)",
-        "config": {"workload": desc, "images_per_gpu": count, "image_bytes": IMAGE_BYTES.get(kind, L if L else "96/608/1492"),
-                   "bytes_per_gpu": img_bytes, "parallelism": f"shard{world} (independent per-GPU batches, no collective)"},
-        "roofline": roofline,
-        "settle": {"ms": round(settle_ms, 1), "launches": settled,
-                   "why": "untimed launches before the W warm-ups: the idle GPU's clock ramp lasts 10-50 ms"},
+        "config": {"workload": w.desc, "images_per_gpu": w.count,
+                   "image_bytes": IMAGE_BYTES.get(w.kind, w.L if w.L else "96/608/1492"),
+                   "bytes_per_gpu": w.img_bytes,
+                   "parallelism": f"shard{world} (independent per-GPU batches, no collective)"},
+        "roofline": roofline(w, launch_ms, launch_ms_all, args.config, world),
+        "settle": settle,
     }
-    if world == 1 and not args.no_cpu_baseline and kind in ("fixed", "mixed"):
-        rec["cpu_baseline"] = cpu_baseline(arena, res, kind, count, L, args.cpu_seconds,
-                                           None if kind == "fixed" else (off, ln))
+    kind, count, L, layout = w.kind, w.count, w.L, w.layout
+    del w
+    torch.cuda.empty_cache()
+
+    # The other BASELINE configs, driver-timed in the same process (default run only)
+    if args.config == "c2" and not args.no_extras:
+        for name, key in EXTRAS:
+            k, r = extra_config(name, key, ctx, stream, rank, world, args, coll_dev)
+            rec[k] = r
+    if want_cpu:
+        rec["cpu_baseline"] = cpu_baseline(host_arena, res, kind, count, L, args.cpu_seconds, layout)
     if e2e is not None:
         rec["e2e"] = e2e
-    print(json.dumps(rec), flush=True)
+    if rank == 0:
+        print(json.dumps(rec), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    ctx.close()
+
+
+def metric_for(kind):
+    if kind == "slots":
+        return "GiB/s device-resident TCP verify over a slotted receive arena (image bytes); % HBM roofline"
+    if kind == "fill":
+        return "GiB/s device-resident TCP send-side fill (zero, checksum, store in place) over batched segments; % HBM roofline"
+    if kind == "receive":
+        return ("GiB/s device-resident TCP receive (verify + TcpHeaderN2H into a header array) over a slotted "
+                "receive arena (image bytes); % HBM roofline (read + write)")
+    if kind == "segment":
+        return "GiB/s of device-resident send stream segmented into checksummed images; % HBM roofline (read + write)"
+    return METRIC
 
 
 def pmc_traffic(config: str):
@@ -364,74 +449,72 @@ def pmc_traffic(config: str):
         return None
 
 
-def cpu_threads() -> int:
-    n = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
-    if n <= 0:
-        n = os.cpu_count() or 1
-    return max(1, min(n, 16))
+def cpu_threads() -> tuple[int, dict]:
+    """Threads for the CPU baseline: this process's CPU share.  The GPU box
+    gives one GPU's job a 16-CPU share (OMP_NUM_THREADS=16 there; nproc and
+    the affinity mask show the whole machine), so the baseline uses
+    min(affinity, OMP_NUM_THREADS) threads and reports all three counts."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    n = min(aff, omp) if omp > 0 else aff
+    return max(1, n), {"affinity_cpus": aff, "nproc": os.cpu_count(), "omp_num_threads": omp or None}
 
 
-def cpu_baseline(arena, gpu_res, kind, count, L, budget_s, var_layout):
-    """Reference CalculateChecksum on host cores over a bounded sample of the same images."""
+def cpu_baseline(host_arena, gpu_res, kind, count, L, budget_s, var_layout):
+    """Reference CalculateChecksum on the host cores over the WHOLE batch (the
+    C2 arena is 1.56 GB, ~6x the host's 256 MB L3, so the passes stream from
+    DRAM like the GPU's): 5 timed passes of `reps` sweeps each, median."""
     from oracle import ref16 as R
-    nthr = cpu_threads()
+    nthr, counts = cpu_threads()
     if kind == "fixed":
-        n = min(count, max(1, (256 << 20) // L))
-        sample = arena[: n * L].cpu().numpy()
-        sargs = dict(stride=L, length=L, count=n)
-        sbytes = n * L
-        sdesc = f"first {n} of the batch's {L}-B images ({sbytes / 1e6:.0f} MB), repeated"
+        sargs = dict(stride=L, length=L, count=count)
+        sbytes = count * L
     else:
         off, ln = var_layout
-        n = min(count, 1 << 18)
-        end = int(off[n - 1] + ln[n - 1])
-        sample = arena[:end].cpu().numpy()
-        sargs = dict(offsets=off[:n], lengths=ln[:n])
-        sbytes = int(ln[:n].astype(np.int64).sum())
-        sdesc = f"first {n} images of the batch ({sbytes / 1e6:.0f} MB), repeated"
-    pk = None
+        sargs = dict(offsets=off, lengths=ln)
+        sbytes = int(ln.astype(np.int64).sum())
+    sdesc = f"all {count} images of the batch ({sbytes / 1e9:.2f} GB, host copy), MakeNetPacket once"
+    out = {"unit": "GiB/s", "cores": nthr, **counts}
     if R.RefLib.available("O3"):
         kind_s = "reference"
-        pk = R.RefLib("O3").packets(sample, **sargs)  # MakeNetPacket once, outside timing
-        run = pk.run
+        pk = R.RefLib("O3").packets(host_arena, **sargs)  # MakeNetPacket once, outside timing
+
+        def passes(lib_pk, threads, n_pass, target_s):
+            """Median GiB/s over n_pass timed passes of ~target_s each."""
+            t1 = lib_pk.run_reps(threads, 1)
+            reps = max(1, int(target_s / max(t1, 1e-6)))
+            rates = [sbytes * reps / lib_pk.run_reps(threads, reps) / GIB for _ in range(n_pass)]
+            return statistics.median(rates), rates, reps
+
+        got, _ = pk.run(nthr)
+        match = bool(np.array_equal(got, gpu_res[:count]))
+        med, rates, reps = passes(pk, nthr, 5, budget_s / 5)
+        one, _, _ = passes(pk, 1, 1, 0.5)
+        pk.close()
+        out.update({"value": round(med, 2), "kind": kind_s, "one_thread_GiBs": round(one, 2),
+                    "passes_GiBs": [round(r, 1) for r in rates],
+                    "sample": sdesc + f"; median of 5 passes of {reps} sweeps on {nthr} threads; CalculateChecksum "
+                              f"(tcp-header.h:252-263) built -O3 -march=x86-64-v3; results == GPU results: {match}"})
+        if R.RefLib.available("O0"):
+            # secondary: the reference as its makefile builds it (-O0 -g, makefile:2), same threads
+            p0 = R.RefLib("O0").packets(host_arena, **sargs)
+            med0, rates0, _ = passes(p0, nthr, 5, 0.3)
+            p0.close()
+            out["reference_O0_GiBs"] = round(med0, 2)
+            out["reference_O0_note"] = f"-O0 -g build (makefile:2), median of 5 passes on {nthr} threads"
     else:
         c = R.Ref16C(build=False)
-        kind_s = "port"
-
-        def run(threads):
+        t0 = time.perf_counter()
+        got = c.batch(host_arena, threads=nthr, **sargs)
+        dt = []
+        for _ in range(5):
             t0 = time.perf_counter()
-            r = c.batch(sample, threads=threads, **sargs)
-            return r, time.perf_counter() - t0
-    got, _ = run(nthr)
-    match = bool(np.array_equal(got, gpu_res[:n]))
-    secs, reps = 0.0, 0
-    w0 = time.perf_counter()
-    while secs < budget_s and time.perf_counter() - w0 < 2 * budget_s:
-        _, s = run(nthr)
-        secs += s
-        reps += 1
-    rate = sbytes * reps / secs / GIB
-    _, s1 = run(1)
-    rate1 = sbytes / s1 / GIB
-    if pk is not None:
-        pk.close()
-    log(f"cpu baseline: {rate:.1f} GiB/s on {nthr} threads, {rate1:.2f} GiB/s on 1 thread")
-    out = {"value": round(rate, 2), "unit": "GiB/s", "cores": nthr, "kind": kind_s,
-           "sample": sdesc + f" x{reps} ({secs:.1f} s); CalculateChecksum built -O3 -march=x86-64-v3; "
-                             f"results == GPU results: {match}",
-           "one_thread_GiBs": round(rate1, 2)}
-    if R.RefLib.available("O0"):
-        # secondary: the reference as its makefile builds it (-O0 -g, makefile:2), 1 thread
-        ref0 = R.RefLib("O0")
-        m = min(n, 20000)
-        kw = dict(sargs)
-        if "count" in kw:
-            kw["count"] = m
-        else:
-            kw["offsets"], kw["lengths"] = kw["offsets"][:m], kw["lengths"][:m]
-        _, s0 = ref0.timed_batch(sample, threads=1, **kw)
-        b0 = m * L if L else int(kw["lengths"].astype(np.int64).sum())
-        out["reference_O0_1thread_GiBs"] = round(b0 / s0 / GIB, 3)
+            c.batch(host_arena, threads=nthr, **sargs)
+            dt.append(time.perf_counter() - t0)
+        out.update({"value": round(sbytes / statistics.median(dt) / GIB, 2), "kind": "port",
+                    "sample": sdesc + f"; oracle/ref16.c restatement, median of 5 passes; results == GPU "
+                              f"results: {bool(np.array_equal(got, gpu_res[:count]))}"})
+    log(f"cpu baseline: {out['value']} GiB/s on {nthr} threads ({out.get('one_thread_GiBs')} on 1)")
     try:
         out["cpu_model"] = open("/proc/cpuinfo").read().split("model name")[1].split("\n")[0].strip(": \t")
     except Exception:

@@ -116,7 +116,11 @@ for s in ${STEPS:-tests smoke bench prof}; do
     prof_segment) step prof_segment 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_segment -o run --output-format csv -- python3 bench.py --config segment --steps 10 --warmup 2 --no-cpu-baseline --no-e2e ;;
     segtests2) step segtests2 600 python -u -m pytest tests/test_gpu_segment.py tests/test_gpu_sstream.py -x -q --timeout 300 --timeout-method thread ;;
     prof_c4) step prof_c4 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c4 -o run --output-format csv -- python3 bench.py --config c4 --steps 10 --warmup 2 --no-cpu-baseline --no-e2e ;;
-    prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-e2e ;;
+    prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-e2e --no-extras ;;
+    prof_all)  # the driver's default bench command (C2 + the c3 / c4 / c5_strong keys) under the kernel trace
+      step prof_all 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_all -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-e2e &&
+      python3 scripts/bench_trace_summary.py gpurun_out/prof_all/run_kernel_trace.csv --last 20 > gpurun_out/prof_all_summary.txt ;;
+    tests_new) step tests_new 900 python -u -m pytest tests/test_gpu_c5.py tests/test_gpu_multi_ctx.py tests/test_drop_in.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
     bench_receive) step bench_receive 600 python bench.py --config receive ;;
     bench_fill) step bench_fill 600 python bench.py --config fill ;;
     bench_slots) step bench_slots 600 python bench.py --config slots ;;
@@ -125,7 +129,7 @@ for s in ${STEPS:-tests smoke bench prof}; do
     prof_receive) step prof_receive 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_receive -o run --output-format csv -- python3 bench.py --config receive --steps 10 --warmup 2 --no-cpu-baseline --no-e2e ;;
     pmc_c2|pmc_c3|pmc_c4|pmc_c5|pmc_slots|pmc_segment|pmc_receive|pmc_fill)  # separate FETCH_SIZE / WRITE_SIZE passes (TCC slots), kernel trace only
       c=${s#pmc_}
-      step ${s}_fetch 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d gpurun_out/pmc_${c}_fetch -o run --output-format csv -- python3 bench.py --config $c --steps 3 --warmup 1 --settle-ms 0 --no-cpu-baseline --no-e2e
-      step ${s}_write 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d gpurun_out/pmc_${c}_write -o run --output-format csv -- python3 bench.py --config $c --steps 3 --warmup 1 --settle-ms 0 --no-cpu-baseline --no-e2e ;;
+      step ${s}_fetch 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d gpurun_out/pmc_${c}_fetch -o run --output-format csv -- python3 bench.py --config $c --steps 3 --warmup 1 --settle-ms 0 --no-cpu-baseline --no-e2e --no-extras
+      step ${s}_write 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d gpurun_out/pmc_${c}_write -o run --output-format csv -- python3 bench.py --config $c --steps 3 --warmup 1 --settle-ms 0 --no-cpu-baseline --no-e2e --no-extras ;;
   esac
 done

@@ -121,17 +121,33 @@ def test_receive_cpp_gpu(built_lib, n, slot):
     assert lines[-1].endswith("mismatches=0"), lines
 
 
-def test_loopback_c1(built_lib):
-    """Config C1: segments over UDP loopback, filled and verified through the drop-in."""
+def _loopback_c1(n):
     import json
     exe = os.path.join(LIBDIR, "bin", "loopback_c1")
     if not os.path.exists(exe):
         subprocess.run(["make", "-s", "-C", LIBDIR], check=True)
-    r = subprocess.run([exe, "3000", "1460"], capture_output=True, text=True, timeout=120)
+    r = subprocess.run([exe, str(n), "1460"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     d = json.loads(r.stdout)
-    assert d["received"] == d["verified"] == 3000
+    assert d["received"] == d["verified"] == n
     assert d["image_bytes"] == 1492
+    return d
+
+
+def test_loopback_c1(built_lib):
+    """Config C1: segments over UDP loopback, filled and verified through the drop-in
+    (socket-manager.cc:9-10 send insert, network-service.cc:49-56 receive buffer,
+    socket-manager.h:182 verify)."""
+    _loopback_c1(3000)
+
+
+@pytest.mark.gpu
+def test_loopback_c1_gpu_box(built_lib):
+    """C1 again inside the `-m gpu` run, so the driver's GPU-box record holds it:
+    the same prebuilt binary (host CPU only: one segment never goes to the GPU)
+    with verified == received over 20000 segments."""
+    d = _loopback_c1(20000)
+    assert d["us_per_segment"] > 0
 
 
 def _recv_burst(args, gpu):

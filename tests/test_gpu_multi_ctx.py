@@ -97,3 +97,62 @@ def test_multi_errors_propagate(ctxs):
     ln = np.full(8, 20, np.uint32)
     with pytest.raises(tcpck.TcpckError):  # FILL of images < 30 B
         tcpck.host_batch_var_multi(ctxs[:2], tcpck.OP_FILL, a, off, ln, 8, out)
+
+
+# ---- distinct devices (skipped on a one-GPU box; runs wherever >= 2 GPUs exist) ----
+
+def _device_count():
+    return torch.cuda.device_count() if torch.cuda.is_available() else 0
+
+
+@pytest.mark.skipif(_device_count() < 2, reason="needs >= 2 GPUs (contexts on distinct devices)")
+@pytest.mark.parametrize("length", [1492, 65536])
+def test_multi_fixed_distinct_devices(built_lib, oracle_c, length):
+    """tcpck_host_batch_fixed_multi with one context per GPU (one
+    contiguous shard per device, no exchange): CHECKSUM against the oracle, then
+    FILL -> VERIFY, and every call leaves the calling thread's current device as
+    it found it (the ABI's DeviceGuard)."""
+    import tcpck
+    ndev = _device_count()
+    cs = [tcpck.Context(d) for d in range(ndev)]
+    try:
+        for c in cs:
+            c.set_chunk_bytes(8 << 20)
+        count = 4096 if length == 1492 else 96
+        rng = np.random.default_rng(length + ndev)
+        a = rng.integers(0, 256, count * length, dtype=np.uint8)
+        out = np.zeros(count, np.uint16)
+        torch.cuda.set_device(0)
+        tcpck.host_batch_fixed_multi(cs, tcpck.OP_CHECKSUM, a, length, length, count, out)
+        assert torch.cuda.current_device() == 0
+        np.testing.assert_array_equal(out, oracle_c.batch(a, stride=length, length=length, count=count))
+        b = a.copy()
+        tcpck.host_batch_fixed_multi(cs, tcpck.OP_FILL, b, length, length, count, out)
+        exp_a, want = fill_expect(a, np.arange(count) * length, np.full(count, length))
+        np.testing.assert_array_equal(out, want)
+        np.testing.assert_array_equal(b, exp_a)
+        ok = np.zeros(count, np.uint8)
+        tcpck.host_batch_fixed_multi(cs, tcpck.OP_VERIFY, b, length, length, count, ok)
+        assert ok.all()
+    finally:
+        for c in cs:
+            c.close()
+
+
+@pytest.mark.skipif(_device_count() < 2, reason="needs >= 2 GPUs (contexts on distinct devices)")
+def test_device_batches_on_distinct_devices(built_lib, oracle_c):
+    """Device-resident batches: one context and one C2-layout shard per GPU,
+    each on its own device's current stream, results equal to the oracle."""
+    import tcpck
+    ndev = _device_count()
+    L, per = 1492, 20000
+    rng = np.random.default_rng(ndev)
+    a = rng.integers(0, 256, ndev * per * L, dtype=np.uint8)
+    exp = oracle_c.batch(a, stride=L, length=L, count=ndev * per)
+    for d in range(ndev):
+        with tcpck.Context(d) as c, torch.cuda.device(d):
+            arena = torch.from_numpy(a[d * per * L:(d + 1) * per * L]).to(f"cuda:{d}")
+            out = torch.empty(per, dtype=torch.int16, device=f"cuda:{d}")
+            c.batch_fixed(tcpck.OP_CHECKSUM, arena, L, L, per, out, stream=torch.cuda.current_stream(d))
+            torch.cuda.synchronize(d)
+            np.testing.assert_array_equal(out.cpu().numpy().view(np.uint16), exp[d * per:(d + 1) * per])
