@@ -488,12 +488,12 @@ def cpu_baseline(host_arena, gpu_res, kind, count, L, budget_s, var_layout):
 
         got, _ = pk.run(nthr)
         match = bool(np.array_equal(got, gpu_res[:count]))
-        med, rates, reps = passes(pk, nthr, 5, budget_s / 5)
+        med, rates, reps = passes(pk, nthr, 7, budget_s / 7)
         one, _, _ = passes(pk, 1, 1, 0.5)
         pk.close()
         out.update({"value": round(med, 2), "kind": kind_s, "one_thread_GiBs": round(one, 2),
                     "passes_GiBs": [round(r, 1) for r in rates],
-                    "sample": sdesc + f"; median of 5 passes of {reps} sweeps on {nthr} threads; CalculateChecksum "
+                    "sample": sdesc + f"; median of 7 passes of {reps} sweeps on {nthr} threads; CalculateChecksum "
                               f"(tcp-header.h:252-263) built -O3 -march=x86-64-v3; results == GPU results: {match}"})
         if R.RefLib.available("O0"):
             # secondary: the reference as its makefile builds it (-O0 -g, makefile:2), same threads
