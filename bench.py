@@ -28,7 +28,7 @@ ONE JSON line with the driver's fields plus:
                 rank's kernel time, per_gpu_frac = each GPU's roofline fraction
   cpu_baseline  the reference's own CalculateChecksum (oracle/_ref, built from
                 /root/reference/include/tcp-header.h) on the host cores over the
-                whole C2 arena (DRAM-sized: 6x the host L3), median of 5 passes
+                whole C2 arena (DRAM-sized: 6x the host L3), median of 7 passes
                 (rank 0, N=1 only); falls back to the in-repo C restatement
                 ("port") where oracle/_ref is absent
   e2e           host-memory rate incl. pinned hipMemcpyAsync H2D + D2H (not `value`)
@@ -100,7 +100,7 @@ def parse():
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--config", default="c2", choices=sorted(CONFIGS) + ["c1"] + sorted(EXTRA))
-    p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline time budget (5 passes)")
+    p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline time budget (7 passes)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-e2e", action="store_true")
     p.add_argument("--no-extras", action="store_true", help="default run: skip the c3/c4/c5_strong keys")

@@ -219,6 +219,7 @@ constexpr int kSegXcdOrder = 1 << 24;    // seg: XCD-chunked order
 // 480 B +0.6 %, the C3 mix -3.7 %: bytes per image up to 448)
 constexpr uint64_t kFillKeepMaxLen = 448;
 constexpr int kVvKeep = 32;              // vvstream: kFill reads with the default policy
+constexpr int kSstreamHdrStream = 32;    // sstream RECEIVE: headers from the stream's registers
 
 // Packed fixed images above 4 KiB: seg's W-wave shapes stream W KiB of an
 // image per step (shape_for_len: W = 2, 4, 8, 16 up to 8, 16, 32, 64 KiB), so
@@ -331,13 +332,13 @@ hipError_t run_fixed_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint
       param = kRstreamPolicy;
     }
   }
-  // RECEIVE into a header array: the header pass follows the VERIFY pass.
-  // sstream can instead write each run's headers after the run's verdicts
-  // (one launch), but those stores inside the other waves' read streams cost
-  // more than the separate pass (1492 B in 2048-B slots 302 vs 258 us, the
-  // receive ring 181 vs 156 us; scripts/receive_fused_probe.py,
-  // profiles/r02/receive_fused_probe.log): tuning only for fixed slots
-  const bool fuse_hdr = op == TCPCK_OP_RECEIVE && hdr && !auto_pick && !(param & TCPCK_PARAM_RECEIVE_TWO_PASS);
+  // RECEIVE into a header array: where the VERIFY kernel is sstream, it emits
+  // each image's host-order header from the stream's registers (the header
+  // bytes read once, DESIGN.md "Receive path"); elsewhere the header pass
+  // follows the VERIFY pass
+  if (auto_pick && op == TCPCK_OP_RECEIVE && hdr && kernel == TCPCK_KERNEL_SSTREAM) param |= kSstreamHdrStream;
+  const bool fuse_hdr = op == TCPCK_OP_RECEIVE && hdr && (!auto_pick || kernel == TCPCK_KERNEL_SSTREAM) &&
+                        !(param & TCPCK_PARAM_RECEIVE_TWO_PASS);
   if (op == TCPCK_OP_RECEIVE) op = TCPCK_OP_VERIFY;  // the header pass follows (run_fixed)
   // FILL on rstream with a results buffer: the stream writes only the results,
   // then a second pass rewrites each field's 64-B block whole -- never slower
@@ -521,9 +522,9 @@ hipError_t run_var_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const 
       // (41-58 % either way: the scattered field writes bound it)
       kernel = TCPCK_KERNEL_SSTREAM;
       param = 0;
-      if (op == TCPCK_OP_RECEIVE && hdr && typical <= 256) {
+      if (op == TCPCK_OP_RECEIVE && hdr) {
         fuse_small = true;
-        param = 16;
+        param = kSstreamHdrStream;
       }
     } else if (!packed || typical > kRunMaxLen ||
                (op == TCPCK_OP_FILL && layout->min_len != 0 && layout->min_len < 30)) {
@@ -534,10 +535,8 @@ hipError_t run_var_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const 
       param = kVvPolicy | (op == TCPCK_OP_FILL && typical <= kFillKeepMaxLen ? kVvKeep : 0);
     }
   }
-  // RECEIVE into a header array (as run_fixed_impl): the header pass, except
-  // for rings of small images (typical <= 256 B), where sstream writing each
-  // run's headers itself with a default-policy stream wins (4M 32-254-B
-  // datagrams in 256-B slots: 236 vs 259 us; receive_fused_probe.log)
+  // RECEIVE into a header array (as run_fixed_impl): sstream emits the
+  // headers from its stream; other kernels are followed by the header pass
   bool fuse_hdr = op == TCPCK_OP_RECEIVE && hdr && !(param & TCPCK_PARAM_RECEIVE_TWO_PASS) &&
                   (!auto_pick || fuse_small);
   if (op == TCPCK_OP_RECEIVE) op = TCPCK_OP_VERIFY;  // the header pass follows (run_var)

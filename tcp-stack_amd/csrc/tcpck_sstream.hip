@@ -42,13 +42,17 @@
 //     stores the result at the image's arena address (d_i + 16 C_i + h_i +
 //     28); images < 30 B send the run to the per-image pass, which skips
 //     them (the C ABI rejects them).
-//   * HDR (kVerify, tcpck_batch_receive with a header array): after the
-//     verdicts the wave converts its run's headers to host order
-//     (TcpHeaderN2H, include/socket-manager.h:184; tcp-header.h:208-221) into
-//     the dense array, one image per lane: the run's records leave as one
-//     burst of whole lines instead of a second launch over the batch.  The
-//     header lines were read by the stream moments before (KEEPL: with the
-//     default cache policy, so they are still in L2).
+//   * HDR (kVerify, tcpck_batch_receive with a header array): the run's
+//     headers in host order (TcpHeaderN2H, include/socket-manager.h:184;
+//     tcp-header.h:208-221) into the dense array.  HDR >= 2 (AUTO): from the
+//     stream's own registers -- an image that starts on a 16-B boundary has
+//     its 32 header bytes in compacted chunks C_i and C_i + 1, so the two lanes
+//     holding them permute their dwords and store 16 B each at hdr + 32 k
+//     (+ 16) as the step is consumed: the header bytes are read once, by the
+//     stream (3: nt stores).  A run with a misaligned or < 32-B image (or a
+//     misaligned array) and HDR 1 instead convert after the verdicts, one
+//     image per lane, re-reading the header lines (KEEPL: the stream read
+//     with the default cache policy so they are still in L2).
 #include <algorithm>
 #include <type_traits>
 
@@ -104,7 +108,7 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t x) {
 
 // MODE kRfc1071: exact u32 prefix tables (as tcpck_vvstream.hip), the
 // differences folded
-template <int U, int OP, bool FIXED, int MODE = kRef, bool HDR = false, bool KEEPL = false>
+template <int U, int OP, bool FIXED, int MODE = kRef, int HDR = 0, bool KEEPL = false>
 __global__ void __launch_bounds__(kBlock) sstream_kernel(SSArgs a) {
   __shared__ uint32_t s_end[kWavesPerBlock][FIXED ? 1 : kEnds];         // virtual ends, compacted bytes
   __shared__ uint32_t s_c[kWavesPerBlock][FIXED ? 1 : kMaxRun + 64];    // first compacted chunk, ~0 past the run
@@ -142,6 +146,7 @@ __global__ void __launch_bounds__(kBlock) sstream_kernel(SSArgs a) {
   uint32_t T = 0;    // compacted chunks of the run
   uint32_t R = 0;    // buffer range from B (bytes, whole chunks)
   bool al4;          // every virtual end 4-B aligned: u32 prefix table
+  bool hs = false;   // HDR >= 2: every header in its image's first two chunks (the stream emits them)
   const uint32_t S = a.stride;
   const uint32_t L = FIXED ? a.len : 0u;
   const uint32_t n16 = FIXED ? a.nchunk << 4 : 0u;  // fixed: compacted bytes per image
@@ -152,6 +157,7 @@ __global__ void __launch_bounds__(kBlock) sstream_kernel(SSArgs a) {
     R = ((nimg - 1) * S + h + L + 15) & ~15u;
     al4 = ((h | L) & 3u) == 0;
     if (OP == kFill) bad = L < 30;
+    hs = h == 0 && L >= 32;
   } else {
     uint64_t o[kPer];
     uint32_t l[kPer];
@@ -163,13 +169,18 @@ __global__ void __launch_bounds__(kBlock) sstream_kernel(SSArgs a) {
     }
     B = dev::align16_rel(arena, dev::read_lane64(o[0], 0));
     uint32_t n[kPer], hh[kPer], r16[kPer], hi = 0;
-    bool ok = true, odd = false, shrt = false;
+    bool ok = true, odd = false, shrt = false, hmis = false;
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
       const uint32_t j = kPer * lane + i;
       const uint64_t r = o[i] - B;  // from the run base; an image before it wraps high
       const bool in = j < nimg;
-      ok = ok && (!in || (r < (uint64_t{1} << 30) && l[i] <= (1u << 23)));
+      // RFC 1071: the u32 prefix differences are exact only for images below
+      // 128 KiB (2^16 words of <= 0xFFFF); a longer image (an understated
+      // max_len hint, or the kernel named explicitly) sends the run to the
+      // exact per-image pass
+      ok = ok && (!in || (r < (uint64_t{1} << 30) && l[i] <= (1u << 23) &&
+                          (MODE == kRef || l[i] < (1u << 17))));
       const uint32_t rr = static_cast<uint32_t>(r);
       hh[i] = in ? rr & 15u : 0u;
       r16[i] = rr & ~15u;
@@ -177,9 +188,11 @@ __global__ void __launch_bounds__(kBlock) sstream_kernel(SSArgs a) {
       hi = in ? max(hi, rr + l[i]) : hi;
       odd = odd || (in && ((hh[i] | l[i]) & 3u) != 0);
       shrt = shrt || (in && l[i] < 30);
+      hmis = hmis || (in && (hh[i] != 0 || l[i] < 32));  // HDR >= 2: header not in chunks C_i, C_i + 1
     }
     bad = __ballot(!ok) != 0;
     al4 = __ballot(odd) == 0;
+    hs = __ballot(hmis) == 0;
     if (OP == kFill) bad = bad || __ballot(shrt) != 0;
     uint32_t c[kPer];  // exclusive prefix of n inside the lane, then across the wave
     uint32_t lsum = 0;
@@ -210,6 +223,7 @@ __global__ void __launch_bounds__(kBlock) sstream_kernel(SSArgs a) {
     __builtin_amdgcn_wave_barrier();
   }
 
+  hs = HDR >= 2 && hs && !bad && (reinterpret_cast<uintptr_t>(a.hdr) & 15u) == 0;
   if (!bad) {
     const uint32_t span = T << 4;  // compacted bytes; every end <= span
     const uint32_t nsteps = (T + 63) >> 6;
@@ -226,12 +240,18 @@ __global__ void __launch_bounds__(kBlock) sstream_kernel(SSArgs a) {
     // chunk -> arena offset (from B) of the lane's chunk of step t; steps are
     // mapped in order, U ahead of their sums
     uint32_t il = 0;  // variable: the image holding the first chunk of the next step mapped
+    // HDR >= 2: the step's header chunks -- (run image << 1) | (0: bytes 0-15,
+    // 1: bytes 16-31) of the lane's chunk, ~0 for any other chunk
+    uint32_t hk_next = ~0u;
+    uint32_t hf_prev = 0;  // variable: the previous step's lane 63 held a first chunk
     auto map_step = [&](uint32_t t) -> uint32_t {
       const uint32_t q0 = t << 6;
       const uint32_t q = q0 + lane;
       if constexpr (FIXED) {
         const uint32_t i = a.magic ? (__umulhi(q, a.magic) >> a.shift) : (q >> a.shift);
-        return i * S + ((q - i * a.nchunk) << 4);
+        const uint32_t c = q - i * a.nchunk;
+        if constexpr (HDR >= 2) hk_next = (q < T && c < 2u) ? (i << 1) | c : ~0u;
+        return i * S + (c << 4);
       } else {
         const uint32_t cj = s_c[wv][il + lane];  // image il + lane starts at chunk cj
         const uint32_t p = cj - q0;              // il itself may start before q0: wraps high
@@ -245,6 +265,13 @@ __global__ void __launch_bounds__(kBlock) sstream_kernel(SSArgs a) {
         // flags at or below l, less il's own flag when il starts at q0
         const uint32_t idx = il + below + f - static_cast<uint32_t>(M & 1u);
         const uint32_t d = s_d[wv][idx];
+        if constexpr (HDR >= 2) {
+          // first chunk: the lane's own flag; second: the flag one lane down
+          // (lane 0: the previous step's lane 63) -- every image here has >= 2 chunks
+          const uint32_t second = lane ? static_cast<uint32_t>(M >> (lane - 1)) & 1u : hf_prev;
+          hk_next = f ? idx << 1 : (second ? (idx << 1) | 1u : ~0u);
+          hf_prev = static_cast<uint32_t>(M >> 63);
+        }
         // the image holding chunk q0 + 64: one that starts there, else lane 63's
         const uint64_t b64 = __ballot(p == 64u);
         const uint32_t i63 = dev::read_lane(idx, 63);
@@ -291,8 +318,12 @@ __global__ void __launch_bounds__(kBlock) sstream_kernel(SSArgs a) {
     };
 
     u32x4 ring[U];
+    uint32_t hring[U];  // HDR >= 2: header keys of the ring's chunks
 #pragma unroll
-    for (int u = 0; u < U; ++u) ring[u] = load_step(static_cast<uint32_t>(u));
+    for (int u = 0; u < U; ++u) {
+      ring[u] = load_step(static_cast<uint32_t>(u));
+      hring[u] = hk_next;
+    }
 
     uint32_t carry = 0, p_last = 0, jn = 0, fj = 0;
     uint32_t e_last = 0;  // end of virtual jn - 1 (the stream start for jn = 0)
@@ -304,6 +335,20 @@ __global__ void __launch_bounds__(kBlock) sstream_kernel(SSArgs a) {
           const uint32_t st = g + u;
           const uint32_t sb = st << 10;
           u32x4 w = ring[u];
+          if constexpr (HDR >= 2) {
+            if (hs && hring[u] != ~0u) {  // this lane holds header bytes 0-15 or 16-31 of an image
+              const uint32_t hk = hring[u];
+              // TcpHeaderN2H per dword (dev::n2h_selector): dwords 0/4, 1/5 byte
+              // reversed, 2/6 TcpLength/window swapped, 3 the ports, 7 urgent
+              const u32x4 o{dev::n2h_dword(w.x, 0x00010203u), dev::n2h_dword(w.y, 0x00010203u),
+                            dev::n2h_dword(w.z, 0x02030100u), dev::n2h_dword(w.w, (hk & 1u) ? 0x02030100u : 0x02030001u)};
+              u32x4 *dst = reinterpret_cast<u32x4 *>(a.hdr + 32 * (kb + (hk >> 1)) + 16 * (hk & 1u));
+              if constexpr (HDR == 3)
+                __builtin_nontemporal_store(o, dst);
+              else
+                *dst = o;
+            }
+          }
           if (sb + 1024 > span && sb + (lane << 4) >= span) w = u32x4{0u, 0u, 0u, 0u};  // past the run
           const uint32_t j = jn + lane;
           uint32_t e = ends_at(jn);
@@ -384,6 +429,7 @@ __global__ void __launch_bounds__(kBlock) sstream_kernel(SSArgs a) {
           __builtin_amdgcn_wave_barrier();  // the next step rewrites the table
           carry += dev::read_lane(incl, 63);
           ring[u] = load_step(st + U);
+          hring[u] = hk_next;
         }
       }
     };
@@ -417,7 +463,7 @@ __global__ void __launch_bounds__(kBlock) sstream_kernel(SSArgs a) {
       if (lane == 0) store(k, sum, start);
     }
   }
-  if constexpr (HDR) {
+  if (HDR == 1 || (HDR >= 2 && !hs)) {
     // the run's headers in host order, image kb + i by lane i (mod 64): 32-B
     // records, consecutive lanes consecutive records -- whole lines out
     for (uint32_t i = lane; i < nimg; i += 64) {
@@ -450,7 +496,7 @@ __global__ void __launch_bounds__(kBlock) sstream_kernel(SSArgs a) {
   }
 }
 
-template <int U, int OP, bool FIXED, int MODE = kRef, bool HDR = false, bool KEEPL = false>
+template <int U, int OP, bool FIXED, int MODE = kRef, int HDR = 0, bool KEEPL = false>
 hipError_t launch_one(SSArgs a, uint32_t oversub, uint64_t min_waves, uint32_t num_cus, hipStream_t stream) {
   static const uint32_t per_cu = dev::resident_blocks_per_cu(sstream_kernel<U, OP, FIXED, MODE, HDR, KEEPL>);
   const uint64_t resident = static_cast<uint64_t>(per_cu) * num_cus;
@@ -470,14 +516,18 @@ hipError_t launch_one(SSArgs a, uint32_t oversub, uint64_t min_waves, uint32_t n
 
 template <int U, bool FIXED>
 hipError_t dispatch(int op, const SSArgs &a, uint32_t m, uint64_t min_waves, uint32_t num_cus, hipStream_t s,
-                    bool keepl) {
+                    bool keepl, int hdr_mode) {
   if (a.hdr) {  // VERIFY + the run's headers into the array (tcpck_batch_receive)
     if (op != kVerify) return hipErrorInvalidValue;
-    if (a.mode != kRef)
-      return keepl ? launch_one<U, kVerify, FIXED, kRfc1071, true, true>(a, m, min_waves, num_cus, s)
-                   : launch_one<U, kVerify, FIXED, kRfc1071, true, false>(a, m, min_waves, num_cus, s);
-    return keepl ? launch_one<U, kVerify, FIXED, kRef, true, true>(a, m, min_waves, num_cus, s)
-                 : launch_one<U, kVerify, FIXED, kRef, true, false>(a, m, min_waves, num_cus, s);
+    if (a.mode != kRef) {
+      if (hdr_mode == 2) return launch_one<U, kVerify, FIXED, kRfc1071, 2>(a, m, min_waves, num_cus, s);
+      return keepl ? launch_one<U, kVerify, FIXED, kRfc1071, 1, true>(a, m, min_waves, num_cus, s)
+                   : launch_one<U, kVerify, FIXED, kRfc1071, 1, false>(a, m, min_waves, num_cus, s);
+    }
+    if (hdr_mode == 2) return launch_one<U, kVerify, FIXED, kRef, 2>(a, m, min_waves, num_cus, s);
+    if (hdr_mode == 3) return launch_one<U, kVerify, FIXED, kRef, 3>(a, m, min_waves, num_cus, s);
+    return keepl ? launch_one<U, kVerify, FIXED, kRef, 1, true>(a, m, min_waves, num_cus, s)
+                 : launch_one<U, kVerify, FIXED, kRef, 1, false>(a, m, min_waves, num_cus, s);
   }
   if (a.mode != kRef) {
     switch (op) {
@@ -553,11 +603,13 @@ hipError_t launch_sstream(int op, int variant, bool fixed, const RunArgs &r, uin
                                       fixed ? 8u << 10 : 16u << 10);
   const int u = variant & 3;  // 0: policy, 1: U4, 2: U8
   const bool u8 = u == 2;
-  const bool keepl = (variant & 16) != 0;  // HDR: the stream read with the default cache policy
-  if (fixed) return u8 ? dispatch<8, true>(op, a, m, min_waves, num_cus, stream, keepl)
-                       : dispatch<4, true>(op, a, m, min_waves, num_cus, stream, keepl);
-  return u8 ? dispatch<8, false>(op, a, m, min_waves, num_cus, stream, keepl)
-            : dispatch<4, false>(op, a, m, min_waves, num_cus, stream, keepl);
+  const bool keepl = (variant & 16) != 0;  // HDR 1: the stream read with the default cache policy
+  // HDR: + 32 the headers from the stream's registers (kSstreamHdrStream), + 64 with nt stores
+  const int hdr_mode = (variant & 32) ? ((variant & 64) ? 3 : 2) : 1;
+  if (fixed) return u8 ? dispatch<8, true>(op, a, m, min_waves, num_cus, stream, keepl, hdr_mode)
+                       : dispatch<4, true>(op, a, m, min_waves, num_cus, stream, keepl, hdr_mode);
+  return u8 ? dispatch<8, false>(op, a, m, min_waves, num_cus, stream, keepl, hdr_mode)
+            : dispatch<4, false>(op, a, m, min_waves, num_cus, stream, keepl, hdr_mode);
 }
 
 }  // namespace tcpck

@@ -216,6 +216,12 @@ __global__ void __launch_bounds__(kBlock) vvstream_kernel(VVArgs a) {
       uint32_t d[4];
       load_round(r, d);
       al4 = al4 && __ballot(((d[0] | d[1] | d[2] | d[3]) & 3u) != 0) == 0;  // lengths past nimg are 0
+      if constexpr (MODE == kRfc1071) {
+        // the u32 prefix differences are exact only below 128 KiB: a longer
+        // image (an understated max_len hint, or the kernel named explicitly)
+        // sends the run to the exact per-image pass, which rewrites every result
+        bad = bad || __ballot((d[0] | d[1] | d[2] | d[3]) >= (1u << 17)) != 0;
+      }
       const uint32_t e1 = d[0], e2 = e1 + d[1], e3 = e2 + d[2], e4 = e3 + d[3];
       const uint32_t incl = dev::wave_inclusive_scan(e4);
       const uint32_t ex = pos + incl - e4;
@@ -263,12 +269,12 @@ __global__ void __launch_bounds__(kBlock) vvstream_kernel(VVArgs a) {
           for (uint32_t j = lane; j < nimg; j += 64) {
             const uint32_t l = lens[j];
             sum += l;
-            sh |= l < 30;
+            sh |= l < 30 || (MODE == kRfc1071 && l >= (1u << 17));  // (RFC 1071: as fill_round)
           }
           short_fill = short_fill || __ballot(sh) != 0;
-          bad = short_fill || lead + dev::group_sum<64>(sum) != span;
+          bad = bad || short_fill || lead + dev::group_sum<64>(sum) != span;
         } else {
-          bad = short_fill || pos != span;
+          bad = bad || short_fill || pos != span;
         }
       }
     } else {

@@ -454,13 +454,15 @@ def test_batch_receive_sstream_variants(ctx, variant):
 
 # ---- RECEIVE with the headers written by sstream itself (one launch) -------------------
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 4, 8, 16, 17, 18, 1 << 30])
-@pytest.mark.parametrize("layout", ["ring", "ring-mis", "unordered", "fixed-slots", "fixed-mis"])
+@pytest.mark.parametrize("variant", [0, 1, 2, 4, 8, 16, 17, 18, 32, 33, 34, 36, 40, 96, 98, 1 << 30])
+@pytest.mark.parametrize("layout", ["ring", "ring-mis", "ring-short", "unordered", "fixed-slots", "fixed-mis"])
 @pytest.mark.parametrize("hdr_mis", [0, 4])
 def test_batch_receive_fused_hdr(ctx, variant, layout, hdr_mis):
     """tcpck_batch_receive_ex on KERNEL_SSTREAM: each wave writes its run's
     host-order headers after its verdicts (variant + 16: the stream read with
-    the default cache policy; 1 << 30: the separate header pass instead).
+    the default cache policy; + 32: each header from the stream's registers,
+    + 64 with nt stores -- runs holding a misaligned or < 32-B image fall back
+    to the per-run conversion; 1 << 30: the separate header pass instead).
     Rings (16-B and 2-B aligned starts), unordered offsets (the per-image
     fallback), fixed slots; header arrays 16-B and only 4-B aligned; both
     modes.  Verdicts, every header byte, the arena unchanged."""
@@ -476,6 +478,8 @@ def test_batch_receive_fused_hdr(ctx, variant, layout, hdr_mis):
         off = off[rng.permutation(n)].copy()
     if layout.startswith("fixed"):
         ln[:] = 1492
+    if layout == "ring-short":  # some runs hold images below 32 B (headers past the image end)
+        ln[rng.integers(0, n, 40)] = (rng.integers(1, 16, 40) * 2).astype(np.uint32)
     a = rng.integers(0, 256, n * slot + 64, dtype=np.uint8)
     v = a[mis:]
     for o, l in zip(off[::3], ln[::3]):
