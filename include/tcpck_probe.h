@@ -1,0 +1,31 @@
+/*
+ * tcpck_probe.h -- measurement-only entry points, exported by
+ * libtcpck_probe.so alone (tcp-stack_amd/Makefile builds it from the same
+ * sources with -DTCPCK_PROBE).  The product library libtcpck.so does not
+ * carry them: scripts/ and the variant tests use them to time kernels.
+ */
+#ifndef TCPCK_PROBE_H_
+#define TCPCK_PROBE_H_
+
+#include "tcpck_tuning.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Device buffer of 4 x u64 per wave receiving {start, end} s_memrealtime
+ * (100 MHz) stamps, HW_ID and XCC_ID from the rstream variants built with
+ * stamps (3, 7; NULL = off). */
+int tcpck_ctx_set_debug(tcpck_ctx *ctx, void *d_buf);
+
+/* Timing-only streaming micro-kernel over d_buf (results are not checksums):
+ * variant = chunks per lane per step x steps in flight x scan, see
+ * tcp-stack_amd/csrc/tcpck_diag.hip.  d_out: u32 per wave. */
+int tcpck_diag_stream(tcpck_ctx *ctx, int variant, const void *d_buf, uint64_t bytes, void *d_out,
+                      tcpck_stream stream);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+
+#endif /* TCPCK_PROBE_H_ */

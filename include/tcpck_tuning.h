@@ -1,8 +1,22 @@
 /*
- * tcpck_tuning.h -- kernel-selection entry points of libtcpck.so for
- * benchmarking and tuning.  Not needed by a drop-in caller: tcpck_batch_fixed /
- * tcpck_batch_var (tcpck.h) pick the kernel themselves.  Results never depend
- * on the kernel chosen; an inapplicable choice returns an error.
+ * tcpck_tuning.h -- kernel-selection entry points for benchmarking and tuning.
+ * Not needed by a drop-in caller: tcpck_batch_fixed / tcpck_batch_var
+ * (tcpck.h) pick the kernel themselves.  Results never depend on the kernel
+ * chosen; an inapplicable choice returns an error.
+ *
+ * Two libraries export these functions:
+ *   libtcpck.so        the product.  It holds only the kernels the AUTO
+ *                      policy picks, so here it accepts exactly AUTO's own
+ *                      choices: SEG shapes 0 (by length), 1, 2, 7, 8, 9, 11;
+ *                      RSTREAM variant 20 (FILL also 25); VVSTREAM variant 4
+ *                      with any of the flags + 8 / + 16 / + 32; GSTREAM FILL
+ *                      with 0, 0x80 or 0x401 (+ 4); SSTREAM 0 (RECEIVE also
+ *                      + 32); tcpck_batch_segment_ex variant 0 (+ 8); with any
+ *                      oversubscription / cap bits and the TCPCK_PARAM_* bits
+ *                      below.  Any other value returns an error there
+ *                      (hipErrorInvalidValue).
+ *   libtcpck_probe.so  the same sources built with -DTCPCK_PROBE: every
+ *                      variant documented below, plus tcpck_probe.h.
  */
 #ifndef TCPCK_TUNING_H_
 #define TCPCK_TUNING_H_
@@ -38,7 +52,9 @@ extern "C" {
                                   consecutive runs; 20/21: 18/14 with the run's
                                   first step read with the default cache policy,
                                   20 = the policy's; 22: 18 with every step read
-                                  with the default policy)
+                                  with the default policy; 23/24: 20 with 8/2
+                                  steps in flight; 25: 20's FILL with the fields
+                                  stored by the 64-B block pass, AUTO's FILL)
                                   | (blocks per CU cap << 8)
                                   | (grid oversubscription << 16: 0 = by batch
                                   size, 1 = none, M = M x the resident grid)    */
@@ -76,46 +92,41 @@ extern "C" {
                                   U8, AUTO's FILL choice up to 128 B)
                                   | (grid oversubscription << 16: 0 = by batch
                                   size, 1 = none, M = M x the resident grid)    */
-#define TCPCK_KERNEL_SSTREAM 10 /* MODE_REF, all ops: slotted layouts -- fixed
-                                   slots (stride % 16 == 0) or any offset list --
-                                   read as one compacted stream per wave (lines
-                                   wholly in a gap are never read; runs of <= 256
-                                   images for offset lists); param = variant (0:
+#define TCPCK_KERNEL_SSTREAM 10 /* all ops: slotted layouts -- fixed slots
+                                   (stride % 16 == 0) or any offset list -- read
+                                   as one compacted stream per wave (lines
+                                   wholly in a gap are never read; runs of <= 128
+                                   images for offset lists); REF and RFC 1071
+                                   (images < 128 KiB); param = variant (0:
                                    policy = 4 steps in flight, scattered block
                                    order; 1: 4 steps in flight, 2: 8; + 4:
                                    default block order, + 8: scattered, else
-                                   XCD-chunked; + 16, RECEIVE into a header
-                                   array only: the stream read with the default
-                                   cache policy)
+                                   XCD-chunked; RECEIVE into a header array
+                                   only: + 32 each header from the stream's
+                                   registers (AUTO), + 64 with nt stores; else
+                                   converted after the run's verdicts, + 16
+                                   with the stream read with the default cache
+                                   policy)
                                    | (grid oversubscription << 16: 0 = by batch
                                    size, M = M x the resident grid)             */
 /* FILL in TCPCK_MODE_REF with a results buffer, any kernel (param bits, OR'ed
  * with the kernel's own param):
  *   TCPCK_PARAM_FILL_UPDATE    the kernel's CHECKSUM pass, then a field pass that
  *                              derives each zero-field checksum from the old field
- *                              (c = ~(~C - f) mod 2^16) and stores it (AUTO's
- *                              choice; fixed layouts need stride >= 64)
+ *                              (c = ~(~C - f) mod 2^16) and stores it (AUTO takes
+ *                              it for fixed layouts with stride > len and images
+ *                              above 4 KiB; fixed layouts need stride >= 64)
  *   TCPCK_PARAM_FILL_INSTREAM  with TCPCK_KERNEL_AUTO: the field zeroed in the
  *                              stream instead (the kernel AUTO picks for FILL) */
 #define TCPCK_PARAM_FILL_UPDATE (1 << 28)
 #define TCPCK_PARAM_FILL_INSTREAM (1 << 29)
 /* RECEIVE into a header array (tcpck_batch_receive_ex): where the VERIFY kernel
- * is sstream it writes each run's headers itself after the run's verdicts;
- * this bit keeps the separate header pass instead (tuning). */
+ * is sstream it writes the headers itself (see TCPCK_KERNEL_SSTREAM); this bit
+ * keeps the separate header pass instead. */
 #define TCPCK_PARAM_RECEIVE_TWO_PASS (1 << 30)
 int tcpck_batch_fixed_ex(tcpck_ctx *ctx, int op, int mode, void *d_arena,
                          uint64_t stride, uint32_t len, uint64_t count, void *d_out,
                          int kernel, int param, tcpck_stream stream);
-/* Device buffer of 2 x u64 per wave receiving {start, end} s_memrealtime
- * (100 MHz) stamps from kernels built with stamps (NULL = off). */
-int tcpck_ctx_set_debug(tcpck_ctx *ctx, void *d_buf);
-
-/* Timing-only streaming micro-kernel over d_buf (results are not checksums):
- * variant = chunks per lane per step x steps in flight x scan, see
- * tcp-stack_amd/csrc/tcpck_diag.hip.  d_out: u32 per wave. */
-int tcpck_diag_stream(tcpck_ctx *ctx, int variant, const void *d_buf, uint64_t bytes, void *d_out,
-                      tcpck_stream stream);
-
 /* tcpck_batch_segment (tcpck.h) with param = variant (0: policy = 4 steps in
  * flight, nt stores; 1: 8 in flight; 2: default-policy stores; 3: sc1 stores;
  * + 8: default block order, else XCD-chunked) | (grid oversubscription << 16). */

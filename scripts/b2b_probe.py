@@ -20,7 +20,7 @@ def main():
     ap.add_argument("--what", default="c3")
     ap.add_argument("--params", default="")
     args = ap.parse_args()
-    ctx = tcpck.Context(0)
+    ctx = tcpck.Context(0, probe=True)
     s = torch.cuda.current_stream()
     if args.what == "c3":
         from synth_np import mixed_layout

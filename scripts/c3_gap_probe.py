@@ -36,7 +36,7 @@ def b2b(fn, s, reps=20, rounds=5):
 
 def main():
     from synth_np import mixed_layout
-    ctx = tcpck.Context(0)
+    ctx = tcpck.Context(0, probe=True)
     s = torch.cuda.current_stream()
     n = 4 << 20
     for name, L in (("736 B x 4M", 736), ("C3 mix", None)):

@@ -34,7 +34,7 @@ def b2b(fn, s, reps=10, rounds=5):
 
 
 def main():
-    ctx = tcpck.Context(0)
+    ctx = tcpck.Context(0, probe=True)
     s = torch.cuda.current_stream()
     L, n = 65536, 256 << 10
     a = torch.empty(n * L, dtype=torch.uint8, device="cuda")

@@ -36,7 +36,7 @@ def b2b(fn, s, reps=10, rounds=5):
 
 
 def main():
-    ctx = tcpck.Context(0)
+    ctx = tcpck.Context(0, probe=True)
     s = torch.cuda.current_stream()
     half = 1536 * (1 << 20)
     buf = torch.randint(0, 255, (2 * half,), dtype=torch.uint8, device="cuda")

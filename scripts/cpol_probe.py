@@ -14,7 +14,7 @@ import tcpck  # noqa: E402
 
 
 def main():
-    ctx = tcpck.Context(0)
+    ctx = tcpck.Context(0, probe=True)
     s = torch.cuda.current_stream()
     buf = torch.empty(17 << 30, dtype=torch.uint8, device="cuda")
     tcpck.synth_fixed(buf, 65536, 65536, (17 << 30) // 65536, seed=1)

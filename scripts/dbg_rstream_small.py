@@ -3,7 +3,7 @@ sys.path[:0]=['/root/repo','/root/repo/tcp-stack_amd','/root/repo/tests']
 import tcpck
 from oracle.ref16 import Ref16C
 o=Ref16C()
-ctx=tcpck.Context(0)
+ctx=tcpck.Context(0, probe=True)
 count, L, variant = 1, 16, 0
 rng = np.random.default_rng(L * 7 + count + variant)
 a = rng.integers(0, 256, count * L + 32, dtype=np.uint8)

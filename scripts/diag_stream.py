@@ -20,7 +20,7 @@ NAMES = {0: "1x16B U4 scan", 1: "1x16B U4 noscan", 2: "2x16B U2 scan", 3: "2x16B
 
 
 def main():
-    ctx = tcpck.Context(0)
+    ctx = tcpck.Context(0, probe=True)
     stream = torch.cuda.current_stream()
     buf = torch.empty(17 << 30, dtype=torch.uint8, device="cuda")
     tcpck.synth_fixed(buf, 65536, 65536, (17 << 30) // 65536, seed=1)

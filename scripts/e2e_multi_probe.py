@@ -24,7 +24,7 @@ def main():
     h.copy_(d.cpu())
     out = torch.empty(n, dtype=torch.int16).pin_memory()
     ref = torch.empty(n, dtype=torch.int16, device="cuda")
-    ctxs = [tcpck.Context(0) for _ in range(4)]
+    ctxs = [tcpck.Context(0, probe=True) for _ in range(4)]
     ctxs[0].batch_fixed(tcpck.OP_CHECKSUM, d, L, L, n, ref)
     torch.cuda.synchronize()
     ref = ref.cpu()

@@ -14,7 +14,7 @@ from slot_probe import PEAK, timed  # noqa: E402
 
 
 def main():
-    ctx = tcpck.Context(0)
+    ctx = tcpck.Context(0, probe=True)
     s = torch.cuda.current_stream()
     for L in (512, 1024, 1492, 2000, 4096, 9000):
         n = (1566572544 // L)

@@ -38,7 +38,7 @@ def b2b(fn, s, reps=20, rounds=5):
 
 
 def main():
-    ctx = tcpck.Context(0)
+    ctx = tcpck.Context(0, probe=True)
     s = torch.cuda.current_stream()
     sizes = [int(x) for x in sys.argv[1].split(",")] if len(sys.argv) > 1 else [512, 1024, 1492, 2048, 4096]
     for L in sizes:

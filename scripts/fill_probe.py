@@ -36,7 +36,7 @@ def bench(label, fn, nbytes, s, check):
 
 
 def main():
-    ctx = tcpck.Context(0)
+    ctx = tcpck.Context(0, probe=True)
     s = torch.cuda.current_stream()
     K = tcpck
     off, ln, total = mixed_layout(4 << 20, seed=42)

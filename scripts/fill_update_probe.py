@@ -118,7 +118,7 @@ def main():
                                        "9000/9000,65536/65536,1492/2048,96/256,9000/16384,9000/9216")
     p.add_argument("--var", default="c3,slots")
     args = p.parse_args()
-    ctx = tcpck.Context(0)
+    ctx = tcpck.Context(0, probe=True)
     s = torch.cuda.current_stream()
     for spec in filter(None, args.fixed.split(",")):
         L, S = (int(x) for x in spec.split("/"))

@@ -15,7 +15,7 @@ import tcpck  # noqa: E402
 
 
 def main():
-    ctx = tcpck.Context(0)
+    ctx = tcpck.Context(0, probe=True)
     s = torch.cuda.current_stream()
     nbytes = 1492 << 20
     buf = torch.empty(nbytes, dtype=torch.uint8, device="cuda")

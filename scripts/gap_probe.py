@@ -31,7 +31,7 @@ def timed(fn, s, reps=20, rounds=4):
 
 
 def main():
-    ctx = tcpck.Context(0)
+    ctx = tcpck.Context(0, probe=True)
     s = torch.cuda.current_stream()
     K = tcpck
     for S, L in ((1536, 1492), (2048, 1492), (128, 96), (160, 96), (256, 96), (96, 64), (1492, 1492)):

@@ -31,7 +31,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--gs", default="", help="gstream params to compare (variant | oversub << 16), e.g. 0x100000,0x200002")
     args = ap.parse_args()
-    ctx = tcpck.Context(0)
+    ctx = tcpck.Context(0, probe=True)
     s = torch.cuda.current_stream()
     ops = {"checksum": tcpck.OP_CHECKSUM, "fill": tcpck.OP_FILL}
     cands = [("auto", None, 0), ("gstream U4", tcpck.KERNEL_GSTREAM, 0),

@@ -42,7 +42,7 @@ def report(name, ms, nbytes):
 
 
 def main():
-    ctx = tcpck.Context(0)
+    ctx = tcpck.Context(0, probe=True)
     s = torch.cuda.current_stream()
     target = 1.5e9
     for L in (96, 160, 192, 320, 480):

@@ -57,7 +57,7 @@ def main():
     ap.add_argument("--ms", default="1,4,8,12,16,24,32,64")
     args = ap.parse_args()
     ms = [int(m) for m in args.ms.split(",")]
-    ctx = tcpck.Context(0)
+    ctx = tcpck.Context(0, probe=True)
     for what in args.what.split(","):
         if what in FIXED:
             L, n, kern, variants = FIXED[what]

@@ -31,7 +31,7 @@ def run(fn, n=5):
 
 
 def main():
-    ctx = tcpck.Context(0)
+    ctx = tcpck.Context(0, probe=True)
     n, L = 1 << 20, 1492
     if "--rs" in sys.argv:  # rstream 18 vs 20 (default-policy first step): FETCH_SIZE per launch
         a = torch.empty(n * L, dtype=torch.uint8, device="cuda")

@@ -46,7 +46,7 @@ def main():
     p.add_argument("--no-fixed", action="store_true")
     p.add_argument("--lengths", default="", help="comma list of fixed image lengths (default: all)")
     args = p.parse_args()
-    ctx = tcpck.Context(0)
+    ctx = tcpck.Context(0, probe=True)
     s = torch.cuda.current_stream()
     K = tcpck
     fixed_l = [int(x) for x in args.lengths.split(",")] if args.lengths else FIXED_L

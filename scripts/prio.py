@@ -20,7 +20,7 @@ VARIANTS = [("U4", 0), ("U2", 1), ("U8", 2), ("U4 prio-graded", 4), ("U4 prio-ha
 
 
 def main():
-    ctx = tcpck.Context(0)
+    ctx = tcpck.Context(0, probe=True)
     stream = torch.cuda.current_stream()
     L = 1492
     nmax = (16 << 30) // L

@@ -85,7 +85,7 @@ def case(ctx, s, name, n, slot, ln, fixed_len=None):
 
 
 def main():
-    ctx = tcpck.Context(0)
+    ctx = tcpck.Context(0, probe=True)
     s = torch.cuda.current_stream()
     rng = np.random.default_rng(42)
     n = 1 << 20

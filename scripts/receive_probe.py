@@ -37,7 +37,7 @@ def b2b(fn, s, reps=20, rounds=5):
 
 
 def main():
-    ctx = tcpck.Context(0)
+    ctx = tcpck.Context(0, probe=True)
     s = torch.cuda.current_stream()
     n, L = 1 << 20, 1492
     ok = torch.empty(n, dtype=torch.uint8, device="cuda")

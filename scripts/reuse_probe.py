@@ -18,7 +18,7 @@ import tcpck  # noqa: E402
 
 
 def main():
-    ctx = tcpck.Context(0)
+    ctx = tcpck.Context(0, probe=True)
     s = torch.cuda.current_stream()
     n, L = 1 << 20, 1492
     arenas = []

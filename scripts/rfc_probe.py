@@ -13,7 +13,7 @@ from slot_probe import PEAK, timed  # noqa: E402
 
 
 def main():
-    ctx = tcpck.Context(0)
+    ctx = tcpck.Context(0, probe=True)
     s = torch.cuda.current_stream()
     for L in (1492, 1024, 4096):
         n = 1566572544 // L

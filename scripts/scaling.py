@@ -32,7 +32,7 @@ def time_launch(fn, reps=15):
 
 
 def main():
-    ctx = tcpck.Context(0)
+    ctx = tcpck.Context(0, probe=True)
     stream = torch.cuda.current_stream()
     max_bytes = 24 << 30
     arena = torch.empty(max_bytes, dtype=torch.uint8, device="cuda")

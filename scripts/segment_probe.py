@@ -29,7 +29,7 @@ def main():
     ap.add_argument("--cases", default="1460:1504,1024:1056,1448:1488,9000:9040,65532:65568")
     ap.add_argument("--bytes", type=int, default=1536 << 20)
     args = ap.parse_args()
-    ctx = tcpck.Context(0)
+    ctx = tcpck.Context(0, probe=True)
     s = torch.cuda.current_stream()
     P = args.bytes
     payload = torch.empty(P, dtype=torch.uint8, device="cuda")

@@ -69,7 +69,7 @@ def main():
     ap.add_argument("--kernels", default="auto,seg,ss,ss4,ss8")
     ap.add_argument("--bytes", type=int, default=1 << 31)
     args = ap.parse_args()
-    ctx = tcpck.Context(0)
+    ctx = tcpck.Context(0, probe=True)
     s = torch.cuda.current_stream()
     K = tcpck
     kern = {"auto": (K.KERNEL_AUTO, 0), "seg": (K.KERNEL_SEG, 0)}

@@ -35,7 +35,7 @@ def b2b(fn, s, reps=20, rounds=5):
 
 
 def main():
-    ctx = tcpck.Context(0)
+    ctx = tcpck.Context(0, probe=True)
     s = torch.cuda.current_stream()
     # slots
     n = 1 << 20

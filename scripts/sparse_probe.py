@@ -23,7 +23,7 @@ MS = [int(x) for x in os.environ.get("SP_MS", "4,8,16,32").split(",")]
 
 
 def main():
-    ctx = tcpck.Context(0)
+    ctx = tcpck.Context(0, probe=True)
     s = torch.cuda.current_stream()
     arena = torch.empty(3 << 30, dtype=torch.uint8, device="cuda")
     arena.fill_(7)

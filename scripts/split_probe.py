@@ -16,7 +16,7 @@ import tcpck  # noqa: E402
 
 
 def main():
-    ctx = tcpck.Context(0)
+    ctx = tcpck.Context(0, probe=True)
     s = torch.cuda.current_stream()
     N, L = 8 << 20, 1492
     a = torch.empty(N * L, dtype=torch.uint8, device="cuda")

@@ -24,7 +24,7 @@ def main():
     ap.add_argument("--variants", default="1,2,5")
     ap.add_argument("--ops", default="checksum")
     args = ap.parse_args()
-    ctx = tcpck.Context(0)
+    ctx = tcpck.Context(0, probe=True)
     s = torch.cuda.current_stream()
     K = tcpck
     rng = np.random.default_rng(7)

@@ -18,7 +18,7 @@ import tcpck  # noqa: E402
 
 
 def main():
-    ctx = tcpck.Context(0)
+    ctx = tcpck.Context(0, probe=True)
     L, n = 1492, 1 << 20
     arena = torch.empty(n * L, dtype=torch.uint8, device="cuda")
     tcpck.synth_fixed(arena, L, L, n, seed=5)

@@ -68,7 +68,7 @@ def main():
     p.add_argument("--rounds", type=int, default=5)
     p.add_argument("--reps", type=int, default=10)
     args = p.parse_args()
-    ctx = tcpck.Context(0)
+    ctx = tcpck.Context(0, probe=True)
     stream = torch.cuda.current_stream()
     report = {}
     for cfg in args.configs.split(","):

@@ -23,7 +23,7 @@ def main():
     ap.add_argument("--n", type=int, default=400)
     ap.add_argument("--idle", type=float, default=2.0, help="idle seconds before the series")
     args = ap.parse_args()
-    ctx = tcpck.Context(0)
+    ctx = tcpck.Context(0, probe=True)
     s = torch.cuda.current_stream()
     if args.what == "c3":
         from synth_np import mixed_layout

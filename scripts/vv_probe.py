@@ -16,7 +16,7 @@ from synth_np import mixed_layout  # noqa: E402
 
 
 def main():
-    ctx = tcpck.Context(0)
+    ctx = tcpck.Context(0, probe=True)
     s = torch.cuda.current_stream()
     off, ln, total = mixed_layout(4 << 20, seed=42)
     n = ln.size

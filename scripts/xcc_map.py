@@ -15,7 +15,7 @@ import tcpck  # noqa: E402
 
 
 def main():
-    ctx = tcpck.Context(0)
+    ctx = tcpck.Context(0, probe=True)
     props = torch.cuda.get_device_properties(0)
     print(f"device: {props.name} CUs {props.multi_processor_count} mem {props.total_memory / 2**30:.0f} GiB "
           f"gcn {getattr(props, 'gcnArchName', '?')}", flush=True)

@@ -31,7 +31,7 @@ def b2b(fn, s, reps=20, rounds=5):
 
 
 def main():
-    ctx = tcpck.Context(0)
+    ctx = tcpck.Context(0, probe=True)
     s = torch.cuda.current_stream()
     K = tcpck
     n, L = 1 << 20, 1492

@@ -72,7 +72,7 @@ def main():
     ap.add_argument("--m-sweep", action="store_true")
     ap.add_argument("--cap-sweep", action="store_true")
     what = ap.parse_args().what
-    ctx = tcpck.Context(0)
+    ctx = tcpck.Context(0, probe=True)
     s = torch.cuda.current_stream()
     if what == "bare":
         buf = torch.empty(17 << 30, dtype=torch.uint8, device="cuda")

@@ -22,6 +22,7 @@
 
 #include "tcpck.h"
 #include "tcpck_tuning.h"
+#include "tcpck_probe.h"
 #include "tcpck_internal.h"
 
 using tcpck::SegArgs;
@@ -787,6 +788,8 @@ int tcpck_batch_var(tcpck_ctx *ctx, int op, int mode, void *d_arena, const uint6
                             TCPCK_KERNEL_AUTO, 0, stream);
 }
 
+#ifdef TCPCK_PROBE
+// measurement-only entry points (libtcpck_probe.so; include/tcpck_tuning.h)
 int tcpck_diag_stream(tcpck_ctx *ctx, int variant, const void *d_buf, uint64_t bytes, void *d_out,
                       tcpck_stream stream) {
   if (!ctx || !d_buf || !d_out || bytes < 4096) return TCPCK_EINVAL;
@@ -801,6 +804,7 @@ int tcpck_ctx_set_debug(tcpck_ctx *ctx, void *d_buf) {
   ctx->dbg = d_buf;
   return TCPCK_OK;
 }
+#endif  // TCPCK_PROBE
 
 int tcpck_batch_fixed_ex(tcpck_ctx *ctx, int op, int mode, void *d_arena, uint64_t stride, uint32_t len,
                          uint64_t count, void *d_out, int kernel, int param, tcpck_stream stream) {

@@ -191,10 +191,17 @@ hipError_t launch_one(const GroupStreamArgs &a, uint32_t num_cus, hipStream_t st
 
 template <int U, int G, int SPOL, int LPOL, bool FLINE, int WB>
 hipError_t by_op(int op, const GroupStreamArgs &a, uint32_t num_cus, hipStream_t s) {
+#ifndef TCPCK_PROBE
+  // AUTO sends only FILL here: vvstream / rstream CHECKSUM and VERIFY these
+  // layouts equally fast or faster (gstream)
+  if (op != kFill) return hipErrorInvalidValue;
+#endif
   switch (op) {
-    case kChecksum: return launch_one<U, G, kChecksum, SPOL, LPOL, false>(a, num_cus, s);
     case kFill: return launch_one<U, G, kFill, SPOL, LPOL, FLINE, WB>(a, num_cus, s);
+#ifdef TCPCK_PROBE
+    case kChecksum: return launch_one<U, G, kChecksum, SPOL, LPOL, false>(a, num_cus, s);
     case kVerify: return launch_one<U, G, kVerify, SPOL, LPOL, false>(a, num_cus, s);
+#endif
     default: return hipErrorInvalidValue;
   }
 }
@@ -233,12 +240,15 @@ hipError_t by_len_np(int op, const GroupStreamArgs &a, uint32_t num_cus, hipStre
 
 hipError_t launch_np(int op, int variant, const GroupStreamArgs &b, uint32_t num_cus, hipStream_t stream) {
   switch (variant & ~4) {
+    // AUTO's variants (tcpck_api.hip run_fixed_impl: FILL of 48-240 B)
     case 0: return by_len_np<4>(op, b, num_cus, stream);
+    case 0x80: return by_len_np<4, 0>(op, b, num_cus, stream);
+    case 0x401: return op == kFill ? by_len_np<8, 2, 2>(op, b, num_cus, stream) : hipErrorInvalidValue;
+#ifdef TCPCK_PROBE
     case 1: return by_len_np<8>(op, b, num_cus, stream);
     case 2: return by_len_np<2>(op, b, num_cus, stream);
-    case 0x80: return by_len_np<4, 0>(op, b, num_cus, stream);
     case 0x400: return op == kFill ? by_len_np<4, 2, 2>(op, b, num_cus, stream) : hipErrorInvalidValue;
-    case 0x401: return op == kFill ? by_len_np<8, 2, 2>(op, b, num_cus, stream) : hipErrorInvalidValue;
+#endif
     default: return hipErrorInvalidValue;
   }
 }
@@ -258,12 +268,22 @@ hipError_t launch_gstream(int op, int variant, const GroupStreamArgs &a, uint32_
   b.order = (variant & 4) ? dev::kOrderDefault : 4u;  // XCD-chunked order, groups of 16 blocks
   if (variant & ~0xFF7) return hipErrorInvalidValue;
   if (a.len & (a.len - 1)) return launch_np(op, variant, b, num_cus, stream);
+  // AUTO's variants (tcpck_api.hip run_fixed_impl): 0 (FILL of 512 B-1 KiB),
+  // kGstreamDefaultLoads (FILL <= 256 B), kGstreamWriteBack (FILL <= 128 B)
+  switch (variant & ~4) {
+    case 0: return by_len<4>(op, b, num_cus, stream);
+    case kGstreamDefaultLoads: return by_len<4, -1, 0>(op, b, num_cus, stream);  // default-policy loads
+    case kGstreamWriteBack:  // every chunk written back whole, nt stores, U8
+      return op == kFill ? by_len<8, -1, 2, false, 2>(op, b, num_cus, stream) : hipErrorInvalidValue;
+    default: break;
+  }
+#ifdef TCPCK_PROBE
+  // measurement-only variants (libtcpck_probe.so)
   if (variant & 0xC00) {  // FILL: whole-chunk write-back (bit 10: nt stores, bit 11: default policy)
     if (op != kFill) return hipErrorInvalidValue;
     switch (variant & 0xDF3) {
       case 0x400: return by_len<4, -1, 2, false, 2>(op, b, num_cus, stream);
       case 0x800: return by_len<4, -1, 2, false, 0>(op, b, num_cus, stream);
-      case 0x401: return by_len<8, -1, 2, false, 2>(op, b, num_cus, stream);
       case 0xC00: return by_len<4, -1, 2, false, 16>(op, b, num_cus, stream);  // sc1
       default: return hipErrorInvalidValue;
     }
@@ -281,18 +301,18 @@ hipError_t launch_gstream(int op, int variant, const GroupStreamArgs &a, uint32_
       case 0x10: return by_len<4, 0>(op, b, num_cus, stream);    // buffer stores, default policy
       case 0x20: return by_len<4, 2>(op, b, num_cus, stream);    // buffer stores, nt
       case 0x40: return by_len<4, 16>(op, b, num_cus, stream);   // buffer stores, sc1
-      case 0x80: return by_len<4, -1, 0>(op, b, num_cus, stream);   // default-policy loads
       case 0x100: return by_len<4, 0, 0>(op, b, num_cus, stream);   // both
       case 0x22: return by_len<2, 2>(op, b, num_cus, stream);    // U2, nt buffer stores
       default: return hipErrorInvalidValue;
     }
   }
   switch (variant & 3) {
-    case 0: return by_len<4>(op, b, num_cus, stream);
     case 1: return by_len<8>(op, b, num_cus, stream);
     case 2: return by_len<2>(op, b, num_cus, stream);
-    default: return hipErrorInvalidValue;
+    default: break;
   }
+#endif
+  return hipErrorInvalidValue;
 }
 
 }  // namespace tcpck

@@ -240,17 +240,21 @@ SegShape shape_for_len(uint64_t typical_len) {
 hipError_t launch_seg(int op, int mode, bool fixed, SegShape shape, const SegArgs &a,
                       uint32_t num_cus, hipStream_t stream) {
   switch (shape) {
+    // the shapes AUTO picks (shape_for_len)
     case kShapeSmall: return dispatch_mode<8, 2>(mode, op, fixed, a, num_cus, stream);
     case kShapeMss: return dispatch_mode<16, 6>(mode, op, fixed, a, num_cus, stream);
+    case kShapeW2: return dispatch_mode<128, 4>(mode, op, fixed, a, num_cus, stream);
+    case kShapeW4: return dispatch_mode<256, 4>(mode, op, fixed, a, num_cus, stream);
+    case kShapeW8: return dispatch_mode<512, 4>(mode, op, fixed, a, num_cus, stream);
+    case kShapeW16: return dispatch_mode<1024, 2>(mode, op, fixed, a, num_cus, stream);
+#ifdef TCPCK_PROBE
+    // measurement-only shapes (libtcpck_probe.so)
     case kShapeJumbo: return dispatch_mode<64, 4>(mode, op, fixed, a, num_cus, stream);
     case kShapeWave2: return dispatch_mode<64, 2>(mode, op, fixed, a, num_cus, stream);
     case kShapeG32: return dispatch_mode<32, 3>(mode, op, fixed, a, num_cus, stream);
     case kShapeG4: return dispatch_mode<4, 8>(mode, op, fixed, a, num_cus, stream);
-    case kShapeW4: return dispatch_mode<256, 4>(mode, op, fixed, a, num_cus, stream);
-    case kShapeW8: return dispatch_mode<512, 4>(mode, op, fixed, a, num_cus, stream);
-    case kShapeW16: return dispatch_mode<1024, 2>(mode, op, fixed, a, num_cus, stream);
     case kShapeW16U4: return dispatch_mode<1024, 4>(mode, op, fixed, a, num_cus, stream);
-    case kShapeW2: return dispatch_mode<128, 4>(mode, op, fixed, a, num_cus, stream);
+#endif
     default: return hipErrorInvalidValue;
   }
 }

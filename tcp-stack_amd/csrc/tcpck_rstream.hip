@@ -261,6 +261,14 @@ hipError_t launch_rstream(int op, int variant, const FixedStreamArgs &a, uint32_
     b.order = 4u;
     return dispatch<4, false, 0, 7, kRfc1071>(op, b, num_cus, stream);
   }
+  if (variant == 20) {  // the policy (AUTO): U4, v_dot2 sums, buffer loads, XCD-chunked order, L2-kept first step
+    FixedStreamArgs b = a;
+    b.order = 4u;
+    return dispatch<4, false, 0, 7>(op, b, num_cus, stream);
+  }
+#ifdef TCPCK_PROBE
+  // measurement-only variants (libtcpck_probe.so): steps in flight, time
+  // stamps, issue priorities, sum/load flavours and block orders
   switch (variant) {
     case 0: return dispatch<4, false>(op, a, num_cus, stream);
     case 1: return dispatch<2, false>(op, a, num_cus, stream);
@@ -276,12 +284,12 @@ hipError_t launch_rstream(int op, int variant, const FixedStreamArgs &a, uint32_
     case 11: return dispatch<4, false, 0, 2>(op, a, num_cus, stream);
     case 12: return dispatch<2, false, 0, 3>(op, a, num_cus, stream);
     case 13: return dispatch<8, false, 0, 3>(op, a, num_cus, stream);
-    case 20: case 21: {  // 18 / 14 with the first step read with the default policy (FLAV bit 2)
+    case 21: {  // 14 with the first step read with the default policy (FLAV bit 2)
       FixedStreamArgs b = a;
-      b.order = variant == 20 ? 4u : dev::kOrderXcd;
+      b.order = dev::kOrderXcd;
       return dispatch<4, false, 0, 7>(op, b, num_cus, stream);
     }
-    case 22: {  // 18 with every step read with the default policy (FLAV bit 3)
+    case 22: {  // 20 with every step read with the default policy (FLAV bit 3)
       FixedStreamArgs b = a;
       b.order = 4u;
       return dispatch<4, false, 0, 11>(op, b, num_cus, stream);
@@ -299,8 +307,10 @@ hipError_t launch_rstream(int op, int variant, const FixedStreamArgs &a, uint32_
       b.order = variant <= 15 ? dev::kOrderXcd : (variant == 16 ? 1u : (variant == 17 ? 2u : (variant == 18 ? 4u : 6u)));
       return variant == 15 ? dispatch<8, false, 0, 3>(op, b, num_cus, stream) : dispatch<4, false, 0, 3>(op, b, num_cus, stream);
     }
-    default: return hipErrorInvalidValue;
+    default: break;
   }
+#endif
+  return hipErrorInvalidValue;
 }
 
 }  // namespace tcpck

@@ -348,6 +348,8 @@ hipError_t launch_segment(int mode, int variant, SegmentArgs a, uint32_t oversub
         return mode == kRef ? launch_wide<4, 4, kRef>(a, oversub, num_cus, stream)
                             : launch_wide<4, 4, kRfc1071>(a, oversub, num_cus, stream);
       return by_mode<4, 1, 0>(mode, a, oversub, num_cus, stream);
+#ifdef TCPCK_PROBE
+    // measurement-only variants (libtcpck_probe.so)
     case 1: return by_mode<4, 0>(mode, a, oversub, num_cus, stream);
     case 2: return by_mode<4, 1>(mode, a, oversub, num_cus, stream);
     case 3: return by_mode<4, 2>(mode, a, oversub, num_cus, stream);
@@ -363,6 +365,7 @@ hipError_t launch_segment(int mode, int variant, SegmentArgs a, uint32_t oversub
       return mode == kRef ? launch_wide<4, 4, kRef>(a, oversub, num_cus, stream)
                           : launch_wide<4, 4, kRfc1071>(a, oversub, num_cus, stream);
     }
+#endif
     default: return hipErrorInvalidValue;
   }
 }

@@ -519,15 +519,19 @@ hipError_t dispatch(int op, const SSArgs &a, uint32_t m, uint64_t min_waves, uin
                     bool keepl, int hdr_mode) {
   if (a.hdr) {  // VERIFY + the run's headers into the array (tcpck_batch_receive)
     if (op != kVerify) return hipErrorInvalidValue;
-    if (a.mode != kRef) {
-      if (hdr_mode == 2) return launch_one<U, kVerify, FIXED, kRfc1071, 2>(a, m, min_waves, num_cus, s);
+    if (hdr_mode == 2 && !keepl)  // AUTO: the headers from the stream's registers
+      return a.mode != kRef ? launch_one<U, kVerify, FIXED, kRfc1071, 2>(a, m, min_waves, num_cus, s)
+                            : launch_one<U, kVerify, FIXED, kRef, 2>(a, m, min_waves, num_cus, s);
+#ifdef TCPCK_PROBE
+    if (a.mode != kRef)
       return keepl ? launch_one<U, kVerify, FIXED, kRfc1071, 1, true>(a, m, min_waves, num_cus, s)
                    : launch_one<U, kVerify, FIXED, kRfc1071, 1, false>(a, m, min_waves, num_cus, s);
-    }
-    if (hdr_mode == 2) return launch_one<U, kVerify, FIXED, kRef, 2>(a, m, min_waves, num_cus, s);
     if (hdr_mode == 3) return launch_one<U, kVerify, FIXED, kRef, 3>(a, m, min_waves, num_cus, s);
     return keepl ? launch_one<U, kVerify, FIXED, kRef, 1, true>(a, m, min_waves, num_cus, s)
                  : launch_one<U, kVerify, FIXED, kRef, 1, false>(a, m, min_waves, num_cus, s);
+#else
+    return hipErrorInvalidValue;
+#endif
   }
   if (a.mode != kRef) {
     switch (op) {
@@ -603,13 +607,20 @@ hipError_t launch_sstream(int op, int variant, bool fixed, const RunArgs &r, uin
                                       fixed ? 8u << 10 : 16u << 10);
   const int u = variant & 3;  // 0: policy, 1: U4, 2: U8
   const bool u8 = u == 2;
+#ifndef TCPCK_PROBE
+  // the product library runs the policy (0) and its RECEIVE form (+ 32) only
+  if ((variant & ~32) != 0) return hipErrorInvalidValue;
+#endif
   const bool keepl = (variant & 16) != 0;  // HDR 1: the stream read with the default cache policy
   // HDR: + 32 the headers from the stream's registers (kSstreamHdrStream), + 64 with nt stores
   const int hdr_mode = (variant & 32) ? ((variant & 64) ? 3 : 2) : 1;
-  if (fixed) return u8 ? dispatch<8, true>(op, a, m, min_waves, num_cus, stream, keepl, hdr_mode)
-                       : dispatch<4, true>(op, a, m, min_waves, num_cus, stream, keepl, hdr_mode);
-  return u8 ? dispatch<8, false>(op, a, m, min_waves, num_cus, stream, keepl, hdr_mode)
-            : dispatch<4, false>(op, a, m, min_waves, num_cus, stream, keepl, hdr_mode);
+#ifdef TCPCK_PROBE
+  if (u8) return fixed ? dispatch<8, true>(op, a, m, min_waves, num_cus, stream, keepl, hdr_mode)
+                       : dispatch<8, false>(op, a, m, min_waves, num_cus, stream, keepl, hdr_mode);
+#endif
+  if (u8) return hipErrorInvalidValue;
+  return fixed ? dispatch<4, true>(op, a, m, min_waves, num_cus, stream, keepl, hdr_mode)
+               : dispatch<4, false>(op, a, m, min_waves, num_cus, stream, keepl, hdr_mode);
 }
 
 }  // namespace tcpck

@@ -502,8 +502,13 @@ hipError_t launch_vvstream(int op, int variant, bool fixed, const RunArgs &a, ui
       u8 = false;
     }
     split = m >= 4;
-  } else if (variant > 4 || variant < 0) {
-    return hipErrorInvalidValue;
+  } else {
+#ifdef TCPCK_PROBE
+    // measurement-only (libtcpck_probe.so): 0/1 byte split U4/U8, 2/3 equal counts, one run per resident wave
+    if (variant > 4 || variant < 0) return hipErrorInvalidValue;
+#else
+    return hipErrorInvalidValue;  // the product library runs the policy only
+#endif
   }
   if (gap) return u8 ? dispatch<8, 1, 2>(op, a, m, flags, num_cus, stream) : dispatch<4, 1, 2>(op, a, m, flags, num_cus, stream);
   if (fixed) return u8 ? dispatch<8, 1, 1>(op, a, m, flags, num_cus, stream) : dispatch<4, 1, 1>(op, a, m, flags, num_cus, stream);

@@ -5,6 +5,12 @@ parity tests and bench.py.  There is no Python or CPU fallback for the batched
 path: if libtcpck.so is missing or the device is not a gfx950, constructing a
 ``Context`` raises.
 
+libtcpck.so holds the kernels the AUTO policy can pick; its tcpck_tuning.h
+entry points (``batch_*_ex``) accept only those.  ``Context(probe=True)``
+binds libtcpck_probe.so instead: the same sources built with every measured
+variant, the per-wave time stamps and the diag kernels (scripts/, the
+variant tests).
+
 Reference API mirrored (filixi/TCP-stack):
   * ``checksum16``   <- CalculateChecksum(const TcpPacket&), include/tcp-header.h:252-263
   * OP_FILL          <- Checksum()=0; Checksum()=CalculateChecksum(pkt),
@@ -19,6 +25,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_ROOT = os.path.dirname(HERE)
 LIB_PATH = os.path.join(PKG_ROOT, "libtcpck.so")
+PROBE_PATH = os.path.join(PKG_ROOT, "libtcpck_probe.so")
 
 OK = 0
 EINVAL = -22
@@ -46,8 +53,40 @@ KERNEL_VVSTREAM = 8  # packed variable or fixed (stride >= len): param = 0/1 U4/
 KERNEL_GSTREAM = 9  # fixed stride == len, len a power of two in [32, 1024], 16-B aligned arena: param = 0/1/2 U4/U8/U2 (+4 default block order) | oversub << 16
 KERNEL_SSTREAM = 10  # slotted layouts (fixed slots, stride % 16 == 0, or any offset list): param = 0 policy (U4, scattered order), 1 U4, 2 U8 (+4 default block order, +8 scattered) | oversub << 16
 SEG_SHAPES = {1: "G8/U2", 2: "G16/U6", 3: "G64/U4", 4: "G64/U2", 5: "G32/U3", 6: "G4/U8", 7: "W4/U4", 8: "W8/U4", 9: "W16/U2", 10: "W16/U4", 11: "W2/U4"}
-TUNING_EXPORTS = ("tcpck_batch_fixed_ex", "tcpck_batch_var_ex", "tcpck_ctx_set_debug", "tcpck_diag_stream",
-                  "tcpck_batch_segment_ex", "tcpck_batch_receive_ex")
+# include/tcpck_tuning.h: in libtcpck.so (AUTO's kernels only) and libtcpck_probe.so
+TUNING_EXPORTS = ("tcpck_batch_fixed_ex", "tcpck_batch_var_ex", "tcpck_batch_segment_ex", "tcpck_batch_receive_ex")
+# include/tcpck_tuning.h, measurement only: libtcpck_probe.so
+PROBE_EXPORTS = ("tcpck_ctx_set_debug", "tcpck_diag_stream")
+# Kernel params libtcpck.so runs (the AUTO policy's own choices, tcpck_api.hip
+# run_fixed_impl / run_var_impl); every other value needs libtcpck_probe.so.
+SEG_AUTO_SHAPES = (0, 1, 2, 7, 8, 9, 11)  # by length, G8/U2, G16/U6, W4, W8, W16, W2 (shape_for_len)
+RSTREAM_AUTO = (20, 25)                   # the policy; 25: its FILL with the field-block pass
+GSTREAM_AUTO = (0, 0x80, 0x401)           # (+ 4: default block order)
+SSTREAM_AUTO = (0, 32)                    # the policy; + 32: RECEIVE headers from the stream
+
+
+def in_product(kernel: int, param: int, op: int | None = None) -> bool:
+    """Whether libtcpck.so runs `kernel` with `param` (tcpck_tuning.h) for `op`."""
+    if kernel == KERNEL_AUTO:
+        return True
+    if kernel == KERNEL_SEG:
+        return (param & 0xFF) in SEG_AUTO_SHAPES
+    if kernel == KERNEL_RSTREAM:
+        return (param & 0xFF) in RSTREAM_AUTO
+    if kernel == KERNEL_VVSTREAM:
+        return (param & 7) == 4
+    if kernel == KERNEL_GSTREAM:  # AUTO's FILL only
+        return (param & 0xFFFF & ~4) in GSTREAM_AUTO and op in (None, OP_FILL)
+    if kernel == KERNEL_SSTREAM:
+        return (param & 0xFF) in SSTREAM_AUTO
+    return True  # unknown kernels: both libraries reject them
+
+
+def segment_in_product(param: int) -> bool:
+    """Whether libtcpck.so runs tcpck_batch_segment_ex with `param` (0: the policy; + 8: default order)."""
+    return (param & 7) == 0
+
+
 PARAM_FILL_UPDATE = 1 << 28  # FILL: the kernel's CHECKSUM pass + the field-update pass
 PARAM_FILL_INSTREAM = 1 << 29  # FILL under AUTO: the field zeroed in the stream
 PARAM_RECEIVE_TWO_PASS = 1 << 30  # RECEIVE into a header array: separate header pass
@@ -78,17 +117,18 @@ class Layout(ctypes.Structure):
                 ("reserved", ctypes.c_uint32)]
 
 
-_lib = None
+_libs: dict = {}
 
 
-def lib() -> ctypes.CDLL:
-    """Loads libtcpck.so (built in-tree by __graft_entry__.build()); raises if absent."""
-    global _lib
-    if _lib is not None:
-        return _lib
-    if not os.path.exists(LIB_PATH):
-        raise ImportError(f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
-    L = ctypes.CDLL(LIB_PATH)
+def lib(probe: bool = False) -> ctypes.CDLL:
+    """Loads libtcpck.so (probe: libtcpck_probe.so), built in-tree by
+    __graft_entry__.build(); raises if absent."""
+    if probe in _libs:
+        return _libs[probe]
+    path = PROBE_PATH if probe else LIB_PATH
+    if not os.path.exists(path):
+        raise ImportError(f"{path} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
+    L = ctypes.CDLL(path)
     vp, u64, u32, i32, sz = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int, ctypes.c_size_t
     sig = {
         "tcpck_abi_version": (i32, []),
@@ -130,11 +170,18 @@ def lib() -> ctypes.CDLL:
         "tcpck_diag_stream": (i32, [vp, i32, vp, u64, vp, vp]),
     }
     for name, (res, args) in sig.items():
+        if name in PROBE_EXPORTS and not probe:
+            continue  # measurement-only: not in the product library
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
-    _lib = L
+    _libs[probe] = L
     return L
+
+
+def probe_lib() -> ctypes.CDLL:
+    """libtcpck_probe.so (every measured kernel variant; tcpck_tuning.h in full)."""
+    return lib(probe=True)
 
 
 def strerror(status: int) -> str:
@@ -216,14 +263,16 @@ def synth_var(arena, offsets, lengths, max_len: int, count: int, seed: int = 42,
 class Context:
     """One libtcpck context bound to a HIP device (gfx950 only)."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, probe: bool = False):
         self._h = ctypes.c_void_p()
-        _check(lib().tcpck_ctx_create(device, ctypes.byref(self._h)), f"tcpck_ctx_create({device})")
+        self._L = lib(probe)
+        self.probe = probe
+        _check(self._L.tcpck_ctx_create(device, ctypes.byref(self._h)), f"tcpck_ctx_create({device})")
         self.device = device
 
     def close(self) -> None:
         if self._h:
-            lib().tcpck_ctx_destroy(self._h)
+            self._L.tcpck_ctx_destroy(self._h)
             self._h = ctypes.c_void_p()
 
     def __enter__(self):
@@ -241,7 +290,7 @@ class Context:
     # device-resident batches (the hot path)
     def batch_fixed(self, op: int, arena, stride: int, length: int, count: int, out,
                     mode: int = MODE_REF, stream=None) -> None:
-        _check(lib().tcpck_batch_fixed(self._h, op, mode, _ptr(arena), stride, length, count,
+        _check(self._L.tcpck_batch_fixed(self._h, op, mode, _ptr(arena), stride, length, count,
                                        _ptr(out), _stream(stream)), "tcpck_batch_fixed")
 
     def batch_var(self, op: int, arena, offsets, lengths, count: int, out, mode: int = MODE_REF,
@@ -249,7 +298,7 @@ class Context:
                   sorted: bool = False, stream=None) -> None:
         lay = Layout(total_bytes, min_len, max_len,
                      (LAYOUT_PACKED if packed else 0) | (LAYOUT_SORTED if sorted else 0), 0)
-        _check(lib().tcpck_batch_var(self._h, op, mode, _ptr(arena), _ptr(offsets), _ptr(lengths),
+        _check(self._L.tcpck_batch_var(self._h, op, mode, _ptr(arena), _ptr(offsets), _ptr(lengths),
                                      count, _ptr(out), ctypes.byref(lay), _stream(stream)),
                "tcpck_batch_var")
 
@@ -257,7 +306,7 @@ class Context:
                       out=None, mode: int = MODE_REF, stream=None) -> None:
         """Retransmit batch (socket-internal.h:376-377 + socket-manager.cc:9-10): bytes 20-23 of every
         image := htonl(ack or acks[k]), checksum at 28-29 updated incrementally (tcpck_batch_set_ack)."""
-        _check(lib().tcpck_batch_set_ack(self._h, mode, _ptr(arena), _ptr(offsets), stride, count,
+        _check(self._L.tcpck_batch_set_ack(self._h, mode, _ptr(arena), _ptr(offsets), stride, count,
                                          _ptr(acks), ack & 0xFFFFFFFF, _ptr(out), _stream(stream)),
                "tcpck_batch_set_ack")
 
@@ -265,7 +314,7 @@ class Context:
         """TcpHeaderN2H (== TcpHeaderH2N, tcp-header.h:193-221) in place on the first 32 bytes of
         every image (tcpck_batch_header_swap); after VERIFY this completes ReceivePacket's
         front half (socket-manager.h:182-184)."""
-        _check(lib().tcpck_batch_header_swap(self._h, _ptr(arena), _ptr(offsets), stride, count,
+        _check(self._L.tcpck_batch_header_swap(self._h, _ptr(arena), _ptr(offsets), stride, count,
                                              _stream(stream)), "tcpck_batch_header_swap")
 
     def batch_receive(self, arena, count: int, ok, hdr=None, stride: int = 0, length: int = 0, offsets=None,
@@ -281,9 +330,9 @@ class Context:
         args = (self._h, mode, _ptr(arena), stride, length, _ptr(offsets), _ptr(lengths), count, _ptr(ok), _ptr(hdr),
                 ctypes.byref(lay))
         if kernel is None:
-            _check(lib().tcpck_batch_receive(*args, _stream(stream)), "tcpck_batch_receive")
+            _check(self._L.tcpck_batch_receive(*args, _stream(stream)), "tcpck_batch_receive")
         else:
-            _check(lib().tcpck_batch_receive_ex(*args, kernel, param, _stream(stream)), "tcpck_batch_receive_ex")
+            _check(self._L.tcpck_batch_receive_ex(*args, kernel, param, _stream(stream)), "tcpck_batch_receive_ex")
 
     def batch_segment(self, payload, payload_bytes: int, seg: int, hdr, seq0: int, images, stride: int,
                       out=None, mode: int = MODE_REF, param: int | None = None, stream=None) -> int:
@@ -296,15 +345,15 @@ class Context:
         args = (self._h, mode, _ptr(payload), payload_bytes, seg, h.ctypes.data, seq0 & 0xFFFFFFFF, _ptr(images),
                 stride, _ptr(out))
         if param is None:
-            _check(lib().tcpck_batch_segment(*args, _stream(stream)), "tcpck_batch_segment")
+            _check(self._L.tcpck_batch_segment(*args, _stream(stream)), "tcpck_batch_segment")
         else:
-            _check(lib().tcpck_batch_segment_ex(*args, param, _stream(stream)), "tcpck_batch_segment_ex")
+            _check(self._L.tcpck_batch_segment_ex(*args, param, _stream(stream)), "tcpck_batch_segment_ex")
         return (payload_bytes + seg - 1) // seg
 
     # explicit kernel choice (include/tcpck_tuning.h)
     def batch_fixed_ex(self, op: int, arena, stride: int, length: int, count: int, out, kernel: int,
                        param: int = 0, mode: int = MODE_REF, stream=None) -> None:
-        _check(lib().tcpck_batch_fixed_ex(self._h, op, mode, _ptr(arena), stride, length, count,
+        _check(self._L.tcpck_batch_fixed_ex(self._h, op, mode, _ptr(arena), stride, length, count,
                                           _ptr(out), kernel, param, _stream(stream)), "tcpck_batch_fixed_ex")
 
     def batch_var_ex(self, op: int, arena, offsets, lengths, count: int, out, kernel: int,
@@ -312,35 +361,37 @@ class Context:
                      max_len: int = 0, packed: bool = False, sorted: bool = False, stream=None) -> None:
         lay = Layout(total_bytes, min_len, max_len,
                      (LAYOUT_PACKED if packed else 0) | (LAYOUT_SORTED if sorted else 0), 0)
-        _check(lib().tcpck_batch_var_ex(self._h, op, mode, _ptr(arena), _ptr(offsets), _ptr(lengths),
+        _check(self._L.tcpck_batch_var_ex(self._h, op, mode, _ptr(arena), _ptr(offsets), _ptr(lengths),
                                         count, _ptr(out), ctypes.byref(lay), kernel, param,
                                         _stream(stream)), "tcpck_batch_var_ex")
 
     # host-memory batches (end to end, PCIe included)
     def host_batch_fixed(self, op: int, arena, stride: int, length: int, count: int, out,
                          mode: int = MODE_REF) -> None:
-        _check(lib().tcpck_host_batch_fixed(self._h, op, mode, _ptr(arena), stride, length, count,
+        _check(self._L.tcpck_host_batch_fixed(self._h, op, mode, _ptr(arena), stride, length, count,
                                             _ptr(out)), "tcpck_host_batch_fixed")
 
     def host_batch_var(self, op: int, arena, offsets, lengths, count: int, out,
                        mode: int = MODE_REF) -> None:
-        _check(lib().tcpck_host_batch_var(self._h, op, mode, _ptr(arena), _ptr(offsets),
+        _check(self._L.tcpck_host_batch_var(self._h, op, mode, _ptr(arena), _ptr(offsets),
                                           _ptr(lengths), count, _ptr(out)), "tcpck_host_batch_var")
 
     def diag_stream(self, variant: int, buf, nbytes: int, out, stream=None) -> None:
         """Timing-only streaming micro-kernel (include/tcpck_tuning.h)."""
-        _check(lib().tcpck_diag_stream(self._h, variant, _ptr(buf), nbytes, _ptr(out), _stream(stream)),
+        _check(self._L.tcpck_diag_stream(self._h, variant, _ptr(buf), nbytes, _ptr(out), _stream(stream)),
                "tcpck_diag_stream")
 
     def set_debug(self, buf) -> None:
         """Per-wave {start, end, hw_id, xcc_id} stamp buffer for timing builds (None = off)."""
-        _check(lib().tcpck_ctx_set_debug(self._h, _ptr(buf)), "tcpck_ctx_set_debug")
+        _check(self._L.tcpck_ctx_set_debug(self._h, _ptr(buf)), "tcpck_ctx_set_debug")
 
     def set_chunk_bytes(self, n: int) -> None:
-        _check(lib().tcpck_ctx_set_chunk_bytes(self._h, n), "tcpck_ctx_set_chunk_bytes")
+        _check(self._L.tcpck_ctx_set_chunk_bytes(self._h, n), "tcpck_ctx_set_chunk_bytes")
 
 
 def _ctx_array(ctxs):
+    if len({c.probe for c in ctxs}) > 1:
+        raise ValueError("contexts of libtcpck.so and libtcpck_probe.so cannot be mixed")
     arr = (ctypes.c_void_p * len(ctxs))(*[c._h.value for c in ctxs])
     return ctypes.cast(arr, ctypes.POINTER(ctypes.c_void_p)), arr
 
@@ -349,7 +400,7 @@ def host_batch_fixed_multi(ctxs, op: int, arena, stride: int, length: int, count
                            mode: int = MODE_REF) -> None:
     """tcpck_host_batch_fixed over several contexts (one per GPU): contiguous equal shards, one host thread each."""
     p, keep = _ctx_array(ctxs)
-    _check(lib().tcpck_host_batch_fixed_multi(p, len(ctxs), op, mode, _ptr(arena), stride, length, count, _ptr(out)),
+    _check(ctxs[0]._L.tcpck_host_batch_fixed_multi(p, len(ctxs), op, mode, _ptr(arena), stride, length, count, _ptr(out)),
            "tcpck_host_batch_fixed_multi")
     del keep
 
@@ -357,6 +408,6 @@ def host_batch_fixed_multi(ctxs, op: int, arena, stride: int, length: int, count
 def host_batch_var_multi(ctxs, op: int, arena, offsets, lengths, count: int, out, mode: int = MODE_REF) -> None:
     """tcpck_host_batch_var over several contexts: contiguous shards balanced by bytes."""
     p, keep = _ctx_array(ctxs)
-    _check(lib().tcpck_host_batch_var_multi(p, len(ctxs), op, mode, _ptr(arena), _ptr(offsets), _ptr(lengths), count,
+    _check(ctxs[0]._L.tcpck_host_batch_var_multi(p, len(ctxs), op, mode, _ptr(arena), _ptr(offsets), _ptr(lengths), count,
                                             _ptr(out)), "tcpck_host_batch_var_multi")
     del keep

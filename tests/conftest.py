@@ -113,3 +113,101 @@ def built_lib():
         import subprocess
         subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tcp-stack_amd"), "-j8"], check=True)
     return tcpck.lib()
+
+
+# ---- the product library and the probe library -------------------------------
+#
+# libtcpck.so carries only the kernels the AUTO policy picks; its tuning entry
+# points (batch_*_ex) accept those alone.  libtcpck_probe.so is the same
+# sources with every measured variant.  Variant tests run each AUTO choice on
+# libtcpck.so over their whole matrix, and each measurement-only variant once
+# (one representative case) on libtcpck_probe.so.
+
+class RoutedContext:
+    """A libtcpck.so context that sends explicit-kernel calls the product
+    library does not run to a libtcpck_probe.so context on the same device."""
+
+    def __init__(self, device: int = 0):
+        import tcpck
+        self._tcpck = tcpck
+        self.product = tcpck.Context(device)
+        self.probe = tcpck.Context(device, probe=True)
+
+    def _for(self, kernel, param, op=None):
+        return self.product if self._tcpck.in_product(kernel, param, op) else self.probe
+
+    def batch_fixed_ex(self, op, arena, stride, length, count, out, kernel, param=0, **kw):
+        return self._for(kernel, param, op).batch_fixed_ex(op, arena, stride, length, count, out, kernel, param, **kw)
+
+    def batch_var_ex(self, op, arena, offsets, lengths, count, out, kernel, param=0, **kw):
+        return self._for(kernel, param, op).batch_var_ex(op, arena, offsets, lengths, count, out, kernel, param,
+                                                         **kw)
+
+    def batch_receive(self, *a, kernel=None, param=0, **kw):
+        c = self.product if kernel is None else self._for(kernel, param & ~(1 << 30))
+        return c.batch_receive(*a, kernel=kernel, param=param, **kw)
+
+    def batch_segment(self, *a, param=None, **kw):
+        c = self.product if param is None or self._tcpck.segment_in_product(param) else self.probe
+        return c.batch_segment(*a, param=param, **kw)
+
+    def __getattr__(self, name):
+        return getattr(self.product, name)
+
+    def close(self):
+        self.product.close()
+        self.probe.close()
+
+
+def _variant_kernel(item):
+    """(kernel, param) of a variant test item, or None when the item names no variant."""
+    import tcpck
+    cs = getattr(item, "callspec", None)
+    if cs is None:
+        return None
+    p = cs.params
+    name = item.originalname or item.name
+    if "kernel" in p and ("param" in p or "variant" in p) and isinstance(p["kernel"], int):
+        return p["kernel"], p.get("param", p.get("variant"))
+    v = p.get("variant", p.get("param"))
+    if not isinstance(v, int):
+        return None
+    if "segment" in item.module.__name__ and "param" in p:
+        return ("segment", v)
+    for key, k in (("rstream", tcpck.KERNEL_RSTREAM), ("vvstream", tcpck.KERNEL_VVSTREAM),
+                   ("gstream", tcpck.KERNEL_GSTREAM), ("sstream", tcpck.KERNEL_SSTREAM),
+                   ("fused_hdr", tcpck.KERNEL_SSTREAM)):
+        if key in name or key in item.module.__name__:
+            return k, v
+    return None
+
+
+def pytest_collection_modifyitems(config, items):
+    """Measurement-only variants (libtcpck_probe.so) keep ONE representative
+    case per test function -- the middle one of their matrix; AUTO's variants
+    (libtcpck.so) keep every case."""
+    import tcpck
+    groups, keep, drop = {}, [], []
+    for it in items:
+        kv = _variant_kernel(it)
+        if kv is None:
+            keep.append(it)
+            continue
+        kernel, v = kv
+        op = tcpck.OP_CHECKSUM if kernel == tcpck.KERNEL_GSTREAM and "fill" not in it.name else None
+        prod = tcpck.segment_in_product(v) if kernel == "segment" else tcpck.in_product(kernel, v & ~(1 << 30), op)
+        if prod:
+            keep.append(it)
+        else:
+            groups.setdefault((it.module.__name__, it.originalname, kernel, v), []).append(it)
+    chosen = {id(g[len(g) // 2]) for g in groups.values()}
+    grouped = {id(x) for g in groups.values() for x in g}
+    for it in items:
+        if id(it) in chosen:
+            keep.append(it)
+        elif id(it) in grouped:
+            drop.append(it)
+    if drop:
+        config.hook.pytest_deselected(items=drop)
+        order = {id(it): i for i, it in enumerate(items)}
+        items[:] = sorted(keep, key=lambda it: order[id(it)])

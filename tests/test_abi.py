@@ -21,12 +21,53 @@ def test_header_and_binding_agree(built_lib):
     import tcpck
     assert declared_symbols() == sorted(tcpck.EXPORTS)
     assert declared_symbols("tcpck_tuning.h") == sorted(tcpck.TUNING_EXPORTS)
+    assert declared_symbols("tcpck_probe.h") == sorted(tcpck.PROBE_EXPORTS)
 
 
 def test_library_exports_every_declared_symbol(built_lib):
     for name in declared_symbols() + declared_symbols("tcpck_tuning.h"):
         assert hasattr(built_lib, name), name
     assert built_lib.tcpck_abi_version() == 1
+
+
+def test_probe_symbols_only_in_probe_library(built_lib):
+    """The measurement-only entry points (tcpck_probe.h) live in
+    libtcpck_probe.so; libtcpck.so does not export them."""
+    import ctypes
+    import tcpck
+    product = ctypes.CDLL(tcpck.LIB_PATH)
+    probe = tcpck.probe_lib()
+    for name in declared_symbols("tcpck_probe.h"):
+        assert not hasattr(product, name), name
+        assert hasattr(probe, name), name
+    for name in declared_symbols() + declared_symbols("tcpck_tuning.h"):
+        assert hasattr(probe, name), name
+
+
+def _kernels(path):
+    """{kernel name: {mangled template arguments}} of the code objects in a library."""
+    import re
+    with open(path, "rb") as f:
+        blob = f.read()
+    out = {}
+    for k, args in re.findall(rb"_ZN5tcpck12_GLOBAL__N_1[0-9]+([a-z_]+_kernel)I([A-Za-z0-9_]*?)EEvN", blob):
+        out.setdefault(k.decode(), set()).add(args.decode())
+    return out
+
+
+def test_product_library_holds_only_auto_kernels(built_lib):
+    """libtcpck.so carries the kernels the AUTO policy can pick and nothing
+    else (measurement-only code out of the product): rstream only
+    as the policy's instantiation <U4, op, no stamps, no priority, flavour 7,
+    REF / RFC 1071>; no diag kernels; fewer instantiations than the probe build
+    for every kernel that has measurement-only variants."""
+    import tcpck
+    prod, probe = _kernels(tcpck.LIB_PATH), _kernels(tcpck.PROBE_PATH)
+    assert set(prod["rstream_kernel"]) == {f"Li4ELi{op}ELb0ELi0ELi7ELi{m}E" for op in range(3) for m in range(2)}
+    blobs = [open(p, "rb").read() for p in (tcpck.LIB_PATH, tcpck.PROBE_PATH)]
+    assert b"diag_stream_kernel" not in blobs[0] and b"diag_stream_kernel" in blobs[1]
+    for k in ("rstream_kernel", "seg_kernel", "gstream_kernel", "sstream_kernel", "segment_kernel"):
+        assert len(prod[k]) < len(probe[k]), k
 
 
 def test_library_has_gfx950_code_object(built_lib):

@@ -19,7 +19,8 @@ VVSTREAM = [0, 1, 2, 3, 4, 28, 36, 60]  # 0/1 byte split U4/U8, 2/3 count split,
 def ctx(built_lib):
     import tcpck
     assert torch.cuda.is_available()
-    c = tcpck.Context(0)
+    from conftest import RoutedContext
+    c = RoutedContext(0)  # libtcpck.so; measurement-only variants on libtcpck_probe.so
     yield c
     c.close()
 

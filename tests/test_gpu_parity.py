@@ -22,7 +22,8 @@ torch = pytest.importorskip("torch")
 def ctx(built_lib):
     import tcpck
     assert torch.cuda.is_available(), "gpu tests need a GPU"
-    c = tcpck.Context(0)
+    from conftest import RoutedContext
+    c = RoutedContext(0)  # libtcpck.so; measurement-only variants on libtcpck_probe.so
     yield c
     c.close()
 

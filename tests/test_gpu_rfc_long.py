@@ -23,7 +23,8 @@ LONG = 300000
 def ctx(built_lib):
     import tcpck
     assert torch.cuda.is_available(), "gpu tests need a GPU"
-    c = tcpck.Context(0)
+    from conftest import RoutedContext
+    c = RoutedContext(0)  # libtcpck.so; measurement-only variants on libtcpck_probe.so
     yield c
     c.close()
 
@@ -105,7 +106,8 @@ def test_rfc_long_image_explicit_kernel(ctx, oracle_c, kernel, gap, op):
     a, off, ln = batch(4000, 1492, (5, 3999), gap, seed=7 + gap)
     n = ln.size
     out = torch.zeros(n, dtype=torch.uint8 if op == tcpck.OP_VERIFY else torch.int16, device="cuda")
-    ctx.batch_var_ex(op, dev(a), dev(off), dev(ln), n, out, getattr(tcpck, f"KERNEL_{kernel}"), 0,
+    ctx.batch_var_ex(op, dev(a), dev(off), dev(ln), n, out, getattr(tcpck, f"KERNEL_{kernel}"),
+                     4 if kernel == "VVSTREAM" else 0,  # the policy variants (libtcpck.so)
                      mode=tcpck.MODE_RFC1071, total_bytes=int(ln.astype(np.int64).sum()), min_len=1492,
                      max_len=1492, packed=gap == 0, sorted=True)
     exp = oracle_c.batch(a, off, ln, mode=1, threads=8)

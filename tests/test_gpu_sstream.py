@@ -19,7 +19,8 @@ VARIANTS = [0, 1, 2, 5, 10]  # 0 policy, 1 U4, 2 U8; +4 default block order, +8 
 def ctx(built_lib):
     import tcpck
     assert torch.cuda.is_available()
-    c = tcpck.Context(0)
+    from conftest import RoutedContext
+    c = RoutedContext(0)  # libtcpck.so; measurement-only variants on libtcpck_probe.so
     yield c
     c.close()
 
