@@ -221,6 +221,7 @@ constexpr int kSegXcdOrder = 1 << 24;    // seg: XCD-chunked order
 constexpr uint64_t kFillKeepMaxLen = 448;
 constexpr int kVvKeep = 32;              // vvstream: kFill reads with the default policy
 constexpr int kSstreamHdrStream = 32;    // sstream RECEIVE: headers from the stream's registers
+constexpr uint64_t kHdrStreamMaxLen = 256;  // ... for (typical) images up to this length
 
 // Packed fixed images above 4 KiB: seg's W-wave shapes stream W KiB of an
 // image per step (shape_for_len: W = 2, 4, 8, 16 up to 8, 16, 32, 64 KiB), so
@@ -333,12 +334,15 @@ hipError_t run_fixed_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint
       param = kRstreamPolicy;
     }
   }
-  // RECEIVE into a header array: where the VERIFY kernel is sstream, it emits
-  // each image's host-order header from the stream's registers (the header
-  // bytes read once, DESIGN.md "Receive path"); elsewhere the header pass
-  // follows the VERIFY pass
-  if (auto_pick && op == TCPCK_OP_RECEIVE && hdr && kernel == TCPCK_KERNEL_SSTREAM) param |= kSstreamHdrStream;
-  const bool fuse_hdr = op == TCPCK_OP_RECEIVE && hdr && (!auto_pick || kernel == TCPCK_KERNEL_SSTREAM) &&
+  // RECEIVE into a header array: for small images in slots sstream emits each
+  // host-order header from the stream's registers (one launch, the header
+  // bytes read once); elsewhere the header pass follows the VERIFY pass, which
+  // measured faster than any fused form for MSS-sized images (header stores
+  // inside the read stream cost more than a separate pass: DESIGN.md "Receive
+  // path", profiles/r03/receive_fused_probe.log)
+  if (auto_pick && op == TCPCK_OP_RECEIVE && hdr && kernel == TCPCK_KERNEL_SSTREAM && len <= kHdrStreamMaxLen)
+    param |= kSstreamHdrStream;
+  const bool fuse_hdr = op == TCPCK_OP_RECEIVE && hdr && (!auto_pick || (param & kSstreamHdrStream)) &&
                         !(param & TCPCK_PARAM_RECEIVE_TWO_PASS);
   if (op == TCPCK_OP_RECEIVE) op = TCPCK_OP_VERIFY;  // the header pass follows (run_fixed)
   // FILL on rstream with a results buffer: the stream writes only the results,
@@ -523,7 +527,7 @@ hipError_t run_var_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const 
       // (41-58 % either way: the scattered field writes bound it)
       kernel = TCPCK_KERNEL_SSTREAM;
       param = 0;
-      if (op == TCPCK_OP_RECEIVE && hdr) {
+      if (op == TCPCK_OP_RECEIVE && hdr && typical <= kHdrStreamMaxLen) {
         fuse_small = true;
         param = kSstreamHdrStream;
       }
@@ -536,8 +540,10 @@ hipError_t run_var_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const 
       param = kVvPolicy | (op == TCPCK_OP_FILL && typical <= kFillKeepMaxLen ? kVvKeep : 0);
     }
   }
-  // RECEIVE into a header array (as run_fixed_impl): sstream emits the
-  // headers from its stream; other kernels are followed by the header pass
+  // RECEIVE into a header array (as run_fixed_impl): on rings of small images
+  // sstream emits the headers from its stream (4M 32-254-B datagrams in 256-B
+  // slots: 190 us against 259 with the header pass, 235 with the run's
+  // headers re-read after its verdicts); otherwise the header pass follows
   bool fuse_hdr = op == TCPCK_OP_RECEIVE && hdr && !(param & TCPCK_PARAM_RECEIVE_TWO_PASS) &&
                   (!auto_pick || fuse_small);
   if (op == TCPCK_OP_RECEIVE) op = TCPCK_OP_VERIFY;  // the header pass follows (run_var)
