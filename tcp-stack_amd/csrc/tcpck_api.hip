@@ -222,6 +222,15 @@ constexpr uint64_t kFillKeepMaxLen = 448;
 constexpr int kVvKeep = 32;              // vvstream: kFill reads with the default policy
 constexpr int kSstreamHdrStream = 32;    // sstream RECEIVE: headers from the stream's registers
 constexpr uint64_t kHdrStreamMaxLen = 256;  // ... for (typical) images up to this length
+// RECEIVE with an explicit kernel: the probe build fuses the headers into any
+// kernel that can (sstream's after-the-run conversion, HDR 1); the product
+// carries only the stream-register form (+ kSstreamHdrStream) and otherwise
+// runs the header pass
+#ifdef TCPCK_PROBE
+constexpr bool kFuseAnyHdr = true;
+#else
+constexpr bool kFuseAnyHdr = false;
+#endif
 
 // Packed fixed images above 4 KiB: seg's W-wave shapes stream W KiB of an
 // image per step (shape_for_len: W = 2, 4, 8, 16 up to 8, 16, 32, 64 KiB), so
@@ -342,7 +351,7 @@ hipError_t run_fixed_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint
   // path", profiles/r03/receive_fused_probe.log)
   if (auto_pick && op == TCPCK_OP_RECEIVE && hdr && kernel == TCPCK_KERNEL_SSTREAM && len <= kHdrStreamMaxLen)
     param |= kSstreamHdrStream;
-  const bool fuse_hdr = op == TCPCK_OP_RECEIVE && hdr && (!auto_pick || (param & kSstreamHdrStream)) &&
+  const bool fuse_hdr = op == TCPCK_OP_RECEIVE && hdr && ((kFuseAnyHdr && !auto_pick) || (param & kSstreamHdrStream)) &&
                         !(param & TCPCK_PARAM_RECEIVE_TWO_PASS);
   if (op == TCPCK_OP_RECEIVE) op = TCPCK_OP_VERIFY;  // the header pass follows (run_fixed)
   // FILL on rstream with a results buffer: the stream writes only the results,
@@ -545,7 +554,7 @@ hipError_t run_var_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const 
   // slots: 190 us against 259 with the header pass, 235 with the run's
   // headers re-read after its verdicts); otherwise the header pass follows
   bool fuse_hdr = op == TCPCK_OP_RECEIVE && hdr && !(param & TCPCK_PARAM_RECEIVE_TWO_PASS) &&
-                  (!auto_pick || fuse_small);
+                  ((kFuseAnyHdr && !auto_pick) || fuse_small || (param & kSstreamHdrStream));
   if (op == TCPCK_OP_RECEIVE) op = TCPCK_OP_VERIFY;  // the header pass follows (run_var)
   if (kernel == TCPCK_KERNEL_VVSTREAM) {
     if (mode != TCPCK_MODE_REF && (param & 32)) return hipErrorInvalidValue;
