@@ -13,6 +13,12 @@
 extern "C" {
 #endif
 
+/* tcpck_batch_fixed_ex kernel id: FILL's deferred field pass ALONE
+ * (launch_patch_fields) -- each field's 64-B block read and written back whole
+ * with d_out[k] (u16) patched in; no checksum is computed.  For timing the
+ * pass apart from the stream (scripts/fill_drain_probe.py). */
+#define TCPCK_KERNEL_PATCH 12
+
 /* Device buffer of 4 x u64 per wave receiving {start, end} s_memrealtime
  * (100 MHz) stamps, HW_ID and XCC_ID from the rstream variants built with
  * stamps (3, 7; NULL = off). */

@@ -461,6 +461,18 @@ bool fill_by_update(int op, int mode, const void *out, int kernel, int param, bo
 hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t stride, uint32_t len,
                      uint64_t count, void *out, int kernel, int param, hipStream_t s, uint8_t *hdr = nullptr) {
   bool patch = false;
+#ifdef TCPCK_PROBE
+  if (kernel == TCPCK_KERNEL_PATCH) {  // the deferred field pass alone (timing)
+    if (op != TCPCK_OP_FILL || !out || stride < 64) return hipErrorInvalidValue;
+    tcpck::PatchArgs pa{};
+    pa.arena = arena;
+    pa.stride = stride;
+    pa.count = count;
+    pa.sums = static_cast<uint16_t *>(out);
+    pa.hi = (count - 1) * stride + len;
+    return tcpck::launch_patch_fields(pa, static_cast<uint32_t>(ctx->num_cus), s);
+  }
+#endif
   if (stride >= 64 && fill_by_update(op, mode, out, kernel, param, true, stride, len)) {
     const int p = param & ~(TCPCK_PARAM_FILL_UPDATE | TCPCK_PARAM_FILL_INSTREAM);
     const hipError_t e = run_fixed_impl(ctx, TCPCK_OP_CHECKSUM, mode, arena, stride, len, count, out, kernel, p, s,
