@@ -16,7 +16,8 @@ extern "C" {
 /* tcpck_batch_fixed_ex kernel id: FILL's deferred field pass ALONE
  * (launch_patch_fields) -- each field's 64-B block read and written back whole
  * with d_out[k] (u16) patched in; no checksum is computed.  For timing the
- * pass apart from the stream (scripts/fill_drain_probe.py). */
+ * pass apart from the stream (scripts/fill_drain_probe.py).  param = 1 + the
+ * block stores' cache bits (sc0 1 | nt 2 | sc1 4), 0 = a plain store. */
 #define TCPCK_KERNEL_PATCH 12
 
 /* Device buffer of 4 x u64 per wave receiving {start, end} s_memrealtime

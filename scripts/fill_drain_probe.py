@@ -13,6 +13,8 @@ pause so scripts/fill_drain_summary.py can cut the kernel trace:
   stream+sleepS  control: CHECKSUM + the same spin
   patch          the block pass alone (TCPCK_KERNEL_PATCH, tcpck_probe.h)
   instream       FILL with the 2-B field stores inside the stream (rstream 20)
+  spB            CHECKSUM stream, then the block pass alone with its stores'
+                 cache bits B - 1 (sc0 1 | nt 2 | sc1 4; sp0: plain C++ store)
 
 Run under `rocprofv3 --kernel-trace` (per-kernel durations) and, separately,
 `--pmc FETCH_SIZE` / `--pmc WRITE_SIZE` (where the field writes leave L2)."""
@@ -60,6 +62,12 @@ def main():
             f = lambda: ctx.batch_fixed(tcpck.OP_FILL, arena, L, L, n, out, stream=s)
         elif base == "patch":
             f = lambda: ctx.batch_fixed_ex(tcpck.OP_FILL, arena, L, L, n, out, tcpck.KERNEL_PATCH, 0, stream=s)
+        elif base.startswith("sp"):  # stream, then the block pass with store bits (sp0 plain, spB: 1 + bits)
+            bits = int(base[2:])
+
+            def f():
+                ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, arena, L, L, n, out, R, 20, stream=s)
+                ctx.batch_fixed_ex(tcpck.OP_FILL, arena, L, L, n, out, tcpck.KERNEL_PATCH, bits, stream=s)
         elif base == "instream":
             f = lambda: ctx.batch_fixed_ex(tcpck.OP_FILL, arena, L, L, n, out, R, 20, stream=s)
         else:

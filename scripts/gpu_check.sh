@@ -123,6 +123,7 @@ for s in ${STEPS:-tests smoke bench prof}; do
     fdrain) step fdrain 300 rocprofv3 --kernel-trace -d gpurun_out/fdrain -o run --output-format csv -- python3 scripts/fill_drain_probe.py &&
       step fdrain_w 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d gpurun_out/fdrain_w -o run --output-format csv -- python3 scripts/fill_drain_probe.py --phases stream,fill,patch,instream --steps 10 &&
       step fdrain_f 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d gpurun_out/fdrain_f -o run --output-format csv -- python3 scripts/fill_drain_probe.py --phases stream,fill,patch,instream --steps 10 ;;
+    fpol) step fpol 300 rocprofv3 --kernel-trace -d gpurun_out/fpol -o run --output-format csv -- python3 scripts/fill_drain_probe.py --phases stream,sp0,sp1,sp2,sp3,sp4,sp5,sp6,sp7,sp8,fill ;;
     rtests) step rtests 900 python -u -m pytest tests/test_gpu_receive.py tests/test_gpu_rfc_long.py -x -q --timeout 300 --timeout-method thread ;;
     tests_new) step tests_new 900 python -u -m pytest tests/test_gpu_c5.py tests/test_gpu_multi_ctx.py tests/test_drop_in.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
     bench_receive) step bench_receive 600 python bench.py --config receive ;;

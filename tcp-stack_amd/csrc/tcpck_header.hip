@@ -73,7 +73,32 @@ hipError_t launch_one(const HeaderArgs &a, uint32_t num_cus, hipStream_t s) {
 // FILL's field stores after the stream (PatchArgs): 4 lanes per image, lane j
 // owns 16 B of the 64-B block around the field; whole-block write-backs instead
 // of a masked 2-B write per image.
-template <bool VAR, bool UPDATE>
+// 16-B global store with explicit cache-policy bits (probe builds, timing the
+// field pass's write path): BITS = sc0 1 | nt 2 | sc1 4, -1 = a plain C++ store
+template <int BITS>
+__device__ __forceinline__ void store_block(dev::u32x4 *p, dev::u32x4 v) {
+  if constexpr (BITS < 0) {
+    *p = v;
+  } else if constexpr (BITS == 0) {
+    asm volatile("global_store_dwordx4 %0, %1, off" ::"v"(p), "v"(v) : "memory");
+  } else if constexpr (BITS == 1) {
+    asm volatile("global_store_dwordx4 %0, %1, off sc0" ::"v"(p), "v"(v) : "memory");
+  } else if constexpr (BITS == 2) {
+    asm volatile("global_store_dwordx4 %0, %1, off nt" ::"v"(p), "v"(v) : "memory");
+  } else if constexpr (BITS == 3) {
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 nt" ::"v"(p), "v"(v) : "memory");
+  } else if constexpr (BITS == 4) {
+    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+  } else if constexpr (BITS == 5) {
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
+  } else if constexpr (BITS == 6) {
+    asm volatile("global_store_dwordx4 %0, %1, off sc1 nt" ::"v"(p), "v"(v) : "memory");
+  } else {
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt" ::"v"(p), "v"(v) : "memory");
+  }
+}
+
+template <bool VAR, bool UPDATE, int BITS = -1>
 __global__ void __launch_bounds__(kBlock) patch_fields_kernel(PatchArgs a) {
   const uint64_t step = static_cast<uint64_t>(gridDim.x) * kBlock;
   const uint64_t total = a.count * 4;
@@ -132,18 +157,18 @@ __global__ void __launch_bounds__(kBlock) patch_fields_kernel(PatchArgs a) {
       v.z = di == 2 ? (v.z & m) | x : v.z;
       v.w = di == 3 ? (v.w & m) | x : v.w;
     }
-    *p = v;
+    store_block<BITS>(p, v);
   }
 }
 
-template <bool VAR, bool UPDATE>
+template <bool VAR, bool UPDATE, int BITS = -1>
 hipError_t launch_patch(const PatchArgs &a, uint32_t num_cus, hipStream_t stream) {
-  static const uint32_t per_cu = dev::resident_blocks_per_cu(patch_fields_kernel<VAR, UPDATE>);
+  static const uint32_t per_cu = dev::resident_blocks_per_cu(patch_fields_kernel<VAR, UPDATE, BITS>);
   uint64_t blocks = (a.count * 4 + kBlock - 1) / kBlock;
   const uint64_t cap = static_cast<uint64_t>(per_cu) * num_cus * 8;
   if (blocks > cap) blocks = cap;
-  hipLaunchKernelGGL((patch_fields_kernel<VAR, UPDATE>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0, stream,
-                     a);
+  hipLaunchKernelGGL((patch_fields_kernel<VAR, UPDATE, BITS>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0,
+                     stream, a);
   return hipGetLastError();
 }
 
@@ -157,6 +182,21 @@ hipError_t launch_patch_fields(const PatchArgs &a, uint32_t num_cus, hipStream_t
     return a.update ? launch_patch<true, true>(a, num_cus, stream) : launch_patch<true, false>(a, num_cus, stream);
   }
   if (a.stride < 64) return hipErrorInvalidValue;  // two fields could share a block
+#ifdef TCPCK_PROBE
+  if (a.store_bits && !a.update) {  // timing: the block stores with explicit cache bits
+    switch (a.store_bits - 1) {
+      case 0: return launch_patch<false, false, 0>(a, num_cus, stream);
+      case 1: return launch_patch<false, false, 1>(a, num_cus, stream);
+      case 2: return launch_patch<false, false, 2>(a, num_cus, stream);
+      case 3: return launch_patch<false, false, 3>(a, num_cus, stream);
+      case 4: return launch_patch<false, false, 4>(a, num_cus, stream);
+      case 5: return launch_patch<false, false, 5>(a, num_cus, stream);
+      case 6: return launch_patch<false, false, 6>(a, num_cus, stream);
+      case 7: return launch_patch<false, false, 7>(a, num_cus, stream);
+      default: return hipErrorInvalidValue;
+    }
+  }
+#endif
   return a.update ? launch_patch<false, true>(a, num_cus, stream) : launch_patch<false, false>(a, num_cus, stream);
 }
 

@@ -189,6 +189,7 @@ struct PatchArgs {
   uint64_t lo, hi;          // fixed: byte range (relative to arena) the block writes may cover
   uint32_t update;          // 1: sums hold CHECKSUM results, derive FILL's from the old field
   uint32_t packed;          // offset lists: the PACKED contract holds
+  uint32_t store_bits;      // probe builds: 1 + the block stores' cache bits (sc0 1, nt 2, sc1 4), 0 = plain
 };
 hipError_t launch_patch_fields(const PatchArgs &a, uint32_t num_cus, hipStream_t stream);
 
