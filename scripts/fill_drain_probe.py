@@ -68,6 +68,15 @@ def main():
             def f():
                 ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, arena, L, L, n, out, R, 20, stream=s)
                 ctx.batch_fixed_ex(tcpck.OP_FILL, arena, L, L, n, out, tcpck.KERNEL_PATCH, bits, stream=s)
+        elif base.startswith("sg"):  # stream, then the probe pass: sgG_B (granularity G, bits B - 1)
+            g, b = base[2:].split("_")
+            prm = (int(g) << 4) | int(b)
+
+            def f():
+                ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, arena, L, L, n, out, R, 20, stream=s)
+                ctx.batch_fixed_ex(tcpck.OP_FILL, arena, L, L, n, out, tcpck.KERNEL_PATCH, prm, stream=s)
+        elif base == "instream26":  # in-stream 2-B field stores, sc0 sc1 nt
+            f = lambda: ctx.batch_fixed_ex(tcpck.OP_FILL, arena, L, L, n, out, R, 26, stream=s)
         elif base == "instream":
             f = lambda: ctx.batch_fixed_ex(tcpck.OP_FILL, arena, L, L, n, out, R, 20, stream=s)
         else:

@@ -161,6 +161,68 @@ __global__ void __launch_bounds__(kBlock) patch_fields_kernel(PatchArgs a) {
   }
 }
 
+#ifdef TCPCK_PROBE
+// Timing only: FILL's field stores after the stream at other granularities,
+// fixed strides, BITS as store_block.  GRAN 1: one lane per image, the 16-B
+// chunk holding the field read and written back; 2: the 2-B field alone (no
+// read); 3: eight lanes per image, the field's whole 128-B line.
+template <int GRAN, int BITS>
+__global__ void __launch_bounds__(kBlock) patch_probe_kernel(PatchArgs a) {
+  constexpr int LPI = GRAN == 3 ? 8 : 1;  // lanes per image
+  const uint64_t step = static_cast<uint64_t>(gridDim.x) * kBlock;
+  const uint64_t total = a.count * LPI;
+  const uint64_t base = reinterpret_cast<uint64_t>(a.arena);
+  for (uint64_t t = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x; t < total; t += step) {
+    const uint64_t k = t / LPI;
+    const uint32_t j = static_cast<uint32_t>(t % LPI);
+    const uint64_t f = k * a.stride + 28;
+    const uint16_t c = a.sums[k];
+    if constexpr (GRAN == 2) {
+      uint16_t *p = reinterpret_cast<uint16_t *>(a.arena + f);
+      const uint32_t v = c;
+      if constexpr (BITS == 7)
+        asm volatile("global_store_short %0, %1, off sc0 sc1 nt" ::"v"(p), "v"(v) : "memory");
+      else if constexpr (BITS == 6)
+        asm volatile("global_store_short %0, %1, off sc1 nt" ::"v"(p), "v"(v) : "memory");
+      else
+        *p = c;
+    } else {
+      const uint64_t gm = GRAN == 3 ? 127 : 15;
+      const uint64_t blk = ((base + f) & ~gm) - base;
+      if (GRAN == 3 && (base + blk < base + a.lo || blk + 128 > a.hi)) {
+        if (j == 0) *reinterpret_cast<uint16_t *>(a.arena + f) = c;
+        continue;
+      }
+      dev::u32x4 *p = reinterpret_cast<dev::u32x4 *>(a.arena + blk) + j;
+      dev::u32x4 v = *p;
+      const uint32_t r = static_cast<uint32_t>(f - blk) - 16 * j;
+      if (r < 16) {
+        const uint32_t sh = 16 * ((r >> 1) & 1);
+        const uint32_t di = r >> 2;
+        const uint32_t m = ~(0xFFFFu << sh), x = static_cast<uint32_t>(c) << sh;
+        v.x = di == 0 ? (v.x & m) | x : v.x;
+        v.y = di == 1 ? (v.y & m) | x : v.y;
+        v.z = di == 2 ? (v.z & m) | x : v.z;
+        v.w = di == 3 ? (v.w & m) | x : v.w;
+      }
+      store_block<BITS>(p, v);
+    }
+  }
+}
+
+template <int GRAN, int BITS>
+hipError_t launch_patch_probe(const PatchArgs &a, uint32_t num_cus, hipStream_t stream) {
+  static const uint32_t per_cu = dev::resident_blocks_per_cu(patch_probe_kernel<GRAN, BITS>);
+  const uint64_t lpi = GRAN == 3 ? 8 : 1;
+  uint64_t blocks = (a.count * lpi + kBlock - 1) / kBlock;
+  const uint64_t cap = static_cast<uint64_t>(per_cu) * num_cus * 8;
+  if (blocks > cap) blocks = cap;
+  hipLaunchKernelGGL((patch_probe_kernel<GRAN, BITS>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0, stream,
+                     a);
+  return hipGetLastError();
+}
+#endif
+
 template <bool VAR, bool UPDATE, int BITS = -1>
 hipError_t launch_patch(const PatchArgs &a, uint32_t num_cus, hipStream_t stream) {
   static const uint32_t per_cu = dev::resident_blocks_per_cu(patch_fields_kernel<VAR, UPDATE, BITS>);
@@ -183,6 +245,15 @@ hipError_t launch_patch_fields(const PatchArgs &a, uint32_t num_cus, hipStream_t
   }
   if (a.stride < 64) return hipErrorInvalidValue;  // two fields could share a block
 #ifdef TCPCK_PROBE
+  if (a.store_bits >= 16 && !a.update) {  // timing: other granularities (store_bits >> 4), bits 6 / 7 / plain
+    const int gran = static_cast<int>(a.store_bits >> 4), bits = static_cast<int>(a.store_bits & 15) - 1;
+    if (gran == 1) return bits == 7 ? launch_patch_probe<1, 7>(a, num_cus, stream) : launch_patch_probe<1, -1>(a, num_cus, stream);
+    if (gran == 2) return bits == 7 ? launch_patch_probe<2, 7>(a, num_cus, stream)
+                                    : (bits == 6 ? launch_patch_probe<2, 6>(a, num_cus, stream)
+                                                 : launch_patch_probe<2, -1>(a, num_cus, stream));
+    if (gran == 3) return bits == 7 ? launch_patch_probe<3, 7>(a, num_cus, stream) : launch_patch_probe<3, -1>(a, num_cus, stream);
+    return hipErrorInvalidValue;
+  }
   if (a.store_bits && !a.update) {  // timing: the block stores with explicit cache bits
     switch (a.store_bits - 1) {
       case 0: return launch_patch<false, false, 0>(a, num_cus, stream);

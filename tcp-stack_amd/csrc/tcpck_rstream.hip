@@ -131,8 +131,12 @@ __global__ void __launch_bounds__(kBlock) rstream_kernel(FixedStreamArgs a) {
         static_cast<uint8_t *>(a.out)[k] = (c == 0) ? 1 : 0;
       } else {
         if (a.out) static_cast<uint16_t *>(a.out)[k] = c;
-        if (OP == kFill && !a.defer_field)
-          dev::store16_field(rsrc, (out_rel + lane) * S + lead + 28, c);  // tcp-header.h:177
+        if (OP == kFill && !a.defer_field) {
+          if constexpr (FLAV & 16)  // write-through streaming store (sc0 sc1 nt): not left dirty in the MALL
+            __builtin_amdgcn_raw_buffer_store_b16(c, rsrc, static_cast<int>((out_rel + lane) * S + lead + 28), 0, 19);
+          else
+            dev::store16_field(rsrc, (out_rel + lane) * S + lead + 28, c);  // tcp-header.h:177
+        }
       }
     }
   };
@@ -293,6 +297,11 @@ hipError_t launch_rstream(int op, int variant, const FixedStreamArgs &a, uint32_
       FixedStreamArgs b = a;
       b.order = 4u;
       return dispatch<4, false, 0, 11>(op, b, num_cus, stream);
+    }
+    case 26: {  // 20 with the FILL field stores write-through streaming (sc0 sc1 nt, FLAV bit 4)
+      FixedStreamArgs b = a;
+      b.order = 4u;
+      return dispatch<4, false, 0, 23>(op, b, num_cus, stream);
     }
     case 23: case 24: {  // 20 with 8 (23) or 2 (24) steps in flight
       FixedStreamArgs b = a;
