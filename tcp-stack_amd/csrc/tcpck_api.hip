@@ -209,7 +209,7 @@ constexpr uint64_t kFixedRunMaxLen = 4096;   // packed fixed: rstream up to here
 // profiles/r01/oversub_c5_first_step.log, split_probe.log); vvstream the
 // same with runs >= 8 KiB (C3 86.3 -> 89.5%, profiles/r01/xcd_first_step_probe.log).
 constexpr int kRstreamPolicy = 20;       // v_dot2 sums, buffer loads, XCD-chunked order, L2-kept first step
-constexpr int kRstreamDeferFill = 25;    // FILL: kRstreamPolicy's stream to out, then the 64-B block patch pass
+constexpr int kRstreamDeferFill = 25;    // FILL: kRstreamPolicy's stream to out, then the 2-B write-through field pass
 constexpr int kVvPolicy = 4 | 8 | 16;    // size policy, XCD-chunked order, L2-kept first step
 constexpr int kSegXcdOrder = 1 << 24;    // seg: XCD-chunked order
 // FILL of small images: nearly every line holds a checksum field, so the
@@ -220,6 +220,12 @@ constexpr int kSegXcdOrder = 1 << 24;    // seg: XCD-chunked order
 // 480 B +0.6 %, the C3 mix -3.7 %: bytes per image up to 448)
 constexpr uint64_t kFillKeepMaxLen = 448;
 constexpr int kVvKeep = 32;              // vvstream: kFill reads with the default policy
+constexpr int kVvDeferFill = 64;         // vvstream: kFill writes the results only, the field pass follows
+// FILL with a results buffer on the run kernels: the stream writes only the
+// results and the write-through field pass stores the fields, for (typical)
+// images of at least this many bytes; smaller images pay more for 1M-per-
+// 38-us scattered field stores than the in-stream stores cost them
+constexpr uint64_t kDeferFillMinLen = 512;
 constexpr int kSstreamHdrStream = 32;    // sstream RECEIVE: headers from the stream's registers
 constexpr uint64_t kHdrStreamMaxLen = 256;  // ... for (typical) images up to this length
 // RECEIVE with an explicit kernel: the probe build fuses the headers into any
@@ -355,10 +361,12 @@ hipError_t run_fixed_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint
                         !(param & TCPCK_PARAM_RECEIVE_TWO_PASS);
   if (op == TCPCK_OP_RECEIVE) op = TCPCK_OP_VERIFY;  // the header pass follows (run_fixed)
   // FILL on rstream with a results buffer: the stream writes only the results,
-  // then a second pass rewrites each field's 64-B block whole -- never slower
-  // than the in-stream 2-B stores, 4-8 % faster at 512-768 B and 2.5-4 KiB
-  // (scripts/fill_defer_probe.py, profiles/r02/fill_defer_probe{,2}.log)
-  if (auto_pick && kernel == TCPCK_KERNEL_RSTREAM && op == TCPCK_OP_FILL && out && stride >= 64 &&
+  // then a second pass stores each field with a write-through 2-B store.
+  // Scattered field stores inside a read stream, or left dirty in the
+  // Infinity Cache for the next stream to write back, cost ~70 us per 1M
+  // images; written through to HBM in their own pass they cost 38 us (C2:
+  // 280 -> 248 us, scripts/fill_drain_probe.py, profiles/r03/fill_*.log)
+  if (auto_pick && kernel == TCPCK_KERNEL_RSTREAM && op == TCPCK_OP_FILL && out && stride >= 30 &&
       (param & 0xFF) == kRstreamPolicy)
     param = (param & ~0xFF) | kRstreamDeferFill;
   if (kernel == TCPCK_KERNEL_RSTREAM) {
@@ -375,7 +383,7 @@ hipError_t run_fixed_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint
     a.oversub = static_cast<uint32_t>(param >> 16) & 0xFFu;
     int variant = param & 0xFF;
     if (variant == kRstreamDeferFill) {  // FILL: the policy's stream, the fields in a second pass
-      if (op != TCPCK_OP_FILL || !out || stride < 64) return hipErrorInvalidValue;
+      if (op != TCPCK_OP_FILL || !out || stride < 30) return hipErrorInvalidValue;
       a.defer_field = 1;
       *patch = true;
       variant = kRstreamPolicy;
@@ -413,6 +421,8 @@ hipError_t run_fixed_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint
   }
   if (kernel == TCPCK_KERNEL_VVSTREAM) {  // any even length: the prefix table takes any number of ends per step
     if (len == 0 || stride > (1u << 24) || (op == TCPCK_OP_FILL && len < 30)) return hipErrorInvalidValue;
+    if (auto_pick && op == TCPCK_OP_FILL && out && len >= kDeferFillMinLen) param |= kVvDeferFill;
+    if (param & kVvDeferFill) *patch = true;
     if (mode != TCPCK_MODE_REF && (len >= (1u << 17) || (param & 32))) return hipErrorInvalidValue;
     tcpck::RunArgs a{};
     a.mode = mode == TCPCK_MODE_REF ? tcpck::kRef : tcpck::kRfc1071;
@@ -463,7 +473,7 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
   bool patch = false;
 #ifdef TCPCK_PROBE
   if (kernel == TCPCK_KERNEL_PATCH) {  // the deferred field pass alone (timing)
-    if (op != TCPCK_OP_FILL || !out || stride < 64) return hipErrorInvalidValue;
+    if (op != TCPCK_OP_FILL || !out || stride < 30) return hipErrorInvalidValue;
     tcpck::PatchArgs pa{};
     pa.arena = arena;
     pa.stride = stride;
@@ -474,7 +484,7 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
     return tcpck::launch_patch_fields(pa, static_cast<uint32_t>(ctx->num_cus), s);
   }
 #endif
-  if (stride >= 64 && fill_by_update(op, mode, out, kernel, param, true, stride, len)) {
+  if (stride >= 30 && fill_by_update(op, mode, out, kernel, param, true, stride, len)) {
     const int p = param & ~(TCPCK_PARAM_FILL_UPDATE | TCPCK_PARAM_FILL_INSTREAM);
     const hipError_t e = run_fixed_impl(ctx, TCPCK_OP_CHECKSUM, mode, arena, stride, len, count, out, kernel, p, s,
                                         &patch);
@@ -515,7 +525,7 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
 
 hipError_t run_var_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const uint64_t *off, const uint32_t *len,
                         uint64_t base, uint64_t count, void *out, const tcpck_layout *layout, int kernel, int param,
-                        hipStream_t s, uint8_t *hdr = nullptr, bool *hdr_done = nullptr) {
+                        hipStream_t s, uint8_t *hdr = nullptr, bool *hdr_done = nullptr, bool *patch = nullptr) {
   const uint64_t typical = (layout && layout->total_bytes) ? layout->total_bytes / count : 1500;
   const bool packed = mode == TCPCK_MODE_REF && layout && (layout->flags & TCPCK_LAYOUT_PACKED);
   bool fuse_small = false;  // RECEIVE into a header array on a ring of small datagrams (below)
@@ -571,6 +581,11 @@ hipError_t run_var_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const 
   if (op == TCPCK_OP_RECEIVE) op = TCPCK_OP_VERIFY;  // the header pass follows (run_var)
   if (kernel == TCPCK_KERNEL_VVSTREAM) {
     if (mode != TCPCK_MODE_REF && (param & 32)) return hipErrorInvalidValue;
+    if (auto_pick && op == TCPCK_OP_FILL && out && patch && typical >= kDeferFillMinLen) param |= kVvDeferFill;
+    if (param & kVvDeferFill) {
+      if (!patch) return hipErrorInvalidValue;
+      *patch = true;
+    }
     tcpck::RunArgs a{};
     a.mode = mode == TCPCK_MODE_REF ? tcpck::kRef : tcpck::kRfc1071;
     a.arena = arena;
@@ -636,10 +651,21 @@ hipError_t run_var(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const uint6
     return tcpck::launch_patch_fields(pa, static_cast<uint32_t>(ctx->num_cus), s);
   }
   param &= ~(TCPCK_PARAM_FILL_UPDATE | TCPCK_PARAM_FILL_INSTREAM);
-  bool hdr_done = false;
+  bool hdr_done = false, patch = false;
   const hipError_t e =
-      run_var_impl(ctx, op, mode, arena, off, len, base, count, out, layout, kernel, param, s, hdr, &hdr_done);
-  if (e != hipSuccess || op != TCPCK_OP_RECEIVE || hdr_done) return e;
+      run_var_impl(ctx, op, mode, arena, off, len, base, count, out, layout, kernel, param, s, hdr, &hdr_done, &patch);
+  if (e != hipSuccess) return e;
+  if (patch) {  // the fields the stream left: write-through 2-B stores (launch_patch_fields)
+    tcpck::PatchArgs pa{};
+    pa.arena = arena;
+    pa.offsets = off;
+    pa.lengths = len;
+    pa.base = base;
+    pa.count = count;
+    pa.sums = static_cast<uint16_t *>(out);
+    return tcpck::launch_patch_fields(pa, static_cast<uint32_t>(ctx->num_cus), s);
+  }
+  if (op != TCPCK_OP_RECEIVE || hdr_done) return e;
   tcpck::HeaderArgs h{};
   h.arena = arena;
   h.offsets = off;

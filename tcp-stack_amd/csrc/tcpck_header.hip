@@ -70,11 +70,66 @@ hipError_t launch_one(const HeaderArgs &a, uint32_t num_cus, hipStream_t s) {
   return hipGetLastError();
 }
 
-// FILL's field stores after the stream (PatchArgs): 4 lanes per image, lane j
-// owns 16 B of the 64-B block around the field; whole-block write-backs instead
-// of a masked 2-B write per image.
-// 16-B global store with explicit cache-policy bits (probe builds, timing the
-// field pass's write path): BITS = sc0 1 | nt 2 | sc1 4, -1 = a plain C++ store
+// ---- FILL's field stores after the stream (PatchArgs) ----------------------
+//
+// One lane per image stores the 2-B checksum into bytes 28-29 as a
+// write-through streaming store (global_store_short sc0 sc1 nt): nothing but
+// the field is read or written.  The store policy is what matters here
+// (scripts/fill_drain_probe.py, profiles/r03/fill_store_policy.log): a plain,
+// sc0, sc1 or nt store leaves its line dirty in the memory-side Infinity Cache
+// (MALL) and the next read stream pays for the 1M scattered write-backs -- C2's
+// stream then ran 244 us instead of 209 us, even with 100 us of idle GPU
+// between the passes; with sc1 nt / sc0 sc1 nt the pass writes HBM itself (38
+// us for 1M 2-B stores, 44 us for 64-B blocks) and the next stream runs at
+// 209 us: AUTO's C2 FILL 280 -> 248 us.
+__device__ __forceinline__ void store16_through(uint8_t *p, uint16_t c) {
+  const uint32_t v = c;
+  asm volatile("global_store_short %0, %1, off sc0 sc1 nt" ::"v"(p), "v"(v) : "memory");
+}
+
+// UPDATE: sums[k] is image k's CHECKSUM with its field in; the zero-field
+// checksum follows from the old field f, c = ~(~C - f) mod 2^16, and goes to
+// the field and back to sums[k].  Images < 30 B keep their plain checksum and
+// are not written (seg's FILL does the same).
+template <bool VAR, bool UPDATE>
+__global__ void __launch_bounds__(kBlock) patch_fields_kernel(PatchArgs a) {
+  const uint64_t step = static_cast<uint64_t>(gridDim.x) * kBlock;
+  for (uint64_t k = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x; k < a.count; k += step) {
+    uint64_t f;  // the field, relative to arena
+    if constexpr (VAR) {
+      if (a.lengths[k] < 30) continue;  // no field
+      f = a.offsets[k] - a.base + 28;
+    } else {
+      f = k * a.stride + 28;
+    }
+    uint16_t c = a.sums[k];
+    if constexpr (UPDATE) {
+      const uint16_t old = *reinterpret_cast<const uint16_t *>(a.arena + f);
+      c = static_cast<uint16_t>(~static_cast<uint16_t>(static_cast<uint16_t>(~c) - old));
+      a.sums[k] = c;
+    }
+    store16_through(a.arena + f, c);  // raw host order, tcp-header.h:177
+  }
+}
+
+template <bool VAR, bool UPDATE>
+hipError_t launch_patch(const PatchArgs &a, uint32_t num_cus, hipStream_t stream) {
+  static const uint32_t per_cu = dev::resident_blocks_per_cu(patch_fields_kernel<VAR, UPDATE>);
+  uint64_t blocks = (a.count + kBlock - 1) / kBlock;
+  const uint64_t cap = static_cast<uint64_t>(per_cu) * num_cus * 8;
+  if (blocks > cap) blocks = cap;
+  hipLaunchKernelGGL((patch_fields_kernel<VAR, UPDATE>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0, stream,
+                     a);
+  return hipGetLastError();
+}
+
+#ifdef TCPCK_PROBE
+// Timing only (fixed strides, no update): the field pass at other
+// granularities and store policies.  GRAN 0: four lanes per image, the field's
+// 64-B block read and written back whole (AUTO's form in round 2); 1: one lane,
+// the 16-B chunk holding the field; 2: the 2-B field alone (no read); 3: eight
+// lanes, the field's 128-B line.  BITS: store cache bits sc0 1 | nt 2 | sc1 4,
+// -1 a plain C++ store.
 template <int BITS>
 __device__ __forceinline__ void store_block(dev::u32x4 *p, dev::u32x4 v) {
   if constexpr (BITS < 0) {
@@ -98,77 +153,9 @@ __device__ __forceinline__ void store_block(dev::u32x4 *p, dev::u32x4 v) {
   }
 }
 
-template <bool VAR, bool UPDATE, int BITS = -1>
-__global__ void __launch_bounds__(kBlock) patch_fields_kernel(PatchArgs a) {
-  const uint64_t step = static_cast<uint64_t>(gridDim.x) * kBlock;
-  const uint64_t total = a.count * 4;
-  const uint64_t base = reinterpret_cast<uint64_t>(a.arena);
-  const uint64_t lo = base + a.lo, hi = base + a.hi;
-  for (uint64_t t = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x; t < total; t += step) {
-    const uint64_t k = t >> 2;
-    const uint32_t j = static_cast<uint32_t>(t & 3);
-    uint64_t f;  // the field, relative to arena
-    bool blk_ok;
-    if constexpr (VAR) {
-      const uint32_t len = a.lengths[k];
-      if (len < 30) {  // no field: the plain checksum stays (UPDATE), nothing is written
-        continue;
-      }
-      const uint64_t start = a.offsets[k] - a.base;
-      f = start + 28;
-      // packed: fields >= 64 B apart and the block inside images k-1 .. k
-      blk_ok = a.packed && len >= 96 &&
-               (k > 0 ? a.lengths[k - 1] >= 64 : ((base + f) & ~uint64_t{63}) >= base + start);
-    } else {
-      f = k * a.stride + 28;
-      const uint64_t b = (base + f) & ~uint64_t{63};
-      blk_ok = b >= lo && b + 64 <= hi;
-    }
-    const uint16_t cin = a.sums[k];
-    if (!blk_ok) {
-      if (j == 0) {
-        uint16_t *p = reinterpret_cast<uint16_t *>(a.arena + f);
-        uint16_t c = cin;
-        if constexpr (UPDATE) {
-          c = static_cast<uint16_t>(~static_cast<uint16_t>(static_cast<uint16_t>(~cin) - *p));
-          a.sums[k] = c;
-        }
-        *p = c;
-      }
-      continue;
-    }
-    const uint64_t blk = ((base + f) & ~uint64_t{63}) - base;  // its 64-B block, relative
-    dev::u32x4 *p = reinterpret_cast<dev::u32x4 *>(a.arena + blk) + j;
-    dev::u32x4 v = *p;
-    const uint32_t r = static_cast<uint32_t>(f - blk) - 16 * j;  // field offset in this lane's 16 B
-    if (r < 16) {
-      const uint32_t sh = 16 * ((r >> 1) & 1);
-      const uint32_t di = r >> 2;
-      const uint32_t d = di == 0 ? v.x : (di == 1 ? v.y : (di == 2 ? v.z : v.w));
-      uint16_t c = cin;
-      if constexpr (UPDATE) {
-        const uint16_t old = static_cast<uint16_t>(d >> sh);
-        c = static_cast<uint16_t>(~static_cast<uint16_t>(static_cast<uint16_t>(~cin) - old));
-        a.sums[k] = c;
-      }
-      const uint32_t m = ~(0xFFFFu << sh), x = static_cast<uint32_t>(c) << sh;
-      v.x = di == 0 ? (v.x & m) | x : v.x;
-      v.y = di == 1 ? (v.y & m) | x : v.y;
-      v.z = di == 2 ? (v.z & m) | x : v.z;
-      v.w = di == 3 ? (v.w & m) | x : v.w;
-    }
-    store_block<BITS>(p, v);
-  }
-}
-
-#ifdef TCPCK_PROBE
-// Timing only: FILL's field stores after the stream at other granularities,
-// fixed strides, BITS as store_block.  GRAN 1: one lane per image, the 16-B
-// chunk holding the field read and written back; 2: the 2-B field alone (no
-// read); 3: eight lanes per image, the field's whole 128-B line.
 template <int GRAN, int BITS>
 __global__ void __launch_bounds__(kBlock) patch_probe_kernel(PatchArgs a) {
-  constexpr int LPI = GRAN == 3 ? 8 : 1;  // lanes per image
+  constexpr int LPI = GRAN == 3 ? 8 : (GRAN == 0 ? 4 : 1);  // lanes per image
   const uint64_t step = static_cast<uint64_t>(gridDim.x) * kBlock;
   const uint64_t total = a.count * LPI;
   const uint64_t base = reinterpret_cast<uint64_t>(a.arena);
@@ -187,9 +174,9 @@ __global__ void __launch_bounds__(kBlock) patch_probe_kernel(PatchArgs a) {
       else
         *p = c;
     } else {
-      const uint64_t gm = GRAN == 3 ? 127 : 15;
+      const uint64_t gm = GRAN == 3 ? 127 : (GRAN == 0 ? 63 : 15);
       const uint64_t blk = ((base + f) & ~gm) - base;
-      if (GRAN == 3 && (base + blk < base + a.lo || blk + 128 > a.hi)) {
+      if (GRAN != 1 && (blk < a.lo || blk + gm + 1 > a.hi)) {  // the block would leave the batch
         if (j == 0) *reinterpret_cast<uint16_t *>(a.arena + f) = c;
         continue;
       }
@@ -213,7 +200,7 @@ __global__ void __launch_bounds__(kBlock) patch_probe_kernel(PatchArgs a) {
 template <int GRAN, int BITS>
 hipError_t launch_patch_probe(const PatchArgs &a, uint32_t num_cus, hipStream_t stream) {
   static const uint32_t per_cu = dev::resident_blocks_per_cu(patch_probe_kernel<GRAN, BITS>);
-  const uint64_t lpi = GRAN == 3 ? 8 : 1;
+  const uint64_t lpi = GRAN == 3 ? 8 : (GRAN == 0 ? 4 : 1);
   uint64_t blocks = (a.count * lpi + kBlock - 1) / kBlock;
   const uint64_t cap = static_cast<uint64_t>(per_cu) * num_cus * 8;
   if (blocks > cap) blocks = cap;
@@ -221,53 +208,46 @@ hipError_t launch_patch_probe(const PatchArgs &a, uint32_t num_cus, hipStream_t 
                      a);
   return hipGetLastError();
 }
-#endif
 
-template <bool VAR, bool UPDATE, int BITS = -1>
-hipError_t launch_patch(const PatchArgs &a, uint32_t num_cus, hipStream_t stream) {
-  static const uint32_t per_cu = dev::resident_blocks_per_cu(patch_fields_kernel<VAR, UPDATE, BITS>);
-  uint64_t blocks = (a.count * 4 + kBlock - 1) / kBlock;
-  const uint64_t cap = static_cast<uint64_t>(per_cu) * num_cus * 8;
-  if (blocks > cap) blocks = cap;
-  hipLaunchKernelGGL((patch_fields_kernel<VAR, UPDATE, BITS>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0,
-                     stream, a);
-  return hipGetLastError();
+// store_bits = 1 + BITS (0: plain) | GRAN << 4
+template <int GRAN>
+hipError_t probe_by_bits(const PatchArgs &a, uint32_t num_cus, hipStream_t stream) {
+  switch (static_cast<int>(a.store_bits & 15) - 1) {
+    case -1: return launch_patch_probe<GRAN, -1>(a, num_cus, stream);
+    case 0: return launch_patch_probe<GRAN, 0>(a, num_cus, stream);
+    case 1: return launch_patch_probe<GRAN, 1>(a, num_cus, stream);
+    case 2: return launch_patch_probe<GRAN, 2>(a, num_cus, stream);
+    case 3: return launch_patch_probe<GRAN, 3>(a, num_cus, stream);
+    case 4: return launch_patch_probe<GRAN, 4>(a, num_cus, stream);
+    case 5: return launch_patch_probe<GRAN, 5>(a, num_cus, stream);
+    case 6: return launch_patch_probe<GRAN, 6>(a, num_cus, stream);
+    case 7: return launch_patch_probe<GRAN, 7>(a, num_cus, stream);
+    default: return hipErrorInvalidValue;
+  }
 }
+#endif
 
 }  // namespace
 
 hipError_t launch_patch_fields(const PatchArgs &a, uint32_t num_cus, hipStream_t stream) {
   if (a.count == 0) return hipSuccess;
   if (!a.sums) return hipErrorInvalidValue;
-  if (a.offsets) {
-    if (!a.lengths) return hipErrorInvalidValue;
-    return a.update ? launch_patch<true, true>(a, num_cus, stream) : launch_patch<true, false>(a, num_cus, stream);
-  }
-  if (a.stride < 64) return hipErrorInvalidValue;  // two fields could share a block
 #ifdef TCPCK_PROBE
-  if (a.store_bits >= 16 && !a.update) {  // timing: other granularities (store_bits >> 4), bits 6 / 7 / plain
-    const int gran = static_cast<int>(a.store_bits >> 4), bits = static_cast<int>(a.store_bits & 15) - 1;
-    if (gran == 1) return bits == 7 ? launch_patch_probe<1, 7>(a, num_cus, stream) : launch_patch_probe<1, -1>(a, num_cus, stream);
-    if (gran == 2) return bits == 7 ? launch_patch_probe<2, 7>(a, num_cus, stream)
-                                    : (bits == 6 ? launch_patch_probe<2, 6>(a, num_cus, stream)
-                                                 : launch_patch_probe<2, -1>(a, num_cus, stream));
-    if (gran == 3) return bits == 7 ? launch_patch_probe<3, 7>(a, num_cus, stream) : launch_patch_probe<3, -1>(a, num_cus, stream);
-    return hipErrorInvalidValue;
-  }
-  if (a.store_bits && !a.update) {  // timing: the block stores with explicit cache bits
-    switch (a.store_bits - 1) {
-      case 0: return launch_patch<false, false, 0>(a, num_cus, stream);
-      case 1: return launch_patch<false, false, 1>(a, num_cus, stream);
-      case 2: return launch_patch<false, false, 2>(a, num_cus, stream);
-      case 3: return launch_patch<false, false, 3>(a, num_cus, stream);
-      case 4: return launch_patch<false, false, 4>(a, num_cus, stream);
-      case 5: return launch_patch<false, false, 5>(a, num_cus, stream);
-      case 6: return launch_patch<false, false, 6>(a, num_cus, stream);
-      case 7: return launch_patch<false, false, 7>(a, num_cus, stream);
+  if (a.store_bits && !a.update && !a.offsets) {  // timing forms (TCPCK_KERNEL_PATCH param)
+    switch (a.store_bits >> 4) {
+      case 0: return a.stride >= 64 ? probe_by_bits<0>(a, num_cus, stream) : hipErrorInvalidValue;
+      case 1: return probe_by_bits<1>(a, num_cus, stream);
+      case 2: return probe_by_bits<2>(a, num_cus, stream);
+      case 3: return a.stride >= 128 ? probe_by_bits<3>(a, num_cus, stream) : hipErrorInvalidValue;
       default: return hipErrorInvalidValue;
     }
   }
 #endif
+  if (a.offsets) {
+    if (!a.lengths) return hipErrorInvalidValue;
+    return a.update ? launch_patch<true, true>(a, num_cus, stream) : launch_patch<true, false>(a, num_cus, stream);
+  }
+  if (a.stride < 30) return hipErrorInvalidValue;  // every image holds a field
   return a.update ? launch_patch<false, true>(a, num_cus, stream) : launch_patch<false, false>(a, num_cus, stream);
 }
 

@@ -164,14 +164,10 @@ struct HeaderArgs {
 hipError_t launch_header_swap(const HeaderArgs &a, uint32_t num_cus, hipStream_t stream);
 
 // ---- FILL's field stores as a second pass (tcpck_header.hip) ----
-// For every image, the 64-B aligned block holding bytes 28-29 is read and
-// written back whole with the checksum patched in (no two fields may share a
-// block; the API's arenas are even, so every field is a u16 inside one 16-B
-// word); where that cannot be shown, a 2-B access instead.
-//   fixed stride (offsets == null): stride >= 64, blocks inside [lo, hi) of the arena;
-//   offset lists: PACKED (offsets[k+1] == offsets[k] + lengths[k], the API's
-//   contract for the flag) and lengths[k] >= 96, lengths[k-1] >= 64 -> block;
-//   otherwise (and always without PACKED) the 2-B access.
+// One lane per image writes bytes 28-29 with a write-through streaming 2-B
+// store (nothing else in the arena is read or written).
+//   fixed stride (offsets == null): stride >= 30;
+//   offset lists: image k at offsets[k] - base, images < 30 B skipped.
 // update == 0: sums[k] is the checksum to store (the stream zeroed the field).
 // update == 1 (REF mode only): sums[k] is the checksum of image k as it stands,
 // field included (a CHECKSUM pass), so the zero-field checksum follows exactly
@@ -180,16 +176,16 @@ hipError_t launch_header_swap(const HeaderArgs &a, uint32_t num_cus, hipStream_t
 // their plain checksum and are not written (seg's FILL does the same).
 struct PatchArgs {
   uint8_t *arena;
-  uint64_t stride;          // image k at k * stride (stride >= 64)
+  uint64_t stride;          // image k at k * stride
   const uint64_t *offsets;  // or image k at offsets[k] - base, lengths[k] bytes
   const uint32_t *lengths;
   uint64_t base;
   uint64_t count;
   uint16_t *sums;
-  uint64_t lo, hi;          // fixed: byte range (relative to arena) the block writes may cover
+  uint64_t lo, hi;          // probe block forms: byte range (relative to arena) their writes may cover
   uint32_t update;          // 1: sums hold CHECKSUM results, derive FILL's from the old field
-  uint32_t packed;          // offset lists: the PACKED contract holds
-  uint32_t store_bits;      // probe builds: 1 + the block stores' cache bits (sc0 1, nt 2, sc1 4), 0 = plain
+  uint32_t packed;          // offset lists: the PACKED contract holds (unused by the 2-B pass)
+  uint32_t store_bits;      // probe builds: 1 + store cache bits (sc0 1, nt 2, sc1 4; 0 plain) | granularity << 4
 };
 hipError_t launch_patch_fields(const PatchArgs &a, uint32_t num_cus, hipStream_t stream);
 

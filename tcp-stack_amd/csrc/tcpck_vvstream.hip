@@ -65,6 +65,7 @@ struct VVArgs {
   uint32_t len;             // fixed layouts: image length (<= stride)
   uint32_t order;           // block order (dev::ordered_block)
   uint32_t keep_first;      // 1: the run's first step read with the default cache policy (L2-kept edge line)
+  uint32_t defer_field;     // kFill: results to out only, the fields left for launch_patch_fields
 };
 
 // Word wi (0..7) of a 16-byte chunk set to zero.
@@ -143,7 +144,7 @@ __global__ void __launch_bounds__(kBlock) vvstream_kernel(VVArgs a) {
       static_cast<uint8_t *>(a.out)[k] = (c == 0) ? 1 : 0;
     } else {
       if (a.out) static_cast<uint16_t *>(a.out)[k] = c;
-      if (OP == kFill) dev::store16_field(r, start_rel + 28, c);  // raw, as the reference
+      if (OP == kFill && !a.defer_field) dev::store16_field(r, start_rel + 28, c);  // raw, as the reference
     }
   };
 
@@ -445,6 +446,7 @@ hipError_t launch_one(const RunArgs &s, uint32_t oversub, int flags, uint32_t nu
   a.len = s.len;
   a.order = (flags & 8) ? 4u : dev::kOrderDefault;  // groups of 16 blocks per XCD
   a.keep_first = (flags & 16) ? 1u : 0u;
+  a.defer_field = (flags & 64) ? 1u : 0u;
   hipLaunchKernelGGL((vvstream_kernel<U, OP, SPLIT, LAYOUT, KEEP, MODE>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0,
                      stream, a);
   return hipGetLastError();
@@ -480,8 +482,10 @@ hipError_t launch_vvstream(int op, int variant, bool fixed, const RunArgs &a, ui
   const uint64_t bytes = fixed ? a.count * a.stride : a.total_bytes;
   uint32_t m = a.oversub ? a.oversub : 1;
   // 8: XCD-chunked run order; 16: L2-kept first step; 32: kFill reads every
-  // step with the default cache policy (small images)
-  const int flags = variant & 56;
+  // step with the default cache policy (small images); 64: kFill writes the
+  // results only (the caller runs launch_patch_fields for the fields)
+  const int flags = variant & 120;
+  if ((flags & 64) && (op != kFill || !a.out)) return hipErrorInvalidValue;
   variant &= 7;
   int u8 = (variant & 1);
   int split = variant >= 2 ? 1 : 0;

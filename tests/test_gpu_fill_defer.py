@@ -1,8 +1,9 @@
-"""FILL with the field stores deferred to a block pass (rstream variant 25:
-the stream writes only the results, then each field's 64-B block is rewritten
-whole): every arena byte and result against the oracle's FILL
-(socket-manager.cc:9-10), including the blocks at the batch's edges that fall
-back to 2-B stores."""
+"""FILL with the field stores deferred to a second pass (rstream variant 25:
+the stream writes only the results, then one write-through 2-B store per
+field): every arena byte and result against the oracle's FILL
+(socket-manager.cc:9-10), including the images at the batch's edges; and the
+probe build's other forms of that pass (64-B blocks, 16-B chunks, 128-B lines,
+each store policy) write the same bytes."""
 import numpy as np
 import pytest
 
@@ -76,7 +77,7 @@ def test_odd_arena_rejected(ctx, op):
 @pytest.mark.parametrize("with_out", [True, False])
 def test_fill_auto_rstream(ctx, length, with_out):
     """AUTO FILL on packed fixed images: with a results buffer the policy
-    defers the fields to the block pass, without one it stores them in the
+    defers the fields to the field pass, without one it stores them in the
     stream -- same arena either way."""
     import tcpck
     from oracle import ref16 as R
@@ -91,4 +92,25 @@ def test_fill_auto_rstream(ctx, length, with_out):
     want = np.array([R.fill_np(exp[k * length:(k + 1) * length]) for k in range(count)], np.uint16)
     if with_out:
         np.testing.assert_array_equal(out.cpu().numpy().view(np.uint16), want)
+    np.testing.assert_array_equal(buf.cpu().numpy(), exp)
+
+
+@pytest.mark.parametrize("form", [0x00, 0x08, 0x07, 0x18, 0x10, 0x28, 0x27, 0x20, 0x38, 0x30])
+def test_field_pass_forms(ctx, form):
+    """TCPCK_KERNEL_PATCH (libtcpck_probe.so): the field pass alone, every
+    granularity (form >> 4: 64-B block, 16-B chunk, 2-B field, 128-B line) and
+    store policy (form & 15: 1 + cache bits, 0 plain) stores out[k] into bytes
+    28-29 of image k and leaves every other byte as it was."""
+    import tcpck
+    rng = np.random.default_rng(form)
+    L, count, mis = 1492, 3000, 6
+    a = rng.integers(0, 256, count * L + 256, dtype=np.uint8)
+    sums = rng.integers(0, 1 << 16, count, dtype=np.uint16)
+    buf = torch.from_numpy(a).cuda()
+    out = torch.from_numpy(sums.view(np.int16)).cuda()
+    ctx.probe.batch_fixed_ex(tcpck.OP_FILL, buf.data_ptr() + mis, L, L, count, out, tcpck.KERNEL_PATCH, form)
+    torch.cuda.synchronize()
+    exp = a.copy()
+    for k in range(count):
+        exp[mis + k * L + 28:mis + k * L + 30] = sums[k:k + 1].view(np.uint8)
     np.testing.assert_array_equal(buf.cpu().numpy(), exp)
