@@ -55,6 +55,7 @@ def case(ctx, s, name, off, ln, total, fixed=None):
     res = {}
     for label, fn in (("CHECKSUM", lambda: run(tcpck.OP_CHECKSUM, 28)), ("FILL in-stream", lambda: run(tcpck.OP_FILL, 28)),
                       ("FILL deferred", lambda: run(tcpck.OP_FILL, 28 | 64)), ("FILL AUTO", auto)):
+        time.sleep(0.05)  # phase boundary for scripts/fill_drain_summary.py
         ms = b2b(fn, s)
         torch.cuda.synchronize()
         if label.startswith("FILL"):

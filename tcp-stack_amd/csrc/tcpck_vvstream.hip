@@ -498,7 +498,7 @@ hipError_t launch_vvstream(int op, int variant, bool fixed, const RunArgs &a, ui
     // runs short with larger M, as rstream does (C5: profiles/r01/split_probe.log).
     m = dev::oversub_for(a.oversub, bytes, static_cast<uint64_t>(num_cus) * 32, 1024, 8u << 10);
     u8 = m >= 32;
-    if (op == kFill && !fixed && !(flags & 32)) {
+    if (op == kFill && !fixed && !(flags & 96)) {  // (deferred fields, + 64: the stream is CHECKSUM's)
       // FILL of packed variable batches: runs of >= 4 KiB and U4 (C3: M = 64,
       // 53.7 % of the roof against 48.6 % at the checksum policy's U8 x 32;
       // M = 96-255 fall off fast, profiles/r01/c3_fill_sweep.log)
