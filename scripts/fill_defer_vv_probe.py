@@ -3,8 +3,9 @@
 layouts (round 3): C3's packed mix and other packed / gapped batches, the
 stream storing the fields itself (kVvPolicy, variant 28) against the stream
 writing only the results + launch_patch_fields (variant 28 | 64), CHECKSUM for
-reference.  ~1.5-3 GB per case, median of back-to-back rounds; results and
-arenas compared."""
+reference; the same for sstream's fixed slots (variant 0 against 0 | 128),
+and for gapped layouts also the CHECKSUM + field-update form.  ~1.5-3 GB per
+case, median of back-to-back rounds; results and arenas compared."""
 import os
 import sys
 import time
@@ -36,14 +37,14 @@ def b2b(fn, s, reps=10, rounds=5):
     return float(np.median(t))
 
 
-def case(ctx, s, name, off, ln, total, fixed=None):
+def case(ctx, s, name, off, ln, total, fixed=None, kernel=None, base=28, defer=64):
     n = ln.size
     a = torch.empty(total, dtype=torch.uint8, device="cuda")
     d_off, d_ln = torch.from_numpy(off).cuda(), torch.from_numpy(ln).cuda()
     tcpck.synth_var(a, d_off, d_ln, int(ln.max()), n, seed=42)
     img = int(ln.astype(np.int64).sum())
     out = torch.empty(n, dtype=torch.int16, device="cuda")
-    V = tcpck.KERNEL_VVSTREAM
+    V = tcpck.KERNEL_VVSTREAM if kernel is None else kernel
     if fixed:
         stride, L = fixed
         run = lambda op, p: ctx.batch_fixed_ex(op, a, stride, L, n, out, V, p, stream=s)
@@ -53,8 +54,11 @@ def case(ctx, s, name, off, ln, total, fixed=None):
         run = lambda op, p: ctx.batch_var_ex(op, a, d_off, d_ln, n, out, V, p, **kw)
         auto = lambda: ctx.batch_var(tcpck.OP_FILL, a, d_off, d_ln, n, out, **kw)
     res = {}
-    for label, fn in (("CHECKSUM", lambda: run(tcpck.OP_CHECKSUM, 28)), ("FILL in-stream", lambda: run(tcpck.OP_FILL, 28)),
-                      ("FILL deferred", lambda: run(tcpck.OP_FILL, 28 | 64)), ("FILL AUTO", auto)):
+    runs = [("CHECKSUM", lambda: run(tcpck.OP_CHECKSUM, base)), ("FILL in-stream", lambda: run(tcpck.OP_FILL, base)),
+            ("FILL deferred", lambda: run(tcpck.OP_FILL, base | defer)), ("FILL AUTO", auto)]
+    if fixed:
+        runs.append(("FILL update", lambda: run(tcpck.OP_FILL, base | tcpck.PARAM_FILL_UPDATE)))
+    for label, fn in runs:
         time.sleep(0.05)  # phase boundary for scripts/fill_drain_summary.py
         ms = b2b(fn, s)
         torch.cuda.synchronize()
@@ -86,6 +90,13 @@ def main():
     n = 1 << 20
     case(ctx, s, "1M x 1492 in 1536-B slots (hull)", np.arange(n, dtype=np.uint64) * 1536, np.full(n, 1492, np.uint32),
          n * 1536, fixed=(1536, 1492))
+    S = tcpck.KERNEL_SSTREAM
+    for stride, L, cnt in ((2048, 1492, n), (4096, 1492, n // 2), (1024, 608, 2 * n), (9216, 9000, n // 6),
+                           (16384, 9000, n // 8)):
+        case(ctx, s, f"{cnt // 1024}K x {L} in {stride}-B slots (sstream)", np.arange(cnt, dtype=np.uint64) * stride,
+             np.full(cnt, L, np.uint32), cnt * stride, fixed=(stride, L), kernel=S, base=0, defer=128)
+    case(ctx, s, "171K x 9000 in 9216-B slots (hull)", np.arange(n // 6, dtype=np.uint64) * 9216,
+         np.full(n // 6, 9000, np.uint32), (n // 6) * 9216, fixed=(9216, 9000))
 
 
 if __name__ == "__main__":

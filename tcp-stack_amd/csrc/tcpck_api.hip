@@ -226,6 +226,7 @@ constexpr int kVvDeferFill = 64;         // vvstream: kFill writes the results o
 // images of at least this many bytes; smaller images pay more for 1M-per-
 // 38-us scattered field stores than the in-stream stores cost them
 constexpr uint64_t kDeferFillMinLen = 512;
+constexpr int kSstreamDeferFill = 128;   // sstream: kFill writes the results only, the field pass follows
 constexpr int kSstreamHdrStream = 32;    // sstream RECEIVE: headers from the stream's registers
 constexpr uint64_t kHdrStreamMaxLen = 256;  // ... for (typical) images up to this length
 // RECEIVE with an explicit kernel: the probe build fuses the headers into any
@@ -401,6 +402,8 @@ hipError_t run_fixed_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint
     return tcpck::launch_gstream(op, param & 0xFFFF, a, num_cus, s);
   }
   if (kernel == TCPCK_KERNEL_SSTREAM) {  // fixed slots: stride % 16 == 0, stride >= len
+    if (auto_pick && op == TCPCK_OP_FILL && out && len >= kDeferFillMinLen) param |= kSstreamDeferFill;
+    if (param & kSstreamDeferFill) *patch = true;
     if (count == 1) stride = (static_cast<uint64_t>(len) + 15) & ~uint64_t{15};  // one image: never read
     if (!tcpck::sstream_fixed_applies(stride, len) || (op == TCPCK_OP_FILL && len < 30) ||
         (mode != TCPCK_MODE_REF && len >= (1u << 17)))
@@ -600,6 +603,10 @@ hipError_t run_var_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const 
     return tcpck::launch_vvstream(op, param & 0xFF, false, a, static_cast<uint32_t>(ctx->num_cus), s);
   }
   if (kernel == TCPCK_KERNEL_SSTREAM) {  // any offset list (runs of <= 128 images)
+    if (param & kSstreamDeferFill) {
+      if (!patch) return hipErrorInvalidValue;
+      *patch = true;
+    }
     tcpck::RunArgs a{};
     a.mode = mode == TCPCK_MODE_REF ? tcpck::kRef : tcpck::kRfc1071;
     a.arena = arena;

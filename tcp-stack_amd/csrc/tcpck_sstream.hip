@@ -88,6 +88,7 @@ struct SSArgs {
   uint32_t order;           // block order (dev::ordered_block)
   int mode;                 // kRef or kRfc1071
   uint8_t *hdr;             // HDR: host-order header k at hdr + 32 k
+  uint32_t defer_field;     // kFill: results to out only, the fields left for launch_patch_fields
 };
 
 __device__ __forceinline__ u32x4 zero_word(u32x4 w, uint32_t wi) {
@@ -414,7 +415,7 @@ __global__ void __launch_bounds__(kBlock) sstream_kernel(SSArgs a) {
               if constexpr (OP == kFill) {
                 const uint16_t cs = dev::finish<MODE>(P - pprev);  // tcp-header.h:262 (REF)
                 if (a.out) static_cast<uint16_t *>(a.out)[kb + i] = cs;
-                dev::store16_field(rsrc, field_at(i, lane == 0 ? e_last : el), cs);  // raw, as the reference
+                if (!a.defer_field) dev::store16_field(rsrc, field_at(i, lane == 0 ? e_last : el), cs);  // raw, as the reference
               } else {
                 store(kb + i, P - pprev, 0);
               }
@@ -446,7 +447,7 @@ __global__ void __launch_bounds__(kBlock) sstream_kernel(SSArgs a) {
           if constexpr (OP == kFill) {
             const uint16_t cs = dev::finish<MODE>(sum);
             if (a.out) static_cast<uint16_t *>(a.out)[kb + (v >> 1)] = cs;
-            dev::store16_field(rsrc, field_at(v >> 1, i == 0 ? e_last : span), cs);
+            if (!a.defer_field) dev::store16_field(rsrc, field_at(v >> 1, i == 0 ? e_last : span), cs);
           } else {
             store(kb + (v >> 1), sum, 0);
           }
@@ -566,6 +567,9 @@ hipError_t launch_sstream(int op, int variant, bool fixed, const RunArgs &r, uin
   a.out = r.out;
   a.mode = r.mode;
   a.hdr = r.hdr;
+  // + 128 (kFill with a results buffer): the results only, the caller runs the field pass
+  a.defer_field = (variant & 128) ? 1u : 0u;
+  if (a.defer_field && (op != kFill || !r.out)) return hipErrorInvalidValue;
   // + 4: default block order; + 8: scattered (the policy's); else groups of
   // 16 blocks per XCD
   a.order = (variant & 8) ? kOrderScatter : ((variant & 4) ? dev::kOrderDefault : 4u);
@@ -609,7 +613,7 @@ hipError_t launch_sstream(int op, int variant, bool fixed, const RunArgs &r, uin
   const bool u8 = u == 2;
 #ifndef TCPCK_PROBE
   // the product library runs the policy (0) and its RECEIVE form (+ 32) only
-  if ((variant & ~32) != 0) return hipErrorInvalidValue;
+  if ((variant & ~(32 | 128)) != 0) return hipErrorInvalidValue;
 #endif
   const bool keepl = (variant & 16) != 0;  // HDR 1: the stream read with the default cache policy
   // HDR: + 32 the headers from the stream's registers (kSstreamHdrStream), + 64 with nt stores
