@@ -37,7 +37,7 @@ def b2b(fn, s, reps=10, rounds=5):
     return float(np.median(t))
 
 
-def case(ctx, s, name, off, ln, total, fixed=None, kernel=None, base=28, defer=64):
+def case(ctx, s, name, off, ln, total, fixed=None, kernel=None, base=28, defer=64, defer_param=None):
     n = ln.size
     a = torch.empty(total, dtype=torch.uint8, device="cuda")
     d_off, d_ln = torch.from_numpy(off).cuda(), torch.from_numpy(ln).cuda()
@@ -55,9 +55,8 @@ def case(ctx, s, name, off, ln, total, fixed=None, kernel=None, base=28, defer=6
         auto = lambda: ctx.batch_var(tcpck.OP_FILL, a, d_off, d_ln, n, out, **kw)
     res = {}
     runs = [("CHECKSUM", lambda: run(tcpck.OP_CHECKSUM, base)), ("FILL in-stream", lambda: run(tcpck.OP_FILL, base)),
-            ("FILL deferred", lambda: run(tcpck.OP_FILL, base | defer)), ("FILL AUTO", auto)]
-    if fixed:
-        runs.append(("FILL update", lambda: run(tcpck.OP_FILL, base | tcpck.PARAM_FILL_UPDATE)))
+            ("FILL deferred", lambda: run(tcpck.OP_FILL, base | defer if defer_param is None else defer_param)), ("FILL AUTO", auto)]
+    runs.append(("FILL update", lambda: run(tcpck.OP_FILL, base | tcpck.PARAM_FILL_UPDATE)))
     for label, fn in runs:
         time.sleep(0.05)  # phase boundary for scripts/fill_drain_summary.py
         ms = b2b(fn, s)
@@ -81,6 +80,9 @@ def main():
     ctx = tcpck.Context(0, probe=True)
     s = torch.cuda.current_stream()
     rng = np.random.default_rng(1)
+    n = 1 << 20
+    case(ctx, s, "C2 1M x 1492 fixed (rstream)", np.arange(n, dtype=np.uint64) * 1492, np.full(n, 1492, np.uint32),
+         n * 1492, fixed=(1492, 1492), kernel=tcpck.KERNEL_RSTREAM, base=20, defer_param=25)
     off, ln, total = synth_np.mixed_layout(4 << 20, seed=42)
     case(ctx, s, "C3 4M 96/608/1492 packed", off, ln, total)
     case(ctx, s, "1M x 1492 packed (var)", *packed(np.full(1 << 20, 1492, np.uint32)))
