@@ -76,9 +76,22 @@ def packed(ln):
     return off, ln, int(ln.astype(np.int64).sum())
 
 
+def sweep(ctx, s):
+    """Packed variable mixes around AUTO's update threshold (448 B): the in-stream
+    FILL with default-policy reads (variant 60, AUTO below it), the stream's
+    policy variant (28), and the update form."""
+    rng = np.random.default_rng(3)
+    for lo, hi in ((32, 256), (64, 512), (128, 640), (192, 768), (256, 896), (64, 1460)):
+        n = int((2 << 30) // ((lo + hi) // 2 + 32))
+        ln = (rng.integers(lo // 2, hi // 2 + 1, n) * 2 + 32).astype(np.uint32)
+        case(ctx, s, f"{n // 1024}K x {lo + 32}-{hi + 32} B packed", *packed(ln), base=60)
+
+
 def main():
     ctx = tcpck.Context(0, probe=True)
     s = torch.cuda.current_stream()
+    if "--sweep" in sys.argv:
+        return sweep(ctx, s)
     rng = np.random.default_rng(1)
     n = 1 << 20
     case(ctx, s, "C2 1M x 1492 fixed (rstream)", np.arange(n, dtype=np.uint64) * 1492, np.full(n, 1492, np.uint32),

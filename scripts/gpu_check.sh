@@ -126,6 +126,7 @@ for s in ${STEPS:-tests smoke bench prof}; do
     fpol) step fpol 300 rocprofv3 --kernel-trace -d gpurun_out/fpol -o run --output-format csv -- python3 scripts/fill_drain_probe.py --phases stream,sp0,sp1,sp2,sp3,sp4,sp5,sp6,sp7,sp8,fill ;;
     fgran) step fgran 300 rocprofv3 --kernel-trace -d gpurun_out/fgran -o run --output-format csv -- python3 scripts/fill_drain_probe.py --phases stream,sp8,sg1_8,sg1_0,sg2_8,sg2_7,sg2_0,sg3_8,sg3_0,instream26,instream,sp7,fill ;;
     fdvv) step fdvv 600 python scripts/fill_defer_vv_probe.py ;;
+    fdsweep) step fdsweep 600 python scripts/fill_defer_vv_probe.py --sweep ;;
     fdvvt) step fdvvt 600 rocprofv3 --kernel-trace -d gpurun_out/fdvvt -o run --output-format csv -- python3 scripts/fill_defer_vv_probe.py ;;
     ftests) step ftests 600 python -u -m pytest tests/test_gpu_fill_defer.py tests/test_gpu_fill_update.py tests/test_gpu_kernels.py -k "fill or Fill" -x -q --timeout 300 --timeout-method thread ;;
     rtests) step rtests 900 python -u -m pytest tests/test_gpu_receive.py tests/test_gpu_rfc_long.py -x -q --timeout 300 --timeout-method thread ;;

@@ -227,6 +227,10 @@ constexpr int kVvDeferFill = 64;         // vvstream: kFill writes the results o
 // 38-us scattered field stores than the in-stream stores cost them
 constexpr uint64_t kDeferFillMinLen = 512;
 constexpr int kSstreamDeferFill = 128;   // sstream: kFill writes the results only, the field pass follows
+// variable layouts: vvstream's in-stream zeroing costs ~25 ns per image, so
+// its deferred form pays only for larger images (C3's mean 732 B: 718 -> 702
+// us; 256-1024 B: 700 -> 740 us; 1492 B: 365 -> 262 us; profiles/r03/fill_forms.log)
+constexpr uint64_t kDeferFillMinVar = 1024;
 constexpr int kSstreamHdrStream = 32;    // sstream RECEIVE: headers from the stream's registers
 constexpr uint64_t kHdrStreamMaxLen = 256;  // ... for (typical) images up to this length
 // RECEIVE with an explicit kernel: the probe build fuses the headers into any
@@ -455,20 +459,27 @@ hipError_t run_fixed_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint
 // the header work into rstream's stream measured no faster: DESIGN.md "Receive
 // path").  hdr: host-order headers to hdr[32k, 32k + 32) instead of in place.
 // FILL as CHECKSUM + field update (reference mode, a results buffer): the
-// layout's CHECKSUM kernel at its full streaming rate, then the patch pass
+// layout's CHECKSUM kernel at its full streaming rate, then the field pass
 // derives each zero-field checksum from the old field, c = ~(~C - f) mod 2^16,
-// and writes it into the field and out[k].  FILL's cost is the scattered field
-// writes, not the stream's field zeroing: the two forms tie at 1-4 KiB and on
-// receive slots, the update loses below 1 KiB (64 B 22 vs 40 %) and on C3 (52.7
-// vs 53.8 %), and wins only for jumbo images in slots (9000 B in 9216-B slots
-// 80.7 -> 83.9 %, in 16-KiB slots 75.9 -> 77.1 %; scripts/fill_update_probe.py,
-// profiles/r02/fill_update_probe.log) -- AUTO takes it there (gapped fixed
-// layouts, images > 4 KiB); elsewhere TCPCK_PARAM_FILL_UPDATE selects it.
+// and writes it through into the field and out[k].  Round 3 (the pass's stores
+// written through, scripts/fill_defer_vv_probe.py, profiles/r03/fill_forms.log,
+// % of the roof, in-stream -> update): packed variable batches on vvstream,
+// whose in-stream field zeroing costs ~25 ns per image, gain most -- C3 53.7 ->
+// 62.2 %, a 608/1492 mix 46.6 -> 69.2 %, 256-1024 B 48.3 -> 55.4 % -- so AUTO
+// takes it there for typical images >= 448 B (below, vvstream's default-policy
+// in-stream FILL); gapped fixed jumbo images keep it (9000 B in 9216-B slots
+// 85.2 %); elsewhere the deferred-field form (the stream zeroes the fields and
+// writes only the results, then the same pass stores them) ties with it or
+// wins (C2 254 vs 258 us), and TCPCK_PARAM_FILL_UPDATE selects it.
+constexpr uint64_t kFillUpdateMinVar = kFillKeepMaxLen;
 bool fill_by_update(int op, int mode, const void *out, int kernel, int param, bool fixed, uint64_t stride,
-                    uint32_t len) {
+                    uint32_t len, const tcpck_layout *layout = nullptr, uint64_t count = 0) {
   if (op != TCPCK_OP_FILL || mode != TCPCK_MODE_REF || !out) return false;
   if (param & TCPCK_PARAM_FILL_UPDATE) return true;
-  return kernel == TCPCK_KERNEL_AUTO && !(param & TCPCK_PARAM_FILL_INSTREAM) && fixed && stride > len && len > 4096;
+  if (kernel != TCPCK_KERNEL_AUTO || (param & TCPCK_PARAM_FILL_INSTREAM)) return false;
+  if (fixed) return stride > len && len > 4096;
+  const uint64_t typical = (layout && layout->total_bytes && count) ? layout->total_bytes / count : 0;
+  return layout && (layout->flags & TCPCK_LAYOUT_PACKED) && typical >= kFillUpdateMinVar && typical <= kRunMaxLen;
 }
 
 hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t stride, uint32_t len,
@@ -584,7 +595,8 @@ hipError_t run_var_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const 
   if (op == TCPCK_OP_RECEIVE) op = TCPCK_OP_VERIFY;  // the header pass follows (run_var)
   if (kernel == TCPCK_KERNEL_VVSTREAM) {
     if (mode != TCPCK_MODE_REF && (param & 32)) return hipErrorInvalidValue;
-    if (auto_pick && op == TCPCK_OP_FILL && out && patch && typical >= kDeferFillMinLen) param |= kVvDeferFill;
+    // (REF packed batches of typical >= 448 B take the update form in run_var)
+    if (auto_pick && op == TCPCK_OP_FILL && out && patch && typical >= kDeferFillMinVar) param |= kVvDeferFill;
     if (param & kVvDeferFill) {
       if (!patch) return hipErrorInvalidValue;
       *patch = true;
@@ -641,7 +653,7 @@ hipError_t run_var(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const uint6
                    uint64_t base, uint64_t count, void *out, const tcpck_layout *layout, int kernel, int param,
                    hipStream_t s, uint8_t *hdr = nullptr) {
   if (op == TCPCK_OP_RECEIVE && base != 0) return hipErrorInvalidValue;  // device batches only
-  if (fill_by_update(op, mode, out, kernel, param, false, 0, 0)) {
+  if (fill_by_update(op, mode, out, kernel, param, false, 0, 0, layout, count)) {
     const int p = param & ~(TCPCK_PARAM_FILL_UPDATE | TCPCK_PARAM_FILL_INSTREAM);
     const hipError_t e =
         run_var_impl(ctx, TCPCK_OP_CHECKSUM, mode, arena, off, len, base, count, out, layout, kernel, p, s);
