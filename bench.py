@@ -21,6 +21,10 @@ ONE JSON line with the driver's fields plus:
                 (profiles/pmc_summary.json), else null
   c3, c4        (default C2 run only) BASELINE configs[2] and [3] timed the same
                 way in the same process, after C2: each rank its own batch
+  fill, slots,  (default C2 run only) the SURVEY §8f rows timed the same way:
+  receive,      send-side FILL on C2's layout, VERIFY and RECEIVE (verdicts +
+  segment       host-order headers) on a 1M-slot receive ring, the send stream
+                cut into checksummed MSS images; each with its own metric
   c5_strong     (default C2 run only) BASELINE configs[4]: ONE 8M x 1492-B batch
                 split over the N ranks with shard_range (8M images on one GPU
                 at N=1, 1M per GPU at N=8); value = all ranks' bytes / the
@@ -66,8 +70,9 @@ CONFIGS = {
            "fixed", 8 << 20, 1492),
 }
 STRONG = {"c5"}  # configs whose total work is fixed as N grows; the rest are per-GPU (weak)
-# the other BASELINE configs timed inside the default (C2) run, and their keys in its line
-EXTRAS = (("c3", "c3"), ("c4", "c4"), ("c5", "c5_strong"))
+# the other BASELINE configs, then the §8f ops, timed inside the default (C2) run, and their keys in its line
+EXTRAS = (("c3", "c3"), ("c4", "c4"), ("c5", "c5_strong"), ("fill", "fill"), ("slots", "slots"),
+          ("receive", "receive"), ("segment", "segment"))
 # round-2 ops (not BASELINE configs; same contract, their own metric):
 EXTRA = {
     # the device-resident receive arena: 1M 2048-B slots, one datagram per slot
@@ -325,7 +330,8 @@ def extra_config(name, key, ctx, stream, rank, world, args, coll_dev):
     import torch
     w = Workload(name, ctx, stream, rank, world)
     tmax, launch_ms, launch_ms_all, step_bytes, settle = measure(w, args, world, stream, coll_dev)
-    rec = {"workload": w.desc, "value": round(step_bytes * args.steps / tmax / GIB, 2), "unit": "GiB/s",
+    rec = {"workload": w.desc, "metric": metric_for(w.kind), "value": round(step_bytes * args.steps / tmax / GIB, 2),
+           "unit": "GiB/s",
            "ms_per_step": round(tmax / args.steps * 1e3, 5), "scaling": "strong" if w.strong else "weak",
            "images_per_gpu": w.count, "bytes_per_gpu": w.img_bytes,
            "roofline": roofline(w, launch_ms, launch_ms_all, name, world), "settle": settle}
