@@ -5,7 +5,8 @@ writing each run's headers itself after the run's verdicts (one launch),
 with the stream read nt (variant 0) or with the default cache policy
 (variant 16, the header lines still in L2 when the run's end re-reads them),
 and (round 3) each header emitted from the stream's registers as the step is
-consumed (variant 32; 96: with nt stores).
+consumed (variant 32; 96: with write-through sc0 sc1 nt stores), and the
+header pass with write-through array stores (1 << 27, probe build).
 VERIFY alone for reference.  Results compared byte for byte.  Median of
 back-to-back rounds."""
 import os
@@ -67,7 +68,8 @@ def case(ctx, s, name, n, slot, ln, fixed_len=None):
             ("fused nt", lambda: ctx.batch_receive(a, n, ok, hdr, kernel=S, param=0, **kw)),
             ("fused keep", lambda: ctx.batch_receive(a, n, ok, hdr, kernel=S, param=16, **kw)),
             ("in-stream", lambda: ctx.batch_receive(a, n, ok, hdr, kernel=S, param=32, **kw)),
-            ("in-str nt", lambda: ctx.batch_receive(a, n, ok, hdr, kernel=S, param=96, **kw)),
+            ("in-str WT", lambda: ctx.batch_receive(a, n, ok, hdr, kernel=S, param=96, **kw)),
+            ("2 passes WT", lambda: ctx.batch_receive(a, n, ok, hdr, kernel=S, param=TWO | (1 << 27), **kw)),
             ("AUTO", lambda: ctx.batch_receive(a, n, ok, hdr, **kw))]
     res = {}
     for label, fn in runs:

@@ -233,6 +233,7 @@ constexpr int kSstreamDeferFill = 128;   // sstream: kFill writes the results on
 constexpr uint64_t kDeferFillMinVar = 1024;
 constexpr int kSstreamHdrStream = 32;    // sstream RECEIVE: headers from the stream's registers
 constexpr uint64_t kHdrStreamMaxLen = 256;  // ... for (typical) images up to this length
+constexpr int kProbeHdrWriteThrough = 1 << 27;  // probe builds: the header pass's array stores written through
 // RECEIVE with an explicit kernel: the probe build fuses the headers into any
 // kernel that can (sstream's after-the-run conversion, HDR 1); the product
 // carries only the stream-register form (+ kSstreamHdrStream) and otherwise
@@ -534,6 +535,7 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
   h.stride = stride;
   h.count = count;
   h.out = hdr;
+  h.store_bits = (param & kProbeHdrWriteThrough) ? 1u : 0u;
   return tcpck::launch_header_swap(h, static_cast<uint32_t>(ctx->num_cus), s);
 }
 
@@ -690,6 +692,7 @@ hipError_t run_var(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const uint6
   h.offsets = off;
   h.count = count;
   h.out = hdr;
+  h.store_bits = (param & kProbeHdrWriteThrough) ? 1u : 0u;
   return tcpck::launch_header_swap(h, static_cast<uint32_t>(ctx->num_cus), s);
 }
 

@@ -31,7 +31,7 @@ using dev::kBlock;
 
 __device__ __forceinline__ uint16_t bswap16(uint16_t v) { return static_cast<uint16_t>((v >> 8) | (v << 8)); }
 
-template <bool FIXED, bool EXTRACT>
+template <bool FIXED, bool EXTRACT, bool WT = false>
 __global__ void __launch_bounds__(kBlock) header_swap_kernel(HeaderArgs a) {
   const uint64_t step = static_cast<uint64_t>(gridDim.x) * kBlock;
   const uint64_t total = a.count * 8;
@@ -44,7 +44,13 @@ __global__ void __launch_bounds__(kBlock) header_swap_kernel(HeaderArgs a) {
     if constexpr (EXTRACT) {
       // dense output: lane group k writes the 32 B of header k, whole lines
       const uint32_t h = static_cast<uint32_t>(lo) | (static_cast<uint32_t>(hi) << 16);
-      reinterpret_cast<uint32_t *>(a.out)[t] = dev::n2h_dword(h, dev::n2h_selector(j));
+      const uint32_t v = dev::n2h_dword(h, dev::n2h_selector(j));
+      if constexpr (WT) {  // probe: write-through streaming stores
+        uint32_t *dst = reinterpret_cast<uint32_t *>(a.out) + t;
+        asm volatile("global_store_dword %0, %1, off sc0 sc1 nt" ::"v"(dst), "v"(v) : "memory");
+      } else {
+        reinterpret_cast<uint32_t *>(a.out)[t] = v;
+      }
     } else if (j == 0 || j == 1 || j == 4 || j == 5) {
       // j = 0, 1, 4, 5: a u32 field (its two u16 halves trade places, each swapped)
       w[0] = bswap16(hi);
@@ -57,15 +63,15 @@ __global__ void __launch_bounds__(kBlock) header_swap_kernel(HeaderArgs a) {
   }
 }
 
-template <bool FIXED, bool EXTRACT>
+template <bool FIXED, bool EXTRACT, bool WT = false>
 hipError_t launch_one(const HeaderArgs &a, uint32_t num_cus, hipStream_t s) {
-  static const uint32_t per_cu = dev::resident_blocks_per_cu(header_swap_kernel<FIXED, EXTRACT>);
+  static const uint32_t per_cu = dev::resident_blocks_per_cu(header_swap_kernel<FIXED, EXTRACT, WT>);
   uint64_t blocks = (a.count * 8 + kBlock - 1) / kBlock;
   // grid-stride beyond 8 resident grids (4 loads in flight per lane measured no faster:
   // profiles/r02/receive_probe.log)
   const uint64_t cap = static_cast<uint64_t>(per_cu) * num_cus * 8;
   if (blocks > cap) blocks = cap;
-  hipLaunchKernelGGL((header_swap_kernel<FIXED, EXTRACT>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0, s,
+  hipLaunchKernelGGL((header_swap_kernel<FIXED, EXTRACT, WT>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0, s,
                      a);
   return hipGetLastError();
 }
@@ -253,6 +259,10 @@ hipError_t launch_patch_fields(const PatchArgs &a, uint32_t num_cus, hipStream_t
 
 hipError_t launch_header_swap(const HeaderArgs &a, uint32_t num_cus, hipStream_t stream) {
   if (a.count == 0) return hipSuccess;
+#ifdef TCPCK_PROBE
+  if (a.out && a.store_bits)
+    return a.offsets ? launch_one<false, true, true>(a, num_cus, stream) : launch_one<true, true, true>(a, num_cus, stream);
+#endif
   if (a.out)
     return a.offsets ? launch_one<false, true>(a, num_cus, stream) : launch_one<true, true>(a, num_cus, stream);
   return a.offsets ? launch_one<false, false>(a, num_cus, stream) : launch_one<true, false>(a, num_cus, stream);

@@ -49,7 +49,7 @@
 //     its 32 header bytes in compacted chunks C_i and C_i + 1, so the two lanes
 //     holding them permute their dwords and store 16 B each at hdr + 32 k
 //     (+ 16) as the step is consumed: the header bytes are read once, by the
-//     stream (3: nt stores).  A run with a misaligned or < 32-B image (or a
+//     stream (3: write-through sc0 sc1 nt stores).  A run with a misaligned or < 32-B image (or a
 //     misaligned array) and HDR 1 instead convert after the verdicts, one
 //     image per lane, re-reading the header lines (KEEPL: the stream read
 //     with the default cache policy so they are still in L2).
@@ -344,8 +344,8 @@ __global__ void __launch_bounds__(kBlock) sstream_kernel(SSArgs a) {
               const u32x4 o{dev::n2h_dword(w.x, 0x00010203u), dev::n2h_dword(w.y, 0x00010203u),
                             dev::n2h_dword(w.z, 0x02030100u), dev::n2h_dword(w.w, (hk & 1u) ? 0x02030100u : 0x02030001u)};
               u32x4 *dst = reinterpret_cast<u32x4 *>(a.hdr + 32 * (kb + (hk >> 1)) + 16 * (hk & 1u));
-              if constexpr (HDR == 3)
-                __builtin_nontemporal_store(o, dst);
+              if constexpr (HDR == 3)  // write-through streaming store (probe)
+                asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt" ::"v"(dst), "v"(o) : "memory");
               else
                 *dst = o;
             }
@@ -616,7 +616,7 @@ hipError_t launch_sstream(int op, int variant, bool fixed, const RunArgs &r, uin
   if ((variant & ~(32 | 128)) != 0) return hipErrorInvalidValue;
 #endif
   const bool keepl = (variant & 16) != 0;  // HDR 1: the stream read with the default cache policy
-  // HDR: + 32 the headers from the stream's registers (kSstreamHdrStream), + 64 with nt stores
+  // HDR: + 32 the headers from the stream's registers (kSstreamHdrStream), + 64 with write-through stores
   const int hdr_mode = (variant & 32) ? ((variant & 64) ? 3 : 2) : 1;
 #ifdef TCPCK_PROBE
   if (u8) return fixed ? dispatch<8, true>(op, a, m, min_waves, num_cus, stream, keepl, hdr_mode)
