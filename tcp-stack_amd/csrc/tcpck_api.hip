@@ -495,7 +495,7 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
     pa.count = count;
     pa.sums = static_cast<uint16_t *>(out);
     pa.hi = (count - 1) * stride + len;
-    pa.store_bits = static_cast<uint32_t>(param & 0x3F);  // 1 + sc0 1 | nt 2 | sc1 4 (0 = plain) | granularity << 4
+    pa.store_bits = static_cast<uint32_t>(param & 0x7F);  // 1 + sc0 1 | nt 2 | sc1 4 (0 = plain) | form << 4
     return tcpck::launch_patch_fields(pa, static_cast<uint32_t>(ctx->num_cus), s);
   }
 #endif

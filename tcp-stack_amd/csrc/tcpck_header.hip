@@ -20,6 +20,8 @@
 // streaming bandwidth.  EXTRACT (tcpck_batch_receive with a header array):
 // the arena stays as it is and header k goes to out[32k, 32k + 32) instead --
 // the writes are dense whole lines, not one partial line per image.
+#include <algorithm>
+
 #include "tcpck_device.h"
 #include "tcpck_internal.h"
 
@@ -203,6 +205,34 @@ __global__ void __launch_bounds__(kBlock) patch_probe_kernel(PatchArgs a) {
   }
 }
 
+// Timing only: the 2-B write-through field pass with other image -> thread
+// maps.  MAP 0: four consecutive images per thread; 1: four per thread, a
+// quarter of the batch apart; 2: the resident grid only, grid-stride; 3: each
+// 256-thread block writes its 256 images in a stride-8 interleaved order.
+template <int MAP>
+__global__ void __launch_bounds__(kBlock) patch_map_kernel(PatchArgs a) {
+  const uint64_t step = static_cast<uint64_t>(gridDim.x) * kBlock;
+  const uint64_t t0 = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  auto put = [&](uint64_t k) {
+    if (k < a.count) store16_through(a.arena + k * a.stride + 28, a.sums[k]);
+  };
+  if constexpr (MAP == 0) {
+    for (uint64_t t = t0; 4 * t < a.count; t += step)
+      for (int i = 0; i < 4; ++i) put(4 * t + i);
+  } else if constexpr (MAP == 1) {
+    const uint64_t q = (a.count + 3) / 4;
+    for (uint64_t t = t0; t < q; t += step)
+      for (int i = 0; i < 4; ++i) put(t + i * q);
+  } else if constexpr (MAP == 2) {
+    for (uint64_t t = t0; t < a.count; t += step) put(t);
+  } else {
+    for (uint64_t b = static_cast<uint64_t>(blockIdx.x) * kBlock; b < a.count; b += step) {
+      const uint32_t x = threadIdx.x;
+      put(b + (x & 31u) * 8u + (x >> 5));
+    }
+  }
+}
+
 template <int GRAN, int BITS>
 hipError_t launch_patch_probe(const PatchArgs &a, uint32_t num_cus, hipStream_t stream) {
   static const uint32_t per_cu = dev::resident_blocks_per_cu(patch_probe_kernel<GRAN, BITS>);
@@ -240,6 +270,22 @@ hipError_t launch_patch_fields(const PatchArgs &a, uint32_t num_cus, hipStream_t
   if (!a.sums) return hipErrorInvalidValue;
 #ifdef TCPCK_PROBE
   if (a.store_bits && !a.update && !a.offsets) {  // timing forms (TCPCK_KERNEL_PATCH param)
+    if ((a.store_bits >> 4) >= 4) {  // the 2-B write-through pass with other maps
+      static const uint32_t per_cu = 8;
+      const int map = static_cast<int>(a.store_bits >> 4) - 4;
+      uint64_t blocks = (a.count + kBlock - 1) / kBlock;
+      if (map == 0 || map == 1) blocks = (blocks + 3) / 4;
+      if (map == 2) blocks = std::min<uint64_t>(blocks, static_cast<uint64_t>(per_cu) * num_cus);
+      const dim3 g(static_cast<uint32_t>(blocks)), b(kBlock);
+      switch (map) {
+        case 0: hipLaunchKernelGGL(patch_map_kernel<0>, g, b, 0, stream, a); break;
+        case 1: hipLaunchKernelGGL(patch_map_kernel<1>, g, b, 0, stream, a); break;
+        case 2: hipLaunchKernelGGL(patch_map_kernel<2>, g, b, 0, stream, a); break;
+        case 3: hipLaunchKernelGGL(patch_map_kernel<3>, g, b, 0, stream, a); break;
+        default: return hipErrorInvalidValue;
+      }
+      return hipGetLastError();
+    }
     switch (a.store_bits >> 4) {
       case 0: return a.stride >= 64 ? probe_by_bits<0>(a, num_cus, stream) : hipErrorInvalidValue;
       case 1: return probe_by_bits<1>(a, num_cus, stream);
