@@ -24,9 +24,11 @@
 //     each read with v_readlane into SGPRs; the image that ends there gets
 //     ~(P - P_prev), selected into lane (k mod 64) of a staging VGPR, and 64
 //     results leave as one coalesced store;
-//   * kFill zeroes each image's checksum word (bytes 28-29) in the stream, so
-//     the differences are the checksums of the zero-field images, and writes
-//     them into bytes 28-29 (tcp-header.h:177); kVerify stores checksum == 0.
+//   * kFill reads each image's checksum word (bytes 28-29) as the stream
+//     passes it (one v_readlane) and subtracts it from the image's sum, so the
+//     results are the checksums of the zero-field images (exact in both modes:
+//     the RFC 1071 prefix is an exact word sum); they go into bytes 28-29
+//     (tcp-header.h:177); kVerify stores checksum == 0.
 //     With FixedStreamArgs::defer_field, kFill writes only the results, and
 //     launch_patch_fields (tcpck_header.hip) stores the fields afterwards as
 //     whole 64-B blocks (the AUTO choice when there is a results buffer).
@@ -116,7 +118,16 @@ __global__ void __launch_bounds__(kBlock) rstream_kernel(FixedStreamArgs a) {
   const uint32_t nimg = static_cast<uint32_t>(ke - kb);
   uint32_t nb = lead + S;
   uint32_t jn = 1;
-  uint32_t nf = lead + 28;  // kFill: next checksum field to zero
+  uint32_t nf = lead + 28;  // kFill: next checksum field (image jf's, run-relative)
+  uint32_t jf = 0;
+  // kFill: image j's field word, parked in lane j mod 64 of fstage and
+  // subtracted from the image's sum when its end is resolved -- the same
+  // result as zeroing the field in the stream (socket-manager.cc:9: Checksum()
+  // = 0 before the sum), without touching the data registers.  A step's
+  // fields are read before its ends, but image j + 64's field lies past image
+  // j's end by more than a step (images >= 30 B hold <= 35 fields per KiB),
+  // so no slot is reused before it is consumed.
+  uint32_t fstage = 0;
   uint32_t carry = 0;       // P at the step start
   uint32_t p_last = 0;      // P at the latest boundary (run start: 0)
   // results staged in lane (j - out_rel) until 64 are ready
@@ -141,6 +152,7 @@ __global__ void __launch_bounds__(kBlock) rstream_kernel(FixedStreamArgs a) {
     }
   };
   auto emit = [&](uint32_t jr, uint32_t sum) {  // jr = run-relative image index, sum = its word sum
+    if constexpr (OP == kFill) sum -= dev::read_lane(fstage, jr & 63u);
     const uint32_t j = jr - out_rel;
     stage = lane == j ? static_cast<uint32_t>(dev::finish<MODE>(sum)) : stage;  // j, sum wave-uniform: v_cmp + v_cndmask
     if (j == 63) {
@@ -176,19 +188,15 @@ __global__ void __launch_bounds__(kBlock) rstream_kernel(FixedStreamArgs a) {
         const int32_t hi = min(max(static_cast<int32_t>(span) - crel, 0), 16);
         w = dev::apply_mask(w, dev::word_mask(lo, hi));
       }
-      if constexpr (OP == kFill) {  // zero the checksum fields passing through this step
+      if constexpr (OP == kFill) {  // the checksum fields passing through this step: read, not zeroed
         while (nf < sb + 1024 && nf < span) {
           const uint32_t rel = nf - sb;
-          if (lane == (rel >> 4)) {
-            const uint32_t wi = (rel & 15u) >> 1;
-            const uint32_t keep = (wi & 1u) ? 0x0000FFFFu : 0xFFFF0000u;
-            const uint32_t di = wi >> 1;
-            if (di == 0) w.x &= keep;
-            if (di == 1) w.y &= keep;
-            if (di == 2) w.z &= keep;
-            if (di == 3) w.w &= keep;
-          }
+          const uint32_t lb = rel >> 4, wi = (rel & 15u) >> 1, di = wi >> 1;  // wave-uniform
+          const uint32_t d = dev::read_lane(di == 0 ? w.x : (di == 1 ? w.y : (di == 2 ? w.z : w.w)), lb);
+          const uint32_t fw = (wi & 1u) ? d >> 16 : d & 0xFFFFu;
+          fstage = lane == (jf & 63u) ? fw : fstage;
           nf += S;
+          ++jf;
         }
       }
       const uint32_t tot = (FLAV & 1) ? dev::ref_chunk_sum_dot(w) : dev::ref_chunk_sum(w);
