@@ -30,7 +30,7 @@ def main():
             ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, a[i * L:(i + sub) * L], L, L, sub, out[i:i + sub],
                                tcpck.KERNEL_RSTREAM, 20 | (m << 16), stream=s)
 
-    cases = [(N, 0), (N, 128), (N, 64), (4 << 20, 0), (2 << 20, 0), (1 << 20, 0)]
+    cases = [(N, 0), (N, 128), (N, 64), (4 << 20, 0), (2 << 20, 0), (1 << 20, 0), (1 << 19, 0)]
     for sub, m in cases:
         out.zero_()
         launch(sub, m)
