@@ -130,6 +130,8 @@ for s in ${STEPS:-tests smoke bench prof}; do
     fdvvt) step fdvvt 600 rocprofv3 --kernel-trace -d gpurun_out/fdvvt -o run --output-format csv -- python3 scripts/fill_defer_vv_probe.py ;;
     ftests) step ftests 600 python -u -m pytest tests/test_gpu_fill_defer.py tests/test_gpu_fill_update.py tests/test_gpu_kernels.py -k "fill or Fill" -x -q --timeout 300 --timeout-method thread ;;
     fmap) step fmap 300 rocprofv3 --kernel-trace -d gpurun_out/fmap -o run --output-format csv -- python3 scripts/fill_drain_probe.py --phases stream,sg2_8,sg4_8,sg5_8,sg6_8,sg7_8,fill,sg2_8 ;;
+    wtprobe) step segwt 600 python scripts/segment_probe.py --params 0,64,128 --cases 1460:1504,1024:1056 &&
+      step gswt 600 python scripts/gstream_probe.py --ops fill --lengths 32,64,128 --gs 0x401,0x801,0xC01 ;;
     rtests) step rtests 900 python -u -m pytest tests/test_gpu_receive.py tests/test_gpu_rfc_long.py -x -q --timeout 300 --timeout-method thread ;;
     tests_new) step tests_new 900 python -u -m pytest tests/test_gpu_c5.py tests/test_gpu_multi_ctx.py tests/test_drop_in.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
     bench_receive) step bench_receive 600 python bench.py --config receive ;;

@@ -285,6 +285,8 @@ hipError_t launch_gstream(int op, int variant, const GroupStreamArgs &a, uint32_
       case 0x400: return by_len<4, -1, 2, false, 2>(op, b, num_cus, stream);
       case 0x800: return by_len<4, -1, 2, false, 0>(op, b, num_cus, stream);
       case 0xC00: return by_len<4, -1, 2, false, 16>(op, b, num_cus, stream);  // sc1
+      case 0x801: return by_len<8, -1, 2, false, 18>(op, b, num_cus, stream);  // sc1 nt (write-through)
+      case 0xC01: return by_len<8, -1, 2, false, 19>(op, b, num_cus, stream);  // sc0 sc1 nt
       default: return hipErrorInvalidValue;
     }
   }

@@ -105,7 +105,9 @@ __global__ void __launch_bounds__(kBlock) segment_kernel(SegmentArgs a) {
   auto store16 = [&](uint32_t voff, u32x4 w) {
     typedef unsigned v4u __attribute__((ext_vector_type(4)));
     const v4u v = {w.x, w.y, w.z, w.w};
-    __builtin_amdgcn_raw_buffer_store_b128(v, rout, static_cast<int>(voff), 0, SPOL == 0 ? 2 : (SPOL == 2 ? 16 : 0));
+    // SPOL 0 nt, 1 default, 2 sc1, 3 sc1 nt, 4 sc0 sc1 nt (write-through streaming)
+    constexpr int aux = SPOL == 0 ? 2 : (SPOL == 2 ? 16 : (SPOL == 3 ? 18 : (SPOL == 4 ? 19 : 0)));
+    __builtin_amdgcn_raw_buffer_store_b128(v, rout, static_cast<int>(voff), 0, aux);
   };
   auto header1 = [&](uint32_t i, uint32_t csum) -> u32x4 {  // bytes 16-31: seq, ack, flags/window, checksum/urgent
     const uint32_t seq = a.seq0 + static_cast<uint32_t>((kb + i) * static_cast<uint64_t>(S));
@@ -333,6 +335,13 @@ hipError_t launch_segment(int mode, int variant, SegmentArgs a, uint32_t oversub
   // variant & 7: 0 = policy, 1 = U4 nt stores, 2 = U4 default-policy stores,
   // 3 = U4 sc1 stores, 4 = U8 default-policy stores, 5 = U8 nt stores, 6 = 2 with
   // default-policy loads
+#ifdef TCPCK_PROBE
+  if (variant & 0xC0) {  // the policy's MSS form with write-through stores: 0x40 sc1 nt, 0x80 sc0 sc1 nt
+    if (a.seg >= 8192) return hipErrorInvalidValue;
+    return (variant & 0x80) ? by_mode<4, 4, 0>(mode, a, oversub, num_cus, stream)
+                            : by_mode<4, 3, 0>(mode, a, oversub, num_cus, stream);
+  }
+#endif
   switch (variant & 7) {  // (bit 3: default block order)
     // policy: default-policy stores (66.6 vs 61.2 % with nt at M = 32) and loads
     // (9000-B segments 64.2 vs 60.6 %; MSS +0.2-0.5 %: the 4-B offset loads of
