@@ -225,6 +225,68 @@ def test_c3_full_4m_mixed_vs_oracle(ctx, oracle_c):
     np.testing.assert_array_equal(host(out).view(np.uint16), exp)
 
 
+def test_c3_full_fill_update_then_verify(ctx, oracle_c):
+    """C3 at full size through AUTO's send path (round 3: packed variable batches
+    take CHECKSUM's stream + the write-through field-update pass): every result
+    against the oracle's FILL on a sample and every image verifying afterwards;
+    the bytes outside the fields unchanged."""
+    import tcpck
+    import synth_np
+    from oracle import ref16 as R
+    count = 4 << 20
+    off, ln, total = synth_np.mixed_layout(count, seed=42)
+    a = torch.empty(total, dtype=torch.uint8, device="cuda")
+    d_off, d_ln = dev(off), dev(ln)
+    tcpck.synth_var(a, d_off, d_ln, 1492, count, seed=42)
+    before = host(a).copy()
+    out = torch.empty(count, dtype=torch.int16, device="cuda")
+    ctx.batch_var(tcpck.OP_FILL, a, d_off, d_ln, count, out, total_bytes=int(ln.sum()), min_len=96, max_len=1492,
+                  packed=True)
+    got = host(out).view(np.uint16)
+    after = host(a)
+    rng = np.random.default_rng(4)
+    idx = np.unique(np.concatenate([rng.integers(0, count, 5000), [0, count - 1]]))
+    for k in idx:
+        o, n = int(off[k]), int(ln[k])
+        img = before[o:o + n].copy()
+        assert R.fill_np(img) == got[k], k
+        np.testing.assert_array_equal(after[o:o + n], img, err_msg=f"image {k}")
+    fields = (off.astype(np.int64)[:, None] + np.array([28, 29])[None, :]).reshape(-1)
+    mask = np.ones(total, bool)
+    mask[fields] = False
+    np.testing.assert_array_equal(after[mask], before[mask])  # nothing but bytes 28-29 written
+    ok = torch.empty(count, dtype=torch.uint8, device="cuda")
+    ctx.batch_var(tcpck.OP_VERIFY, a, d_off, d_ln, count, ok, total_bytes=int(ln.sum()), packed=True)
+    assert int(ok.sum(dtype=torch.int64).item()) == count
+    np.testing.assert_array_equal(oracle_c.batch(after, off, ln, threads=16)[idx], np.zeros(idx.size, np.uint16))
+
+
+def test_receive_small_ring_full_size(ctx, oracle_c):
+    """The small-datagram receive ring AUTO sends to the in-stream header form
+    (4M x 32-254-B datagrams in 256-B slots, a third valid): verdicts and every
+    header byte against the numpy receive path, the ring unchanged."""
+    import tcpck
+    from oracle import ref16 as R
+    rng = np.random.default_rng(21)
+    n, slot = 4 << 20, 256
+    ln = (rng.integers(16, 128, n) * 2).astype(np.uint32)
+    off = np.arange(n, dtype=np.uint64) * np.uint64(slot)
+    a = rng.integers(0, 256, n * slot, dtype=np.uint8)
+    for k in range(0, n, 3 * 4096):  # some valid images (FILLed like the send path)
+        R.fill_np(a[k * slot:k * slot + int(ln[k])])
+    d = dev(a)
+    ok = torch.empty(n, dtype=torch.uint8, device="cuda")
+    hdr = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
+    ctx.batch_receive(d, n, ok, hdr, offsets=dev(off), lengths=dev(ln), total_bytes=int(ln.sum()),
+                      min_len=int(ln.min()), max_len=int(ln.max()), sorted=True)
+    exp_ok = (oracle_c.batch(a, off, ln, threads=16) == 0).astype(np.uint8)
+    assert exp_ok.sum() >= n // (3 * 4096)
+    np.testing.assert_array_equal(host(ok), exp_ok)
+    o = off.astype(np.int64)
+    np.testing.assert_array_equal(host(hdr).reshape(n, 32), a[o[:, None] + R.HEADER_PERM[None, :]])
+    np.testing.assert_array_equal(host(d), a)
+
+
 @pytest.mark.parametrize("L", [32, 256])
 def test_small_pow2_above_4gib_sampled(ctx, oracle_c, L):
     """Pure-ACK-sized images in a 4.5 GiB arena (byte offsets past 2^32): gstream
