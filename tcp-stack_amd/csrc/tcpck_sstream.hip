@@ -251,7 +251,7 @@ __global__ void __launch_bounds__(kBlock) sstream_kernel(SSArgs a) {
       if constexpr (FIXED) {
         const uint32_t i = a.magic ? (__umulhi(q, a.magic) >> a.shift) : (q >> a.shift);
         const uint32_t c = q - i * a.nchunk;
-        if constexpr (HDR >= 2) hk_next = (q < T && c < 2u) ? (i << 1) | c : ~0u;
+        if constexpr (HDR >= 2 || HDR < 0) hk_next = (q < T && c < 2u) ? (i << 1) | c : ~0u;
         return i * S + (c << 4);
       } else {
         const uint32_t cj = s_c[wv][il + lane];  // image il + lane starts at chunk cj
@@ -266,7 +266,7 @@ __global__ void __launch_bounds__(kBlock) sstream_kernel(SSArgs a) {
         // flags at or below l, less il's own flag when il starts at q0
         const uint32_t idx = il + below + f - static_cast<uint32_t>(M & 1u);
         const uint32_t d = s_d[wv][idx];
-        if constexpr (HDR >= 2) {
+        if constexpr (HDR >= 2 || HDR < 0) {
           // first chunk: the lane's own flag; second: the flag one lane down
           // (lane 0: the previous step's lane 63) -- every image here has >= 2 chunks
           const uint32_t second = lane ? static_cast<uint32_t>(M >> (lane - 1)) & 1u : hf_prev;
@@ -287,7 +287,17 @@ __global__ void __launch_bounds__(kBlock) sstream_kernel(SSArgs a) {
       }
     };
     auto load_step = [&](uint32_t t) -> u32x4 {
-      if constexpr (KEEPL) {
+      if constexpr (HDR < 0) {
+        // probe (HDR -1): each image's first two chunks read with the default
+        // policy, the rest nt -- the header lines left cached for a header pass
+        const uint32_t off = map_step(t);
+        typedef unsigned v4u __attribute__((ext_vector_type(4)));
+        if (hk_next != ~0u) {
+          const v4u v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, static_cast<int>(off), 0, 0);
+          return u32x4{v.x, v.y, v.z, v.w};
+        }
+        return dev::load16_buf_nt(rsrc, off, 0);
+      } else if constexpr (KEEPL) {
         typedef unsigned v4u __attribute__((ext_vector_type(4)));
         const v4u v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, static_cast<int>(map_step(t)), 0, 0);
         return u32x4{v.x, v.y, v.z, v.w};
@@ -518,6 +528,10 @@ hipError_t launch_one(SSArgs a, uint32_t oversub, uint64_t min_waves, uint32_t n
 template <int U, bool FIXED>
 hipError_t dispatch(int op, const SSArgs &a, uint32_t m, uint64_t min_waves, uint32_t num_cus, hipStream_t s,
                     bool keepl, int hdr_mode) {
+#ifdef TCPCK_PROBE
+  if (!a.hdr && keepl && op == kVerify && a.mode == kRef)  // + 16 without a header array: HDR -1
+    return launch_one<U, kVerify, FIXED, kRef, -1>(a, m, min_waves, num_cus, s);
+#endif
   if (a.hdr) {  // VERIFY + the run's headers into the array (tcpck_batch_receive)
     if (op != kVerify) return hipErrorInvalidValue;
     if (hdr_mode == 2 && !keepl)  // AUTO: the headers from the stream's registers
