@@ -466,34 +466,6 @@ def cpu_threads() -> tuple[int, dict]:
     return max(1, n), {"affinity_cpus": aff, "nproc": os.cpu_count(), "omp_num_threads": omp or None}
 
 
-def spread_cpus(n: int) -> tuple[list, int]:
-    """n CPUs of this process's affinity mask, one per L3 domain (CCD) in turn,
-    first SMT siblings first: a DRAM-sized pass is bound by each CCD's link to
-    memory, so n threads on one or two CCDs read at a fraction of what n
-    threads spread over the host do.  Returns (cpus, L3 domains used)."""
-    cpus = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else list(range(os.cpu_count() or 1))
-
-    def rd(c, leaf, default):
-        try:
-            with open(f"/sys/devices/system/cpu/cpu{c}/{leaf}") as f:
-                return f.read().strip()
-        except OSError:
-            return default
-    dom: dict = {}
-    for c in cpus:
-        sib = rd(c, "topology/thread_siblings_list", str(c)).replace("-", ",").split(",")
-        smt = 0 if str(c) == sib[0] else 1
-        dom.setdefault(rd(c, "cache/index3/id", str(c // 8)), []).append((smt, c))
-    groups = [sorted(v) for _, v in sorted(dom.items(), key=lambda kv: int(kv[0]) if kv[0].isdigit() else 0)]
-    out, i = [], 0
-    while len(out) < min(n, len(cpus)):
-        for g in groups:
-            if i < len(g) and len(out) < n:
-                out.append(g[i][1])
-        i += 1
-    return out, len(groups)
-
-
 def cpu_baseline(host_arena, gpu_res, kind, count, L, budget_s, var_layout):
     """Reference CalculateChecksum on the host cores over the WHOLE batch (the
     C2 arena is 1.56 GB, ~6x the host's 256 MB L3, so the passes stream from
@@ -513,29 +485,21 @@ def cpu_baseline(host_arena, gpu_res, kind, count, L, budget_s, var_layout):
         kind_s = "reference"
         pk = R.RefLib("O3").packets(host_arena, **sargs)  # MakeNetPacket once, outside timing
 
-        cpus, ndom = spread_cpus(nthr)
-
-        def passes(lib_pk, threads, n_pass, target_s, pin=True):
-            """Median GiB/s over n_pass timed passes of ~target_s each (threads
-            pinned one per L3 domain in turn, or left to the scheduler)."""
-            c = cpus if pin else None
-            t1 = lib_pk.run_reps(threads, 1, c)
+        def passes(lib_pk, threads, n_pass, target_s):
+            """Median GiB/s over n_pass timed passes of ~target_s each."""
+            t1 = lib_pk.run_reps(threads, 1)
             reps = max(1, int(target_s / max(t1, 1e-6)))
-            rates = [sbytes * reps / lib_pk.run_reps(threads, reps, c) / GIB for _ in range(n_pass)]
+            rates = [sbytes * reps / lib_pk.run_reps(threads, reps) / GIB for _ in range(n_pass)]
             return statistics.median(rates), rates, reps
 
         got, _ = pk.run(nthr)
         match = bool(np.array_equal(got, gpu_res[:count]))
-        med, rates, reps = passes(pk, nthr, 7, 0.7 * budget_s / 7)
-        med_free, rates_free, _ = passes(pk, nthr, 5, 0.3 * budget_s / 5, pin=False)
+        med, rates, reps = passes(pk, nthr, 7, budget_s / 7)
         one, _, _ = passes(pk, 1, 1, 0.5)
         pk.close()
         out.update({"value": round(med, 2), "kind": kind_s, "one_thread_GiBs": round(one, 2),
                     "passes_GiBs": [round(r, 1) for r in rates],
-                    "placement": f"one thread per L3 domain in turn ({min(nthr, ndom)} of {ndom} domains), "
-                                 f"first SMT siblings; CPUs {cpus}",
-                    "unpinned_GiBs": round(med_free, 2), "unpinned_passes_GiBs": [round(r, 1) for r in rates_free],
-                    "sample": sdesc + f"; median of 7 passes of {reps} sweeps on {nthr} pinned threads; CalculateChecksum "
+                    "sample": sdesc + f"; median of 7 passes of {reps} sweeps on {nthr} threads; CalculateChecksum "
                               f"(tcp-header.h:252-263) built -O3 -march=x86-64-v3; results == GPU results: {match}"})
         if R.RefLib.available("O0"):
             # secondary: the reference as its makefile builds it (-O0 -g, makefile:2), same threads
@@ -543,7 +507,7 @@ def cpu_baseline(host_arena, gpu_res, kind, count, L, budget_s, var_layout):
             med0, rates0, _ = passes(p0, nthr, 5, 0.3)
             p0.close()
             out["reference_O0_GiBs"] = round(med0, 2)
-            out["reference_O0_note"] = f"-O0 -g build (makefile:2), median of 5 passes on the same {nthr} pinned threads"
+            out["reference_O0_note"] = f"-O0 -g build (makefile:2), median of 5 passes on {nthr} threads"
     else:
         c = R.Ref16C(build=False)
         t0 = time.perf_counter()

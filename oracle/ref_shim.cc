@@ -13,9 +13,6 @@
 // uninitialised (tcp-header.h:270-273), see SURVEY.md section 8c.
 #include "tcp-header.h"
 
-#include <pthread.h>
-#include <sched.h>
-
 #include <chrono>
 #include <cstdint>
 #include <cstring>
@@ -139,37 +136,6 @@ double ref_packets_checksum_reps(void *handle, uint16_t *out, int nthreads, int 
   body(0, n / nthreads);
   for (auto &x : th) x.join();
   auto t1 = std::chrono::steady_clock::now();
-  return std::chrono::duration<double>(t1 - t0).count();
-}
-
-// Same, with thread t pinned to CPU cpus[t] (the caller's thread too, its
-// affinity restored afterwards): bench.py spreads the threads over the host's
-// L3 domains (one per CCD), whose links to memory bound a DRAM-sized pass.
-double ref_packets_checksum_reps_pinned(void *handle, uint16_t *out, int nthreads, int reps, const int *cpus) {
-  auto *h = static_cast<RefPackets *>(handle);
-  const size_t n = h->pkts.size();
-  if (nthreads < 1) nthreads = 1;
-  if (reps < 1) reps = 1;
-  auto pin = [&](int t) {
-    cpu_set_t set;
-    CPU_ZERO(&set);
-    CPU_SET(cpus[t], &set);
-    pthread_setaffinity_np(pthread_self(), sizeof(set), &set);
-  };
-  auto body = [&](int t, size_t lo, size_t hi) {
-    pin(t);
-    for (int r = 0; r < reps; ++r)
-      for (size_t k = lo; k < hi; ++k) out[k] = CalculateChecksum(*h->pkts[k]);
-  };
-  cpu_set_t saved;
-  const bool restore = pthread_getaffinity_np(pthread_self(), sizeof(saved), &saved) == 0;
-  auto t0 = std::chrono::steady_clock::now();
-  std::vector<std::thread> th;
-  for (int t = 1; t < nthreads; ++t) th.emplace_back(body, t, n * t / nthreads, n * (t + 1) / nthreads);
-  body(0, 0, n / nthreads);
-  for (auto &x : th) x.join();
-  auto t1 = std::chrono::steady_clock::now();
-  if (restore) pthread_setaffinity_np(pthread_self(), sizeof(saved), &saved);
   return std::chrono::duration<double>(t1 - t0).count();
 }
 
