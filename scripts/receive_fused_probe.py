@@ -71,6 +71,8 @@ def case(ctx, s, name, n, slot, ln, fixed_len=None):
             ("in-str WT", lambda: ctx.batch_receive(a, n, ok, hdr, kernel=S, param=96, **kw)),
             ("2 passes WT", lambda: ctx.batch_receive(a, n, ok, hdr, kernel=S, param=TWO | (1 << 27), **kw)),
             ("2 passes KH", lambda: ctx.batch_receive(a, n, ok, hdr, kernel=S, param=TWO | 16, **kw)),
+            ("concurrent", lambda: ctx.batch_receive(a, n, ok, hdr, kernel=S, param=1 << 26, **kw)),
+            ("concurrent A", lambda: ctx.batch_receive(a, n, ok, hdr, kernel=0, param=1 << 26, **kw)),
             ("AUTO", lambda: ctx.batch_receive(a, n, ok, hdr, **kw))]
     res = {}
     for label, fn in runs:

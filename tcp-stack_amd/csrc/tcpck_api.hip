@@ -42,6 +42,11 @@ struct tcpck_ctx {
   uint64_t stage_images = 0;
   uint64_t chunk_bytes = 64ull << 20;
   void *dbg = nullptr;  // tuning: per-wave time stamp buffer (tcpck_ctx_set_debug)
+
+  // RECEIVE's header pass run beside the VERIFY pass (created on first use)
+  std::mutex side_mu;
+  hipStream_t side = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
 };
 
 namespace {
@@ -166,7 +171,34 @@ int ensure_stage(tcpck_ctx *ctx, uint64_t bytes, uint64_t images) {
   return TCPCK_OK;
 }
 
+// The side stream and the two events that let RECEIVE's header pass run
+// concurrently with its VERIFY pass.  Created once per context, on first use.
+hipError_t ensure_side(tcpck_ctx *ctx) {
+  std::lock_guard<std::mutex> lk(ctx->side_mu);
+  if (ctx->side) return hipSuccess;
+  hipStream_t st = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  hipError_t e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&e0, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&e1, hipEventDisableTiming);
+  if (e != hipSuccess) {
+    if (e1) (void)hipEventDestroy(e1);
+    if (e0) (void)hipEventDestroy(e0);
+    if (st) (void)hipStreamDestroy(st);
+    return e;
+  }
+  ctx->fork = e0;
+  ctx->join = e1;
+  ctx->side = st;
+  return hipSuccess;
+}
+
 void free_stage(tcpck_ctx *ctx) {
+  if (ctx->side) {
+    (void)hipEventDestroy(ctx->fork);
+    (void)hipEventDestroy(ctx->join);
+    (void)hipStreamDestroy(ctx->side);
+  }
   for (int i = 0; i < 2; ++i) {
     if (ctx->stage[i]) (void)hipFree(ctx->stage[i]);
     if (ctx->stage_out[i]) (void)hipFree(ctx->stage_out[i]);
@@ -234,6 +266,7 @@ constexpr uint64_t kDeferFillMinVar = 1024;
 constexpr int kSstreamHdrStream = 32;    // sstream RECEIVE: headers from the stream's registers
 constexpr uint64_t kHdrStreamMaxLen = 256;  // ... for (typical) images up to this length
 constexpr int kProbeHdrWriteThrough = 1 << 27;  // probe builds: the header pass's array stores written through
+constexpr int kReceiveConcurrent = 1 << 26;     // RECEIVE into an array: the header pass beside VERIFY (side stream)
 // RECEIVE with an explicit kernel: the probe build fuses the headers into any
 // kernel that can (sstream's after-the-run conversion, HDR 1); the product
 // carries only the stream-register form (+ kSstreamHdrStream) and otherwise
@@ -973,6 +1006,31 @@ int tcpck_batch_receive_ex(tcpck_ctx *ctx, int mode, void *d_arena, uint64_t str
   auto *arena = static_cast<uint8_t *>(d_arena);
   auto *hdr = static_cast<uint8_t *>(d_hdr);
   const auto s = static_cast<hipStream_t>(stream);
+  if (param & kReceiveConcurrent) {
+    // the header pass on the context's side stream, beside the VERIFY pass on
+    // the caller's: it reads the same arena, writes only the header array
+    hipError_t e = ensure_side(ctx);
+    if (e != hipSuccess) return hip_status(e);
+    std::lock_guard<std::mutex> lk(ctx->side_mu);  // one fork / join at a time per context
+    tcpck::HeaderArgs h{};
+    h.arena = arena;
+    h.offsets = d_offsets;
+    h.stride = stride;
+    h.count = count;
+    h.out = hdr;
+    e = hipEventRecord(ctx->fork, s);
+    if (e == hipSuccess) e = hipStreamWaitEvent(ctx->side, ctx->fork, 0);
+    if (e == hipSuccess) e = tcpck::launch_header_swap(h, static_cast<uint32_t>(ctx->num_cus), ctx->side);
+    if (e == hipSuccess) {
+      const int p = param & ~kReceiveConcurrent;
+      e = d_offsets ? run_var(ctx, TCPCK_OP_VERIFY, mode, arena, d_offsets, d_lengths, 0, count, d_ok, layout, kernel,
+                              p, s)
+                    : run_fixed(ctx, TCPCK_OP_VERIFY, mode, arena, stride, len, count, d_ok, kernel, p, s);
+    }
+    const hipError_t e2 = hipEventRecord(ctx->join, ctx->side);
+    const hipError_t e3 = e2 == hipSuccess ? hipStreamWaitEvent(s, ctx->join, 0) : e2;
+    return hip_status(e != hipSuccess ? e : e3);
+  }
   return hip_status(d_offsets ? run_var(ctx, TCPCK_OP_RECEIVE, mode, arena, d_offsets, d_lengths, 0, count, d_ok,
                                         layout, kernel, param, s, hdr)
                               : run_fixed(ctx, TCPCK_OP_RECEIVE, mode, arena, stride, len, count, d_ok, kernel,
