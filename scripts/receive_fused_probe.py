@@ -89,11 +89,42 @@ def case(ctx, s, name, n, slot, ln, fixed_len=None):
     del a, hdr
 
 
+def sweep(ctx, s, rng, n):
+    """--sweep: VERIFY against the in-stream RECEIVE (param 32) over slot
+    sizes, grid multipliers M (param bits 16-23; 0 = the policy's) and block
+    orders (+4 default, else scattered)."""
+    mix = (np.asarray((64, 576, 1460), np.uint32)[rng.integers(0, 3, n)] + 32).astype(np.uint32)
+    img = int(mix.astype(np.int64).sum())
+    S = tcpck.KERNEL_SSTREAM
+    for slot in (1536, 2048, 2560, 4096):
+        off = np.arange(n, dtype=np.uint64) * np.uint64(slot)
+        a = torch.empty(n * slot, dtype=torch.uint8, device="cuda")
+        d_off, d_ln = torch.from_numpy(off).cuda(), torch.from_numpy(mix).cuda()
+        tcpck.synth_var(a, d_off, d_ln, int(mix.max()), n, seed=42)
+        ok = torch.empty(n, dtype=torch.uint8, device="cuda")
+        hdr = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
+        kw = dict(offsets=d_off, lengths=d_ln, total_bytes=img, min_len=int(mix.min()), max_len=int(mix.max()),
+                  sorted=True, stream=s)
+        for order in (0, 4):
+            for m in (0, 1, 2, 4, 8, 16):
+                p = (m << 16) | order
+                tv = b2b(lambda: ctx.batch_var_ex(tcpck.OP_VERIFY, a, d_off, d_ln, n, ok, kernel=S, param=p,
+                                                  total_bytes=img, min_len=int(mix.min()), max_len=int(mix.max()),
+                                                  sorted=True, stream=s), s)
+                tr = b2b(lambda: ctx.batch_receive(a, n, ok, hdr, kernel=S, param=p | 32, **kw), s)
+                print(f"slot {slot:5d} order {order} M {m:2d}   VERIFY {tv * 1e3:7.1f} us   in-stream RECEIVE "
+                      f"{tr * 1e3:7.1f} us   (+{(tr - tv) * 1e3:5.1f})", flush=True)
+        del a, hdr
+
+
 def main():
     ctx = tcpck.Context(0, probe=True)
     s = torch.cuda.current_stream()
     rng = np.random.default_rng(42)
     n = 1 << 20
+    if "--sweep" in sys.argv:
+        sweep(ctx, s, rng, n)
+        return
     mix = (np.asarray((64, 576, 1460), np.uint32)[rng.integers(0, 3, n)] + 32).astype(np.uint32)
     case(ctx, s, "ring 1M x 2048 (bench mix)", n, 2048, mix)
     case(ctx, s, "ring 1M x 1536 (bench mix)", n, 1536, mix)

@@ -266,7 +266,7 @@ constexpr uint64_t kDeferFillMinVar = 1024;
 constexpr int kSstreamHdrStream = 32;    // sstream RECEIVE: headers from the stream's registers
 constexpr uint64_t kHdrStreamMaxLen = 256;  // ... for (typical) images up to this length
 constexpr int kProbeHdrWriteThrough = 1 << 27;  // probe builds: the header pass's array stores written through
-constexpr int kReceiveConcurrent = 1 << 26;     // RECEIVE into an array: the header pass beside VERIFY (side stream)
+constexpr int kReceiveConcurrent = 1 << 26;  // probe builds: the header pass beside VERIFY on a side stream
 // RECEIVE with an explicit kernel: the probe build fuses the headers into any
 // kernel that can (sstream's after-the-run conversion, HDR 1); the product
 // carries only the stream-register form (+ kSstreamHdrStream) and otherwise
@@ -1006,6 +1006,7 @@ int tcpck_batch_receive_ex(tcpck_ctx *ctx, int mode, void *d_arena, uint64_t str
   auto *arena = static_cast<uint8_t *>(d_arena);
   auto *hdr = static_cast<uint8_t *>(d_hdr);
   const auto s = static_cast<hipStream_t>(stream);
+#ifdef TCPCK_PROBE
   if (param & kReceiveConcurrent) {
     // the header pass on the context's side stream, beside the VERIFY pass on
     // the caller's: it reads the same arena, writes only the header array
@@ -1031,6 +1032,7 @@ int tcpck_batch_receive_ex(tcpck_ctx *ctx, int mode, void *d_arena, uint64_t str
     const hipError_t e3 = e2 == hipSuccess ? hipStreamWaitEvent(s, ctx->join, 0) : e2;
     return hip_status(e != hipSuccess ? e : e3);
   }
+#endif
   return hip_status(d_offsets ? run_var(ctx, TCPCK_OP_RECEIVE, mode, arena, d_offsets, d_lengths, 0, count, d_ok,
                                         layout, kernel, param, s, hdr)
                               : run_fixed(ctx, TCPCK_OP_RECEIVE, mode, arena, stride, len, count, d_ok, kernel,

@@ -107,8 +107,16 @@ __device__ __forceinline__ uint32_t ref_chunk_sum_dot(u32x4 w) {
 
 // Raw buffer (SRSRC) loads: 32-bit lane offset + SGPR step offset, hardware
 // range check (bytes past `bytes` read as 0, no fault), nontemporal (aux 2).
+// Every caller passes wave-uniform values; readfirstlane says so to the
+// compiler, which otherwise wraps each load of a descriptor built from a
+// cross-lane result (a wave_max, a ds_swizzle) in a waterfall loop.
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *p, uint32_t bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), 0, static_cast<int>(bytes), 0x00020000);
+  const uint64_t a = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(a)));
+  const uint32_t hi = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(a >> 32)));
+  const int n = __builtin_amdgcn_readfirstlane(static_cast<int>(bytes));
+  void *u = reinterpret_cast<void *>((static_cast<uint64_t>(hi) << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(u, 0, n, 0x00020000);
 }
 // In-place 2-B store of a FILL result into the image's checksum field, with
 // the sc1 cache-policy bit: 4 % less time than a default-policy store for the

@@ -71,6 +71,17 @@ constexpr uint32_t kMaxRun = 128;             // images per run, variable layout
 constexpr int kPer = kMaxRun / 64;            // descriptors per lane
 constexpr uint32_t kOrderScatter = 0xFDu;     // block order: multiplicative scatter
 constexpr uint32_t kEnds = 2 * kMaxRun + 64;  // virtual ends (gap, image) + 64 read past the run
+// results staged in LDS and stored 64 at a time: a store inside the stream
+// loop counts in vmcnt beside the ring's loads, so every wait that follows it
+// also waits for a younger load.  <= 63 pending + <= 65 ends per step.
+constexpr uint32_t kResRing = 128;
+// HDR >= 2: header records staged the same way when every image of the run
+// is >= 64 B (>= 4 chunks: <= 17 images have header chunks in a step), 8
+// images (256 B) per flush: <= 7 complete + 1 partial pending + 17 < 32.
+// Runs with shorter images store each record as its chunk passes.
+constexpr uint32_t kHdrRing = 32;
+constexpr uint32_t kHdrFlush = 8;
+constexpr uint32_t kHdrStageMin = 64;
 
 struct SSArgs {
   uint8_t *arena;
@@ -117,6 +128,8 @@ __global__ void __launch_bounds__(kBlock) sstream_kernel(SSArgs a) {
   __shared__ uint32_t s_flag[kWavesPerBlock][FIXED ? 1 : 64];           // images starting at chunk q0 + l
   __shared__ __attribute__((aligned(16))) uint32_t s_pre[kWavesPerBlock][MODE == kRef ? 256 : 512];  // the step's prefix table
   __shared__ uint32_t s_fld[kWavesPerBlock][OP == kFill ? 64 : 1];      // kFill: field word + 1 per chunk
+  __shared__ uint16_t s_res[kWavesPerBlock][kResRing];                  // finished checksums awaiting their flush
+  __shared__ u32x4 s_hdr[kWavesPerBlock][HDR >= 2 ? 2 * kHdrRing : 1];  // HDR >= 2: host-order header halves
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wv = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6)));
   // kOrderScatter: block b takes run group (b P) mod nb, P prime > nb -- the
@@ -148,6 +161,7 @@ __global__ void __launch_bounds__(kBlock) sstream_kernel(SSArgs a) {
   uint32_t R = 0;    // buffer range from B (bytes, whole chunks)
   bool al4;          // every virtual end 4-B aligned: u32 prefix table
   bool hs = false;   // HDR >= 2: every header in its image's first two chunks (the stream emits them)
+  bool hst = false;  // HDR >= 2: and every image >= kHdrStageMin (the records staged in LDS)
   const uint32_t S = a.stride;
   const uint32_t L = FIXED ? a.len : 0u;
   const uint32_t n16 = FIXED ? a.nchunk << 4 : 0u;  // fixed: compacted bytes per image
@@ -159,6 +173,7 @@ __global__ void __launch_bounds__(kBlock) sstream_kernel(SSArgs a) {
     al4 = ((h | L) & 3u) == 0;
     if (OP == kFill) bad = L < 30;
     hs = h == 0 && L >= 32;
+    hst = L >= kHdrStageMin;
   } else {
     uint64_t o[kPer];
     uint32_t l[kPer];
@@ -170,7 +185,7 @@ __global__ void __launch_bounds__(kBlock) sstream_kernel(SSArgs a) {
     }
     B = dev::align16_rel(arena, dev::read_lane64(o[0], 0));
     uint32_t n[kPer], hh[kPer], r16[kPer], hi = 0;
-    bool ok = true, odd = false, shrt = false, hmis = false;
+    bool ok = true, odd = false, shrt = false, hmis = false, hsmall = false;
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
       const uint32_t j = kPer * lane + i;
@@ -190,10 +205,12 @@ __global__ void __launch_bounds__(kBlock) sstream_kernel(SSArgs a) {
       odd = odd || (in && ((hh[i] | l[i]) & 3u) != 0);
       shrt = shrt || (in && l[i] < 30);
       hmis = hmis || (in && (hh[i] != 0 || l[i] < 32));  // HDR >= 2: header not in chunks C_i, C_i + 1
+      hsmall = hsmall || (in && l[i] < kHdrStageMin);
     }
     bad = __ballot(!ok) != 0;
     al4 = __ballot(odd) == 0;
     hs = __ballot(hmis) == 0;
+    hst = __ballot(hsmall) == 0;
     if (OP == kFill) bad = bad || __ballot(shrt) != 0;
     uint32_t c[kPer];  // exclusive prefix of n inside the lane, then across the wave
     uint32_t lsum = 0;
@@ -225,6 +242,7 @@ __global__ void __launch_bounds__(kBlock) sstream_kernel(SSArgs a) {
   }
 
   hs = HDR >= 2 && hs && !bad && (reinterpret_cast<uintptr_t>(a.hdr) & 15u) == 0;
+  hst = hs && hst;
   if (!bad) {
     const uint32_t span = T << 4;  // compacted bytes; every end <= span
     const uint32_t nsteps = (T + 63) >> 6;
@@ -337,6 +355,31 @@ __global__ void __launch_bounds__(kBlock) sstream_kernel(SSArgs a) {
     }
 
     uint32_t carry = 0, p_last = 0, jn = 0, fj = 0;
+    uint32_t fl = 0;  // results stored: run images [0, fl)
+    auto flush = [&](uint32_t n) {  // the staged results of run images fl .. fl + n - 1
+      __builtin_amdgcn_wave_barrier();
+      if (lane < n) {
+        const uint16_t c = s_res[wv][(fl + lane) & (kResRing - 1)];
+        if constexpr (OP == kVerify)
+          static_cast<uint8_t *>(a.out)[kb + fl + lane] = c == 0 ? 1 : 0;
+        else if (a.out)
+          static_cast<uint16_t *>(a.out)[kb + fl + lane] = c;
+      }
+      fl += n;
+    };
+    uint32_t flh = 0;  // HDR >= 2: header records stored, run images [0, flh)
+    auto flush_hdr = [&](uint32_t n) {  // records of run images flh .. flh + n - 1, 16 B per lane
+      __builtin_amdgcn_wave_barrier();
+      if (lane < 2 * n) {
+        const u32x4 o = s_hdr[wv][(2 * flh + lane) & (2 * kHdrRing - 1)];
+        u32x4 *dst = reinterpret_cast<u32x4 *>(a.hdr + 32 * (kb + flh) + 16 * lane);
+        if constexpr (HDR == 3)  // write-through streaming store (probe)
+          asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt" ::"v"(dst), "v"(o) : "memory");
+        else
+          *dst = o;
+      }
+      flh += n;
+    };
     uint32_t e_last = 0;  // end of virtual jn - 1 (the stream start for jn = 0)
     auto stream_run = [&](auto al4_tag) {
       constexpr bool AL4 = decltype(al4_tag)::value;
@@ -353,11 +396,15 @@ __global__ void __launch_bounds__(kBlock) sstream_kernel(SSArgs a) {
               // reversed, 2/6 TcpLength/window swapped, 3 the ports, 7 urgent
               const u32x4 o{dev::n2h_dword(w.x, 0x00010203u), dev::n2h_dword(w.y, 0x00010203u),
                             dev::n2h_dword(w.z, 0x02030100u), dev::n2h_dword(w.w, (hk & 1u) ? 0x02030100u : 0x02030001u)};
-              u32x4 *dst = reinterpret_cast<u32x4 *>(a.hdr + 32 * (kb + (hk >> 1)) + 16 * (hk & 1u));
-              if constexpr (HDR == 3)  // write-through streaming store (probe)
-                asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt" ::"v"(dst), "v"(o) : "memory");
-              else
-                *dst = o;
+              if (hst) {
+                s_hdr[wv][hk & (2 * kHdrRing - 1)] = o;  // (image << 1 | half) mod the ring
+              } else {
+                u32x4 *dst = reinterpret_cast<u32x4 *>(a.hdr + 32 * (kb + (hk >> 1)) + 16 * (hk & 1u));
+                if constexpr (HDR == 3)  // write-through streaming store (probe)
+                  asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt" ::"v"(dst), "v"(o) : "memory");
+                else
+                  *dst = o;
+              }
             }
           }
           if (sb + 1024 > span && sb + (lane << 4) >= span) w = u32x4{0u, 0u, 0u, 0u};  // past the run
@@ -422,13 +469,10 @@ __global__ void __launch_bounds__(kBlock) sstream_kernel(SSArgs a) {
                   __builtin_amdgcn_update_dpp(static_cast<int>(e_last), static_cast<int>(e), 0x138, 0xF, 0xF, false));
             if (inb && (jj & 1u)) {  // an image end (odd virtual index)
               const uint32_t i = jj >> 1;
-              if constexpr (OP == kFill) {
-                const uint16_t cs = dev::finish<MODE>(P - pprev);  // tcp-header.h:262 (REF)
-                if (a.out) static_cast<uint16_t *>(a.out)[kb + i] = cs;
+              const uint16_t cs = dev::finish<MODE>(P - pprev);  // tcp-header.h:262 (REF)
+              s_res[wv][i & (kResRing - 1)] = cs;
+              if constexpr (OP == kFill)
                 if (!a.defer_field) dev::store16_field(rsrc, field_at(i, lane == 0 ? e_last : el), cs);  // raw, as the reference
-              } else {
-                store(kb + i, P - pprev, 0);
-              }
             }
             p_last = dev::read_lane(P, cnt - 1);
             e_last = dev::read_lane(e, cnt - 1);
@@ -438,6 +482,10 @@ __global__ void __launch_bounds__(kBlock) sstream_kernel(SSArgs a) {
             e = ends_at(jn);
           }
           __builtin_amdgcn_wave_barrier();  // the next step rewrites the table
+          while ((jn >> 1) - fl >= 64u) flush(64u);  // wave-uniform
+          if constexpr (HDR >= 2)
+            if (hst)
+              while ((jn >> 1) - flh >= kHdrFlush) flush_hdr(kHdrFlush);
           carry += dev::read_lane(incl, 63);
           ring[u] = load_step(st + U);
           hring[u] = hk_next;
@@ -448,6 +496,10 @@ __global__ void __launch_bounds__(kBlock) sstream_kernel(SSArgs a) {
       stream_run(std::true_type{});
     else
       stream_run(std::false_type{});
+    while (fl < (jn >> 1)) flush(min((jn >> 1) - fl, 64u));
+    if constexpr (HDR >= 2)  // every header chunk has passed: the rest of the records
+      if (hst)
+        while (flh < nimg) flush_hdr(min(nimg - flh, kHdrFlush));
     if (jn < nv) {  // ends exactly at the last step's end (= span): the first gets the rest
       const uint32_t rem = nv - jn;
       for (uint32_t i = lane; i < rem; i += 64) {
