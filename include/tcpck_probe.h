@@ -17,7 +17,12 @@ extern "C" {
  * (launch_patch_fields) -- each field's 64-B block read and written back whole
  * with d_out[k] (u16) patched in; no checksum is computed.  For timing the
  * pass apart from the stream (scripts/fill_drain_probe.py).  param = 1 + the
- * block stores' cache bits (sc0 1 | nt 2 | sc1 4), 0 = a plain store. */
+ * block stores' cache bits (sc0 1 | nt 2 | sc1 4), 0 = a plain store, | form
+ * << 4: 0 the 64-B block, 1 the 16-B chunk, 2 the 2-B field, 3 the 128-B line,
+ * 4-7 the 2-B write-through field with other thread maps, 12 the 32-B block;
+ * 8 / 9 / 10 / 11 the 64-B / 128-B / 16-B / 32-B block written without
+ * reading it (zeros around the field: destroys the images, whole-block write
+ * timing only). */
 #define TCPCK_KERNEL_PATCH 12
 
 /* Device buffer of 4 x u64 per wave receiving {start, end} s_memrealtime

@@ -77,6 +77,10 @@ def main():
                 ctx.batch_fixed_ex(tcpck.OP_FILL, arena, L, L, n, out, tcpck.KERNEL_PATCH, prm, stream=s)
         elif base == "instream26":  # in-stream 2-B field stores, sc0 sc1 nt
             f = lambda: ctx.batch_fixed_ex(tcpck.OP_FILL, arena, L, L, n, out, R, 26, stream=s)
+        elif base == "block":  # rstream variant 27: whole 64-B field blocks written from the stream
+            f = lambda: ctx.batch_fixed_ex(tcpck.OP_FILL, arena, L, L, n, out, R, 27, stream=s)
+        elif base == "blockend":  # variant 28: the run's blocks stored after its last load
+            f = lambda: ctx.batch_fixed_ex(tcpck.OP_FILL, arena, L, L, n, out, R, 28, stream=s)
         elif base == "instream":
             f = lambda: ctx.batch_fixed_ex(tcpck.OP_FILL, arena, L, L, n, out, R, 20, stream=s)
         else:

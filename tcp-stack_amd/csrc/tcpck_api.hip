@@ -173,6 +173,7 @@ int ensure_stage(tcpck_ctx *ctx, uint64_t bytes, uint64_t images) {
 
 // The side stream and the two events that let RECEIVE's header pass run
 // concurrently with its VERIFY pass.  Created once per context, on first use.
+#ifdef TCPCK_PROBE
 hipError_t ensure_side(tcpck_ctx *ctx) {
   std::lock_guard<std::mutex> lk(ctx->side_mu);
   if (ctx->side) return hipSuccess;
@@ -192,6 +193,7 @@ hipError_t ensure_side(tcpck_ctx *ctx) {
   ctx->side = st;
   return hipSuccess;
 }
+#endif
 
 void free_stage(tcpck_ctx *ctx) {
   if (ctx->side) {
@@ -266,7 +268,9 @@ constexpr uint64_t kDeferFillMinVar = 1024;
 constexpr int kSstreamHdrStream = 32;    // sstream RECEIVE: headers from the stream's registers
 constexpr uint64_t kHdrStreamMaxLen = 256;  // ... for (typical) images up to this length
 constexpr int kProbeHdrWriteThrough = 1 << 27;  // probe builds: the header pass's array stores written through
+#ifdef TCPCK_PROBE
 constexpr int kReceiveConcurrent = 1 << 26;  // probe builds: the header pass beside VERIFY on a side stream
+#endif
 // RECEIVE with an explicit kernel: the probe build fuses the headers into any
 // kernel that can (sstream's after-the-run conversion, HDR 1); the product
 // carries only the stream-register form (+ kSstreamHdrStream) and otherwise
@@ -528,7 +532,7 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
     pa.count = count;
     pa.sums = static_cast<uint16_t *>(out);
     pa.hi = (count - 1) * stride + len;
-    pa.store_bits = static_cast<uint32_t>(param & 0x7F);  // 1 + sc0 1 | nt 2 | sc1 4 (0 = plain) | form << 4
+    pa.store_bits = static_cast<uint32_t>(param & 0xFF);  // 1 + sc0 1 | nt 2 | sc1 4 (0 = plain) | form << 4
     return tcpck::launch_patch_fields(pa, static_cast<uint32_t>(ctx->num_cus), s);
   }
 #endif

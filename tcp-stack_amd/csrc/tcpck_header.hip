@@ -136,8 +136,10 @@ hipError_t launch_patch(const PatchArgs &a, uint32_t num_cus, hipStream_t stream
 // granularities and store policies.  GRAN 0: four lanes per image, the field's
 // 64-B block read and written back whole (AUTO's form in round 2); 1: one lane,
 // the 16-B chunk holding the field; 2: the 2-B field alone (no read); 3: eight
-// lanes, the field's 128-B line.  BITS: store cache bits sc0 1 | nt 2 | sc1 4,
-// -1 a plain C++ store.
+// lanes, the field's 128-B line; 4: two lanes, the field's 32-B block.  BLIND:
+// the block written without reading it (zeros around the field: destroys the
+// images, timing of whole-block writes only).  BITS: store cache bits sc0 1 |
+// nt 2 | sc1 4, -1 a plain C++ store.
 template <int BITS>
 __device__ __forceinline__ void store_block(dev::u32x4 *p, dev::u32x4 v) {
   if constexpr (BITS < 0) {
@@ -161,9 +163,9 @@ __device__ __forceinline__ void store_block(dev::u32x4 *p, dev::u32x4 v) {
   }
 }
 
-template <int GRAN, int BITS>
+template <int G, bool BLIND, int BITS>
 __global__ void __launch_bounds__(kBlock) patch_probe_kernel(PatchArgs a) {
-  constexpr int LPI = GRAN == 3 ? 8 : (GRAN == 0 ? 4 : 1);  // lanes per image
+  constexpr int LPI = G == 3 ? 8 : (G == 0 ? 4 : (G == 4 ? 2 : 1));  // lanes per image
   const uint64_t step = static_cast<uint64_t>(gridDim.x) * kBlock;
   const uint64_t total = a.count * LPI;
   const uint64_t base = reinterpret_cast<uint64_t>(a.arena);
@@ -172,7 +174,7 @@ __global__ void __launch_bounds__(kBlock) patch_probe_kernel(PatchArgs a) {
     const uint32_t j = static_cast<uint32_t>(t % LPI);
     const uint64_t f = k * a.stride + 28;
     const uint16_t c = a.sums[k];
-    if constexpr (GRAN == 2) {
+    if constexpr (G == 2) {
       uint16_t *p = reinterpret_cast<uint16_t *>(a.arena + f);
       const uint32_t v = c;
       if constexpr (BITS == 7)
@@ -182,14 +184,14 @@ __global__ void __launch_bounds__(kBlock) patch_probe_kernel(PatchArgs a) {
       else
         *p = c;
     } else {
-      const uint64_t gm = GRAN == 3 ? 127 : (GRAN == 0 ? 63 : 15);
+      const uint64_t gm = G == 3 ? 127 : (G == 0 ? 63 : (G == 4 ? 31 : 15));
       const uint64_t blk = ((base + f) & ~gm) - base;
-      if (GRAN != 1 && (blk < a.lo || blk + gm + 1 > a.hi)) {  // the block would leave the batch
+      if (G != 1 && (blk < a.lo || blk + gm + 1 > a.hi)) {  // the block would leave the batch
         if (j == 0) *reinterpret_cast<uint16_t *>(a.arena + f) = c;
         continue;
       }
       dev::u32x4 *p = reinterpret_cast<dev::u32x4 *>(a.arena + blk) + j;
-      dev::u32x4 v = *p;
+      dev::u32x4 v = BLIND ? dev::u32x4{0u, 0u, 0u, 0u} : *p;
       const uint32_t r = static_cast<uint32_t>(f - blk) - 16 * j;
       if (r < 16) {
         const uint32_t sh = 16 * ((r >> 1) & 1);
@@ -233,31 +235,31 @@ __global__ void __launch_bounds__(kBlock) patch_map_kernel(PatchArgs a) {
   }
 }
 
-template <int GRAN, int BITS>
+template <int G, bool BLIND, int BITS>
 hipError_t launch_patch_probe(const PatchArgs &a, uint32_t num_cus, hipStream_t stream) {
-  static const uint32_t per_cu = dev::resident_blocks_per_cu(patch_probe_kernel<GRAN, BITS>);
-  const uint64_t lpi = GRAN == 3 ? 8 : (GRAN == 0 ? 4 : 1);
+  static const uint32_t per_cu = dev::resident_blocks_per_cu(patch_probe_kernel<G, BLIND, BITS>);
+  const uint64_t lpi = G == 3 ? 8 : (G == 0 ? 4 : (G == 4 ? 2 : 1));
   uint64_t blocks = (a.count * lpi + kBlock - 1) / kBlock;
   const uint64_t cap = static_cast<uint64_t>(per_cu) * num_cus * 8;
   if (blocks > cap) blocks = cap;
-  hipLaunchKernelGGL((patch_probe_kernel<GRAN, BITS>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0, stream,
+  hipLaunchKernelGGL((patch_probe_kernel<G, BLIND, BITS>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0, stream,
                      a);
   return hipGetLastError();
 }
 
 // store_bits = 1 + BITS (0: plain) | GRAN << 4
-template <int GRAN>
+template <int G, bool BLIND = false>
 hipError_t probe_by_bits(const PatchArgs &a, uint32_t num_cus, hipStream_t stream) {
   switch (static_cast<int>(a.store_bits & 15) - 1) {
-    case -1: return launch_patch_probe<GRAN, -1>(a, num_cus, stream);
-    case 0: return launch_patch_probe<GRAN, 0>(a, num_cus, stream);
-    case 1: return launch_patch_probe<GRAN, 1>(a, num_cus, stream);
-    case 2: return launch_patch_probe<GRAN, 2>(a, num_cus, stream);
-    case 3: return launch_patch_probe<GRAN, 3>(a, num_cus, stream);
-    case 4: return launch_patch_probe<GRAN, 4>(a, num_cus, stream);
-    case 5: return launch_patch_probe<GRAN, 5>(a, num_cus, stream);
-    case 6: return launch_patch_probe<GRAN, 6>(a, num_cus, stream);
-    case 7: return launch_patch_probe<GRAN, 7>(a, num_cus, stream);
+    case -1: return launch_patch_probe<G, BLIND, -1>(a, num_cus, stream);
+    case 0: return launch_patch_probe<G, BLIND, 0>(a, num_cus, stream);
+    case 1: return launch_patch_probe<G, BLIND, 1>(a, num_cus, stream);
+    case 2: return launch_patch_probe<G, BLIND, 2>(a, num_cus, stream);
+    case 3: return launch_patch_probe<G, BLIND, 3>(a, num_cus, stream);
+    case 4: return launch_patch_probe<G, BLIND, 4>(a, num_cus, stream);
+    case 5: return launch_patch_probe<G, BLIND, 5>(a, num_cus, stream);
+    case 6: return launch_patch_probe<G, BLIND, 6>(a, num_cus, stream);
+    case 7: return launch_patch_probe<G, BLIND, 7>(a, num_cus, stream);
     default: return hipErrorInvalidValue;
   }
 }
@@ -270,7 +272,7 @@ hipError_t launch_patch_fields(const PatchArgs &a, uint32_t num_cus, hipStream_t
   if (!a.sums) return hipErrorInvalidValue;
 #ifdef TCPCK_PROBE
   if (a.store_bits && !a.update && !a.offsets) {  // timing forms (TCPCK_KERNEL_PATCH param)
-    if ((a.store_bits >> 4) >= 4) {  // the 2-B write-through pass with other maps
+    if ((a.store_bits >> 4) >= 4 && (a.store_bits >> 4) < 8) {  // the 2-B write-through pass with other maps
       static const uint32_t per_cu = 8;
       const int map = static_cast<int>(a.store_bits >> 4) - 4;
       uint64_t blocks = (a.count + kBlock - 1) / kBlock;
@@ -291,6 +293,11 @@ hipError_t launch_patch_fields(const PatchArgs &a, uint32_t num_cus, hipStream_t
       case 1: return probe_by_bits<1>(a, num_cus, stream);
       case 2: return probe_by_bits<2>(a, num_cus, stream);
       case 3: return a.stride >= 128 ? probe_by_bits<3>(a, num_cus, stream) : hipErrorInvalidValue;
+      case 8: return a.stride >= 64 ? probe_by_bits<0, true>(a, num_cus, stream) : hipErrorInvalidValue;
+      case 9: return a.stride >= 128 ? probe_by_bits<3, true>(a, num_cus, stream) : hipErrorInvalidValue;
+      case 10: return probe_by_bits<1, true>(a, num_cus, stream);
+      case 11: return a.stride >= 32 ? probe_by_bits<4, true>(a, num_cus, stream) : hipErrorInvalidValue;
+      case 12: return a.stride >= 32 ? probe_by_bits<4>(a, num_cus, stream) : hipErrorInvalidValue;
       default: return hipErrorInvalidValue;
     }
   }

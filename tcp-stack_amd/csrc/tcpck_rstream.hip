@@ -50,6 +50,10 @@ using dev::u32x4;
 // the step offset in an SGPR instead of per-lane 64-bit clamped addresses;
 // bit 2 (with bit 1): the run's first step read with the default cache policy;
 // bit 3 (with bit 1): every step read with the default cache policy;
+// bit 5 (kFill, stride >= 128): each field's whole 64-B block written back
+// from the stream's own registers with the checksum in place, write-through
+// (sc0 sc1 nt) -- a whole-block store needs no read-modify-write of the line,
+// a 2-B store does (scripts/fill_drain_probe.py, profiles/r03/fill_blind.log);
 // a.order (runtime): the block order, dev::ordered_block -- with the XCD
 // orders each XCD streams compact regions instead of every eighth run
 // (measured +4% at C2; the HBM bytes do not change), and
@@ -59,7 +63,13 @@ using dev::u32x4;
 // images < 128 KiB) and RFC 1071 folds it like any other sum
 template <int U, int OP, bool STAMP, int PRIO = 0, int FLAV = 0, int MODE = kRef>
 __global__ void __launch_bounds__(kBlock) rstream_kernel(FixedStreamArgs a) {
+  // SECT: the field blocks of the run's images, staged as the stream passes
+  // them (image j in slot j mod 32) until 16 results are ready.  Fields are
+  // >= 128 B apart: <= 15 staged and waiting + <= 9 staged per step < 32
+  constexpr bool SECT = OP == kFill && (FLAV & 32) != 0;
+  __shared__ u32x4 s_sec[kWavesPerBlock][SECT ? 32 * 4 : 1];
   const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wv = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6)));
   // readfirstlane: the wave index is uniform, but hipcc cannot prove anything
   // derived from threadIdx is; without it every boundary variable below lives
   // in VGPRs and each uniform test becomes an exec-masked region
@@ -128,6 +138,11 @@ __global__ void __launch_bounds__(kBlock) rstream_kernel(FixedStreamArgs a) {
   // j's end by more than a step (images >= 30 B hold <= 35 fields per KiB),
   // so no slot is reused before it is consumed.
   uint32_t fstage = 0;
+  uint32_t ns = lead + 28;  // SECT: the field whose block is being staged, of run image js
+  uint32_t js = 0;
+  // SECT + FLAV bit 6 (probe): a run of <= 32 images keeps every block in LDS
+  // and stores them after its last load -- no store shares vmcnt with the ring
+  const bool end_flush = SECT && (FLAV & 64) != 0 && nimg <= 32;
   uint32_t carry = 0;       // P at the step start
   uint32_t p_last = 0;      // P at the latest boundary (run start: 0)
   // results staged in lane (j - out_rel) until 64 are ready
@@ -142,7 +157,7 @@ __global__ void __launch_bounds__(kBlock) rstream_kernel(FixedStreamArgs a) {
         static_cast<uint8_t *>(a.out)[k] = (c == 0) ? 1 : 0;
       } else {
         if (a.out) static_cast<uint16_t *>(a.out)[k] = c;
-        if (OP == kFill && !a.defer_field) {
+        if (OP == kFill && !a.defer_field && !SECT) {
           if constexpr (FLAV & 16)  // write-through streaming store (sc0 sc1 nt): not left dirty in the MALL
             __builtin_amdgcn_raw_buffer_store_b16(c, rsrc, static_cast<int>((out_rel + lane) * S + lead + 28), 0, 19);
           else
@@ -151,10 +166,39 @@ __global__ void __launch_bounds__(kBlock) rstream_kernel(FixedStreamArgs a) {
       }
     }
   };
+  // SECT: the blocks of run images j0 .. j0 + n - 1 (n <= 16), four lanes per
+  // block, each image's checksum from its staging lane
+  auto flush_sect = [&](uint32_t j0, uint32_t n) {
+    const uint32_t i = j0 + (lane >> 2), c = lane & 3u;
+    const uint32_t cs = static_cast<uint32_t>(__shfl(static_cast<int>(stage), static_cast<int>((i - out_rel) & 63u), 64));
+    if (lane < 4 * n) {
+      const uint32_t f = lead + 28 + i * S;  // the field, run-relative
+      const uint32_t b = f & ~63u;           // its block (A0 is 128-B aligned: so is the block in memory)
+      const uint32_t o = f & 63u;
+      u32x4 v = s_sec[wv][((i & 31u) << 2) | c];
+      if ((o >> 4) == c) {  // the field's chunk: the checksum into bytes o, o + 1 (tcp-header.h:177)
+        const uint32_t di = (o & 15u) >> 2;
+        const uint32_t sh = (o & 2u) << 3;
+        const uint32_t m = ~(0xFFFFu << sh), x = (cs & 0xFFFFu) << sh;
+        v.x = di == 0 ? (v.x & m) | x : v.x;
+        v.y = di == 1 ? (v.y & m) | x : v.y;
+        v.z = di == 2 ? (v.z & m) | x : v.z;
+        v.w = di == 3 ? (v.w & m) | x : v.w;
+      }
+      if (static_cast<int64_t>(A0) + static_cast<int64_t>(b) >= 0) {
+        typedef unsigned v4u __attribute__((ext_vector_type(4)));
+        __builtin_amdgcn_raw_buffer_store_b128(v4u{v.x, v.y, v.z, v.w}, rsrc, static_cast<int>(b + 16 * c), 0, 19);
+      } else if ((o >> 4) == c) {  // the block starts before the arena: the field alone
+        dev::store16_field(rsrc, f, static_cast<uint16_t>(cs));
+      }
+    }
+  };
   auto emit = [&](uint32_t jr, uint32_t sum) {  // jr = run-relative image index, sum = its word sum
     if constexpr (OP == kFill) sum -= dev::read_lane(fstage, jr & 63u);
     const uint32_t j = jr - out_rel;
     stage = lane == j ? static_cast<uint32_t>(dev::finish<MODE>(sum)) : stage;  // j, sum wave-uniform: v_cmp + v_cndmask
+    if constexpr (SECT)
+      if (!end_flush && (j & 15u) == 15u) flush_sect(jr - 15u, 16u);
     if (j == 63) {
       flush(64);
       out_rel += 64;
@@ -182,6 +226,17 @@ __global__ void __launch_bounds__(kBlock) rstream_kernel(FixedStreamArgs a) {
       const uint32_t st = g + u;  // steps past nsteps: masked to zero, no boundary, harmless
       const uint32_t sb = st << 10;
       u32x4 w = ring[u];
+      if constexpr (SECT) {  // the field blocks passing through this step, before the run-edge mask
+        const uint32_t q = sb + (lane << 4);
+        while (js < nimg) {
+          const uint32_t b = ns & ~63u;
+          if (b >= sb + 1024) break;
+          if ((q & ~63u) == b) s_sec[wv][((js & 31u) << 2) | ((q >> 4) & 3u)] = w;
+          if (b + 64 > sb + 1024) break;  // the block's other chunks come with the next step
+          ns += S;
+          ++js;
+        }
+      }
       if (sb == 0 || sb + 1024 > span) {  // run edge (wave-uniform): keep words of [lead, span) only
         const int32_t crel = static_cast<int32_t>(sb + (lane << 4));
         const int32_t lo = min(max(static_cast<int32_t>(lead) - crel, 0), 16);
@@ -219,6 +274,13 @@ __global__ void __launch_bounds__(kBlock) rstream_kernel(FixedStreamArgs a) {
     }
   }
   emit(nimg - 1, carry - p_last);  // the last image ends at the run end
+  if constexpr (SECT) {
+    if (end_flush) {  // every block of the run after its last load
+      for (uint32_t j0 = 0; j0 < nimg; j0 += 16) flush_sect(j0, min(nimg - j0, 16u));
+    } else if (nimg & 15u) {
+      flush_sect(nimg & ~15u, nimg & 15u);
+    }
+  }
   const uint32_t pending = nimg - out_rel;
   if (pending) flush(pending);
   if (STAMP && lane == 0 && a.dbg) {
@@ -305,6 +367,18 @@ hipError_t launch_rstream(int op, int variant, const FixedStreamArgs &a, uint32_
       FixedStreamArgs b = a;
       b.order = 4u;
       return dispatch<4, false, 0, 11>(op, b, num_cus, stream);
+    }
+    case 27: {  // 20 with FILL's whole field blocks written from the stream (FLAV bit 5)
+      if (a.stride < 128 || a.defer_field) return hipErrorInvalidValue;
+      FixedStreamArgs b = a;
+      b.order = 4u;
+      return dispatch<4, false, 0, 39>(op, b, num_cus, stream);
+    }
+    case 28: {  // 27 with a short run's blocks stored after the run's last load (FLAV bit 6)
+      if (a.stride < 128 || a.defer_field) return hipErrorInvalidValue;
+      FixedStreamArgs b = a;
+      b.order = 4u;
+      return dispatch<4, false, 0, 103>(op, b, num_cus, stream);
     }
     case 26: {  // 20 with the FILL field stores write-through streaming (sc0 sc1 nt, FLAV bit 4)
       FixedStreamArgs b = a;

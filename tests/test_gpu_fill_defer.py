@@ -95,10 +95,11 @@ def test_fill_auto_rstream(ctx, length, with_out):
     np.testing.assert_array_equal(buf.cpu().numpy(), exp)
 
 
-@pytest.mark.parametrize("form", [0x00, 0x08, 0x07, 0x18, 0x10, 0x28, 0x27, 0x20, 0x38, 0x30])
+@pytest.mark.parametrize("form", [0x00, 0x08, 0x07, 0x18, 0x10, 0x28, 0x27, 0x20, 0x38, 0x30, 0xC8, 0xC0])
 def test_field_pass_forms(ctx, form):
     """TCPCK_KERNEL_PATCH (libtcpck_probe.so): the field pass alone, every
-    granularity (form >> 4: 64-B block, 16-B chunk, 2-B field, 128-B line) and
+    granularity (form >> 4: 64-B block, 16-B chunk, 2-B field, 128-B line, 12:
+    32-B block) and
     store policy (form & 15: 1 + cache bits, 0 plain) stores out[k] into bytes
     28-29 of image k and leaves every other byte as it was."""
     import tcpck
@@ -114,3 +115,42 @@ def test_field_pass_forms(ctx, form):
     for k in range(count):
         exp[mis + k * L + 28:mis + k * L + 30] = sums[k:k + 1].view(np.uint8)
     np.testing.assert_array_equal(buf.cpu().numpy(), exp)
+
+
+@pytest.mark.parametrize("length", [128, 130, 190, 512, 514, 1024, 1460, 1492, 2048, 4094, 9000, 16384])
+@pytest.mark.parametrize("mis", [0, 2, 36, 126])
+@pytest.mark.parametrize("count", [1, 17, 20000])
+@pytest.mark.parametrize("with_out", [True, False])
+@pytest.mark.parametrize("variant", [27, 28])
+def test_fill_block_vs_oracle(ctx, length, mis, count, with_out, variant):
+    """rstream variants 27 / 28 (libtcpck_probe.so): each field's whole 64-B
+    block written from the stream's registers with the checksum in place (28:
+    a short run's blocks after its last load).  Every
+    arena byte (the blocks also hold the previous image's tail), the bytes
+    before and after the batch, and the results against the oracle's FILL
+    (socket-manager.cc:9-10); misalignments put image 0's block before the
+    arena (the field stored alone)."""
+    import tcpck
+    from oracle import ref16 as R
+    rng = np.random.default_rng(length * 8 + mis + count + with_out + variant)
+    count = max(1, min(count, (8 << 20) // length))
+    a = rng.integers(0, 256, count * length + 256, dtype=np.uint8)
+    buf = torch.from_numpy(a).cuda()
+    out = torch.empty(count, dtype=torch.int16, device="cuda") if with_out else None
+    ctx.batch_fixed_ex(tcpck.OP_FILL, buf.data_ptr() + mis, length, length, count, out, tcpck.KERNEL_RSTREAM,
+                       variant)
+    torch.cuda.synchronize()
+    exp = a.copy()
+    v = exp[mis:]
+    want = np.array([R.fill_np(v[k * length:(k + 1) * length]) for k in range(count)], np.uint16)
+    if with_out:
+        np.testing.assert_array_equal(out.cpu().numpy().view(np.uint16), want)
+    np.testing.assert_array_equal(buf.cpu().numpy(), exp)
+
+
+def test_fill_block_rejects(ctx):
+    import tcpck
+    a = torch.zeros(1 << 16, dtype=torch.uint8, device="cuda")
+    out = torch.empty(1024, dtype=torch.int16, device="cuda")
+    with pytest.raises(tcpck.TcpckError):  # fields < 128 B apart: blocks would overlap a neighbour's
+        ctx.batch_fixed_ex(tcpck.OP_FILL, a, 96, 96, 64, out, tcpck.KERNEL_RSTREAM, 27)
