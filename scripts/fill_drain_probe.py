@@ -79,8 +79,6 @@ def main():
             f = lambda: ctx.batch_fixed_ex(tcpck.OP_FILL, arena, L, L, n, out, R, 26, stream=s)
         elif base == "block":  # rstream variant 27: whole 64-B field blocks written from the stream
             f = lambda: ctx.batch_fixed_ex(tcpck.OP_FILL, arena, L, L, n, out, R, 27, stream=s)
-        elif base == "phase":  # variant 29: the resident grid streams, then stores the 32-B field blocks
-            f = lambda: ctx.batch_fixed_ex(tcpck.OP_FILL, arena, L, L, n, out, R, 29, stream=s)
         elif base == "blockend":  # variant 28: the run's blocks stored after its last load
             f = lambda: ctx.batch_fixed_ex(tcpck.OP_FILL, arena, L, L, n, out, R, 28, stream=s)
         elif base == "instream":

@@ -43,10 +43,6 @@ struct tcpck_ctx {
   uint64_t chunk_bytes = 64ull << 20;
   void *dbg = nullptr;  // tuning: per-wave time stamp buffer (tcpck_ctx_set_debug)
 
-  // probe: rstream 29's grid-barrier counter (device) and its running target
-  uint64_t *bar = nullptr;
-  uint64_t bar_epoch = 0;
-
   // RECEIVE's header pass run beside the VERIFY pass (created on first use)
   std::mutex side_mu;
   hipStream_t side = nullptr;
@@ -200,7 +196,6 @@ hipError_t ensure_side(tcpck_ctx *ctx) {
 #endif
 
 void free_stage(tcpck_ctx *ctx) {
-  if (ctx->bar) (void)hipFree(ctx->bar);
   if (ctx->side) {
     (void)hipEventDestroy(ctx->fork);
     (void)hipEventDestroy(ctx->join);
@@ -430,19 +425,6 @@ hipError_t run_fixed_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint
     a.blocks_per_cu = static_cast<uint32_t>(param >> 8) & 0xFFu;
     a.oversub = static_cast<uint32_t>(param >> 16) & 0xFFu;
     int variant = param & 0xFF;
-#ifdef TCPCK_PROBE
-    if (variant == 29) {  // the phased FILL: a zeroed barrier counter, created once
-      std::lock_guard<std::mutex> lk(ctx->side_mu);
-      if (!ctx->bar) {
-        hipError_t e = hipMalloc(reinterpret_cast<void **>(&ctx->bar), sizeof(uint64_t));
-        if (e == hipSuccess) e = hipMemset(ctx->bar, 0, sizeof(uint64_t));
-        if (e != hipSuccess) return e;
-        ctx->bar_epoch = 0;
-      }
-      a.bar = ctx->bar;
-      a.bar_epoch = &ctx->bar_epoch;
-    }
-#endif
     if (variant == kRstreamDeferFill) {  // FILL: the policy's stream, the fields in a second pass
       if (op != TCPCK_OP_FILL || !out || stride < 30) return hipErrorInvalidValue;
       a.defer_field = 1;

@@ -76,12 +76,6 @@ struct FixedStreamArgs {
   uint32_t order;          // block order (dev::ordered_block; 0xFF default)
   int mode;                // kRef, or kRfc1071 (variant 20 only)
   uint32_t defer_field;    // kFill: results to out only, the fields left for launch_patch_fields
-  // probe (rstream 29): the grid barrier between the stream phase and the
-  // field-block phase -- a monotonic device counter, the value this launch
-  // waits for, and the host-side running total the launcher advances
-  uint64_t *bar;
-  uint64_t bar_target;
-  uint64_t *bar_epoch;
 };
 
 // Fixed stride == len == S, S a power of two in [32, 1024], 16-B aligned arena

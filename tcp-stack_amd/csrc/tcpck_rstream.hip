@@ -54,11 +54,6 @@ using dev::u32x4;
 // from the stream's own registers with the checksum in place, write-through
 // (sc0 sc1 nt) -- a whole-block store needs no read-modify-write of the line,
 // a 2-B store does (scripts/fill_drain_probe.py, profiles/r03/fill_blind.log);
-// bit 7 (kFill, probe): PHASE -- every field's 32-B block of the wave's run
-// (<= kPhaseCap images) kept in LDS with its checksum patched in, and stored
-// only after a bounded grid barrier: the whole grid streams first, then
-// writes (field stores interleaved with the read stream cost ~2x their
-// separate pass, profiles/r03/fill_block_instream.log)
 // a.order (runtime): the block order, dev::ordered_block -- with the XCD
 // orders each XCD streams compact regions instead of every eighth run
 // (measured +4% at C2; the HBM bytes do not change), and
@@ -73,9 +68,6 @@ __global__ void __launch_bounds__(kBlock) rstream_kernel(FixedStreamArgs a) {
   // >= 128 B apart: <= 15 staged and waiting + <= 9 staged per step < 32
   constexpr bool SECT = OP == kFill && (FLAV & 32) != 0;
   __shared__ u32x4 s_sec[kWavesPerBlock][SECT ? 32 * 4 : 1];
-  constexpr bool PHASE = OP == kFill && (FLAV & 128) != 0;
-  constexpr uint32_t kPhaseCap = 144;  // 4.5 KiB of LDS per wave: 8 blocks per CU
-  __shared__ u32x4 s_blk[kWavesPerBlock][PHASE ? 2 * kPhaseCap : 1];
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wv = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6)));
   // readfirstlane: the wave index is uniform, but hipcc cannot prove anything
@@ -104,14 +96,7 @@ __global__ void __launch_bounds__(kBlock) rstream_kernel(FixedStreamArgs a) {
   }
   uint64_t kb, ke;
   dev::count_split(wid, a.per_wave, a.rem, kb, ke);
-  // PHASE: every wave arrives at the barrier once (one vector atomic by lane 0)
-  auto arrive = [&]() {
-    if (PHASE && a.bar && lane == 0) __hip_atomic_fetch_add(a.bar, uint64_t{1}, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  };
-  if (kb >= ke) {
-    arrive();
-    return;
-  }
+  if (kb >= ke) return;
   const uint32_t S = static_cast<uint32_t>(a.stride);
   const uint64_t s0 = kb * S;
   const uint64_t A0 = dev::align128_rel(a.arena, s0);
@@ -158,7 +143,6 @@ __global__ void __launch_bounds__(kBlock) rstream_kernel(FixedStreamArgs a) {
   // SECT + FLAV bit 6 (probe): a run of <= 32 images keeps every block in LDS
   // and stores them after its last load -- no store shares vmcnt with the ring
   const bool end_flush = SECT && (FLAV & 64) != 0 && nimg <= 32;
-  const bool phase = PHASE && nimg <= kPhaseCap;  // else the fields go out with the results (flush)
   uint32_t carry = 0;       // P at the step start
   uint32_t p_last = 0;      // P at the latest boundary (run start: 0)
   // results staged in lane (j - out_rel) until 64 are ready
@@ -173,7 +157,7 @@ __global__ void __launch_bounds__(kBlock) rstream_kernel(FixedStreamArgs a) {
         static_cast<uint8_t *>(a.out)[k] = (c == 0) ? 1 : 0;
       } else {
         if (a.out) static_cast<uint16_t *>(a.out)[k] = c;
-        if (OP == kFill && !a.defer_field && !SECT && !phase) {
+        if (OP == kFill && !a.defer_field && !SECT) {
           if constexpr (FLAV & 16)  // write-through streaming store (sc0 sc1 nt): not left dirty in the MALL
             __builtin_amdgcn_raw_buffer_store_b16(c, rsrc, static_cast<int>((out_rel + lane) * S + lead + 28), 0, 19);
           else
@@ -213,10 +197,6 @@ __global__ void __launch_bounds__(kBlock) rstream_kernel(FixedStreamArgs a) {
     if constexpr (OP == kFill) sum -= dev::read_lane(fstage, jr & 63u);
     const uint32_t j = jr - out_rel;
     stage = lane == j ? static_cast<uint32_t>(dev::finish<MODE>(sum)) : stage;  // j, sum wave-uniform: v_cmp + v_cndmask
-    if constexpr (PHASE)
-      if (phase && lane == 0)  // the checksum into the staged block (its field bytes, tcp-header.h:177)
-        reinterpret_cast<uint16_t *>(&s_blk[wv][0])[(jr * 32u + ((lead + 28 + jr * S) & 31u)) >> 1] =
-            dev::finish<MODE>(sum);
     if constexpr (SECT)
       if (!end_flush && (j & 15u) == 15u) flush_sect(jr - 15u, 16u);
     if (j == 63) {
@@ -246,19 +226,6 @@ __global__ void __launch_bounds__(kBlock) rstream_kernel(FixedStreamArgs a) {
       const uint32_t st = g + u;  // steps past nsteps: masked to zero, no boundary, harmless
       const uint32_t sb = st << 10;
       u32x4 w = ring[u];
-      if constexpr (PHASE) {  // the 32-B field blocks passing through this step, before the run-edge mask
-        if (phase) {
-          const uint32_t q = sb + (lane << 4);
-          while (js < nimg) {
-            const uint32_t b = ns & ~31u;
-            if (b >= sb + 1024) break;
-            if ((q & ~31u) == b) s_blk[wv][(js << 1) | ((q >> 4) & 1u)] = w;
-            if (b + 32 > sb + 1024) break;  // the block's second chunk comes with the next step
-            ns += S;
-            ++js;
-          }
-        }
-      }
       if constexpr (SECT) {  // the field blocks passing through this step, before the run-edge mask
         const uint32_t q = sb + (lane << 4);
         while (js < nimg) {
@@ -316,32 +283,6 @@ __global__ void __launch_bounds__(kBlock) rstream_kernel(FixedStreamArgs a) {
   }
   const uint32_t pending = nimg - out_rel;
   if (pending) flush(pending);
-  if constexpr (PHASE) {
-    arrive();
-    if (phase) {
-      if (a.bar) {  // bounded wait (20 us): the barrier orders the phases, it is not needed for the result
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        for (int it = 0; it < 100000; ++it) {
-          const uint64_t v = __hip_atomic_load(a.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (dev::read_lane64(v, 0) >= a.bar_target) break;
-          if (__builtin_amdgcn_s_memrealtime() - t0 > 2000) break;
-          __builtin_amdgcn_s_sleep(4);
-        }
-      }
-      for (uint32_t t = lane; t < 2 * nimg; t += 64) {
-        const uint32_t i = t >> 1, c = t & 1u;
-        const uint32_t f = lead + 28 + i * S;
-        const uint32_t b = f & ~31u;
-        const u32x4 v = s_blk[wv][t];
-        if (static_cast<int64_t>(A0) + static_cast<int64_t>(b) >= 0) {
-          typedef unsigned v4u __attribute__((ext_vector_type(4)));
-          __builtin_amdgcn_raw_buffer_store_b128(v4u{v.x, v.y, v.z, v.w}, rsrc, static_cast<int>(b + 16 * c), 0, 19);
-        } else if (c == ((f & 31u) >> 4)) {  // the block starts before the arena: the field alone
-          dev::store16_field(rsrc, f, reinterpret_cast<const uint16_t *>(&s_blk[wv][0])[(i * 32u + (f & 31u)) >> 1]);
-        }
-      }
-    }
-  }
   if (STAMP && lane == 0 && a.dbg) {
     uint32_t hw_id, xcc_id;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw_id));
@@ -366,7 +307,6 @@ hipError_t launch_one(const FixedStreamArgs &a, uint32_t num_cus, hipStream_t st
   FixedStreamArgs b = a;
   b.per_wave = a.count / (blocks * kWavesPerBlock);
   b.rem = a.count % (blocks * kWavesPerBlock);
-  if (b.bar) b.bar_target = (*b.bar_epoch += blocks * kWavesPerBlock);  // this launch's waves all arrived
   hipLaunchKernelGGL((rstream_kernel<U, OP, STAMP, PRIO, FLAV, MODE>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0,
                      stream, b);
   return hipGetLastError();
@@ -439,14 +379,6 @@ hipError_t launch_rstream(int op, int variant, const FixedStreamArgs &a, uint32_
       FixedStreamArgs b = a;
       b.order = 4u;
       return dispatch<4, false, 0, 103>(op, b, num_cus, stream);
-    }
-    case 29: {  // 20 with PHASE (FLAV bit 7): the resident grid streams, then writes the 32-B field blocks
-      // >= 64 B: a field's 32-B block ends inside its image (never past the batch)
-      if (a.stride < 64 || a.defer_field) return hipErrorInvalidValue;
-      FixedStreamArgs b = a;
-      b.order = 4u;
-      b.oversub = 1;
-      return dispatch<4, false, 0, 135>(op, b, num_cus, stream);
     }
     case 26: {  // 20 with the FILL field stores write-through streaming (sc0 sc1 nt, FLAV bit 4)
       FixedStreamArgs b = a;
