@@ -41,7 +41,9 @@ def per_launch(path: str, counter: str):
     return " + ".join(sorted(vals)), sum(statistics.mean(v) for v in vals.values()), min(len(v) for v in vals.values())
 
 
-def main(rnd: str = "r01") -> None:
+def main(rnd: str = "r01", *only: str) -> None:
+    """rnd: the profiles/ subdirectory for the CSVs; only: the configs to
+    update (default: every config with both passes under gpurun_out/)."""
     src = os.path.join(ROOT, "gpurun_out")
     dst = os.path.join(ROOT, "profiles", rnd)
     os.makedirs(dst, exist_ok=True)
@@ -52,6 +54,8 @@ def main(rnd: str = "r01") -> None:
     except (OSError, ValueError):
         summary = {}
     for cfg in ("c2", "c3", "c4", "c5", "slots", "segment", "receive", "fill"):
+        if only and cfg not in only:
+            continue
         fp = os.path.join(src, f"pmc_{cfg}_fetch", "run_counter_collection.csv")
         wp = os.path.join(src, f"pmc_{cfg}_write", "run_counter_collection.csv")
         if not (os.path.exists(fp) and os.path.exists(wp)):
@@ -80,4 +84,6 @@ def main(rnd: str = "r01") -> None:
 
 
 if __name__ == "__main__":
+    if any(a.startswith("-") for a in sys.argv[1:]):
+        raise SystemExit("usage: pmc_summary.py [round] [config ...]")
     main(*sys.argv[1:])
