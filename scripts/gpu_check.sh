@@ -127,6 +127,9 @@ for s in ${STEPS:-tests smoke bench prof}; do
     fblind) step fblind 300 rocprofv3 --kernel-trace -d gpurun_out/fblind -o run --output-format csv -- python3 scripts/fill_drain_probe.py --phases stream,sg2_8,sg0_8,sg8_8,sg8_1,sg9_8,sg10_8,sg10_1,sg11_8,sg11_1,sg12_8,sg1_8,stream ;;
     fblock) step fblock_tests 600 python -u -m pytest tests/test_gpu_fill_defer.py -x -q --timeout 120 --timeout-method thread -k "block" &&
       step fblock 300 rocprofv3 --kernel-trace -d gpurun_out/fblock -o run --output-format csv -- python3 scripts/fill_drain_probe.py --phases stream,fill,block,blockend,sg8_8,block,blockend,fill ;;
+    hwide) step hwide 300 python scripts/receive_fused_probe.py --wide &&
+      step hwide_trace 300 rocprofv3 --kernel-trace --stats -d gpurun_out/hwide_trace -o run --output-format csv -- python3 scripts/receive_fused_probe.py --wide &&
+      step hwide_fetch 120 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d gpurun_out/hwide_fetch -o run --output-format csv -- python3 scripts/receive_fused_probe.py --wide ;;
     fgran) step fgran 300 rocprofv3 --kernel-trace -d gpurun_out/fgran -o run --output-format csv -- python3 scripts/fill_drain_probe.py --phases stream,sp8,sg1_8,sg1_0,sg2_8,sg2_7,sg2_0,sg3_8,sg3_0,instream26,instream,sp7,fill ;;
     fdvv) step fdvv 600 python scripts/fill_defer_vv_probe.py ;;
     fdsweep) step fdsweep 600 python scripts/fill_defer_vv_probe.py --sweep ;;

@@ -117,11 +117,43 @@ def sweep(ctx, s, rng, n):
         del a, hdr
 
 
+def wide(ctx, s, rng, n):
+    """--wide: the receive ring's header pass as the product form (8 lanes per
+    image, u16 loads) against two lanes per image with one 16-B load each and
+    the load cache bits default / nt / sc0 sc1 / sc1 (param 1 << 25 | form <<
+    28, probe build); time per RECEIVE step and the results compared."""
+    mix = (np.asarray((64, 576, 1460), np.uint32)[rng.integers(0, 3, n)] + 32).astype(np.uint32)
+    img = int(mix.astype(np.int64).sum())
+    S = tcpck.KERNEL_SSTREAM
+    slot = 2048
+    off = np.arange(n, dtype=np.uint64) * np.uint64(slot)
+    a = torch.empty(n * slot, dtype=torch.uint8, device="cuda")
+    d_off, d_ln = torch.from_numpy(off).cuda(), torch.from_numpy(mix).cuda()
+    tcpck.synth_var(a, d_off, d_ln, int(mix.max()), n, seed=42)
+    ok = torch.empty(n, dtype=torch.uint8, device="cuda")
+    hdr = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
+    kw = dict(offsets=d_off, lengths=d_ln, total_bytes=img, min_len=int(mix.min()), max_len=int(mix.max()),
+              sorted=True, stream=s)
+    res = {}
+    for label, p in (("two passes", TWO), ("wide default", TWO | (1 << 25)), ("wide nt", TWO | (1 << 25) | (1 << 28)),
+                     ("wide sc0 sc1", TWO | (1 << 25) | (2 << 28)), ("wide sc1", TWO | (1 << 25) | (3 << 28))):
+        ms = b2b(lambda: ctx.batch_receive(a, n, ok, hdr, kernel=S, param=p, **kw), s)
+        torch.cuda.synchronize()
+        res[label] = (ok.clone(), hdr.clone())
+        print(f"ring 1M x 2048 (bench mix)   {label:14s} {ms * 1e3:8.1f} us", flush=True)
+    ref = res["two passes"]
+    print("results identical:", all(torch.equal(v[0], ref[0]) and torch.equal(v[1], ref[1]) for v in res.values()),
+          flush=True)
+
+
 def main():
     ctx = tcpck.Context(0, probe=True)
     s = torch.cuda.current_stream()
     rng = np.random.default_rng(42)
     n = 1 << 20
+    if "--wide" in sys.argv:
+        wide(ctx, s, rng, n)
+        return
     if "--sweep" in sys.argv:
         sweep(ctx, s, rng, n)
         return

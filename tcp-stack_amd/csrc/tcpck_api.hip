@@ -268,6 +268,9 @@ constexpr uint64_t kDeferFillMinVar = 1024;
 constexpr int kSstreamHdrStream = 32;    // sstream RECEIVE: headers from the stream's registers
 constexpr uint64_t kHdrStreamMaxLen = 256;  // ... for (typical) images up to this length
 constexpr int kProbeHdrWriteThrough = 1 << 27;  // probe builds: the header pass's array stores written through
+// probe builds: the header pass as two lanes per 16-B aligned image, one 16-B
+// buffer load each, cache bits (bits 28-29: 0 default, 1 nt, 2 sc0 sc1, 3 sc1)
+constexpr int kProbeHdrWide = 1 << 25;
 #ifdef TCPCK_PROBE
 constexpr int kReceiveConcurrent = 1 << 26;  // probe builds: the header pass beside VERIFY on a side stream
 #endif
@@ -551,6 +554,7 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
     pa.update = 1;
     return tcpck::launch_patch_fields(pa, static_cast<uint32_t>(ctx->num_cus), s);
   }
+  const uint32_t hdr_bits = (param & kProbeHdrWide) ? 2u | ((static_cast<uint32_t>(param) >> 28 & 3u) << 4) : 0u;
   param &= ~(TCPCK_PARAM_FILL_UPDATE | TCPCK_PARAM_FILL_INSTREAM);
   bool hdr_done = false;
   const hipError_t e =
@@ -572,7 +576,8 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
   h.stride = stride;
   h.count = count;
   h.out = hdr;
-  h.store_bits = (param & kProbeHdrWriteThrough) ? 1u : 0u;
+  h.store_bits = ((param & kProbeHdrWriteThrough) ? 1u : 0u) |
+                 hdr_bits;
   return tcpck::launch_header_swap(h, static_cast<uint32_t>(ctx->num_cus), s);
 }
 
@@ -708,6 +713,7 @@ hipError_t run_var(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const uint6
     pa.packed = (layout && (layout->flags & TCPCK_LAYOUT_PACKED)) ? 1u : 0u;
     return tcpck::launch_patch_fields(pa, static_cast<uint32_t>(ctx->num_cus), s);
   }
+  const uint32_t hdr_bits = (param & kProbeHdrWide) ? 2u | ((static_cast<uint32_t>(param) >> 28 & 3u) << 4) : 0u;
   param &= ~(TCPCK_PARAM_FILL_UPDATE | TCPCK_PARAM_FILL_INSTREAM);
   bool hdr_done = false, patch = false;
   const hipError_t e =
@@ -729,7 +735,8 @@ hipError_t run_var(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const uint6
   h.offsets = off;
   h.count = count;
   h.out = hdr;
-  h.store_bits = (param & kProbeHdrWriteThrough) ? 1u : 0u;
+  h.store_bits = ((param & kProbeHdrWriteThrough) ? 1u : 0u) |
+                 hdr_bits;
   return tcpck::launch_header_swap(h, static_cast<uint32_t>(ctx->num_cus), s);
 }
 

@@ -65,6 +65,96 @@ __global__ void __launch_bounds__(kBlock) header_swap_kernel(HeaderArgs a) {
   }
 }
 
+#ifdef TCPCK_PROBE
+// Probe: the array form with two lanes per image, each one 16-B buffer load of
+// header bytes 16h..16h+15 and one 16-B store (images 16-B aligned, arena
+// < 4 GiB; the launcher checks), loads with cache bits LP (0 default, 1 nt,
+// 2 sc0 sc1, 3 sc1): how many bytes a 32-B header costs to fetch.
+template <bool FIXED, int LP>
+__global__ void __launch_bounds__(kBlock) header_wide_kernel(HeaderArgs a) {
+  const uint64_t step = static_cast<uint64_t>(gridDim.x) * kBlock;
+  const auto rsrc = dev::make_rsrc(a.arena, 0xFFFFFFF0u);
+  constexpr int aux = LP == 0 ? 0 : (LP == 1 ? 2 : (LP == 2 ? 17 : 16));
+  for (uint64_t t = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x; t < a.count * 2; t += step) {
+    const uint64_t k = t >> 1;
+    const uint32_t h = static_cast<uint32_t>(t & 1);
+    const uint64_t start = FIXED ? k * a.stride : a.offsets[k];
+    typedef unsigned v4u __attribute__((ext_vector_type(4)));
+    const v4u v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, static_cast<int>(start + 16 * h), 0, aux);
+    const dev::u32x4 o{dev::n2h_dword(v.x, 0x00010203u), dev::n2h_dword(v.y, 0x00010203u),
+                       dev::n2h_dword(v.z, 0x02030100u), dev::n2h_dword(v.w, h ? 0x02030100u : 0x02030001u)};
+    reinterpret_cast<dev::u32x4 *>(a.out)[t] = o;
+  }
+}
+
+template <bool FIXED, int LP>
+hipError_t launch_wide(const HeaderArgs &a, uint32_t num_cus, hipStream_t s) {
+  static const uint32_t per_cu = dev::resident_blocks_per_cu(header_wide_kernel<FIXED, LP>);
+  uint64_t blocks = (a.count * 2 + kBlock - 1) / kBlock;
+  const uint64_t cap = static_cast<uint64_t>(per_cu) * num_cus * 8;
+  if (blocks > cap) blocks = cap;
+  hipLaunchKernelGGL((header_wide_kernel<FIXED, LP>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0, s, a);
+  return hipGetLastError();
+}
+
+template <bool FIXED>
+hipError_t wide_by_policy(const HeaderArgs &a, uint32_t num_cus, hipStream_t s) {
+  switch ((a.store_bits >> 4) & 3u) {
+    case 0: return launch_wide<FIXED, 0>(a, num_cus, s);
+    case 1: return launch_wide<FIXED, 1>(a, num_cus, s);
+    case 2: return launch_wide<FIXED, 2>(a, num_cus, s);
+    default: return launch_wide<FIXED, 3>(a, num_cus, s);
+  }
+}
+#endif
+
+// The array form (tcpck_batch_receive with a header array): two lanes per
+// image, lane h converting header bytes 16h..16h+15 -- one 16-B load when the
+// image is 16-B aligned (every receive-ring slot), else eight u16 loads -- and
+// one 16-B store (four 4-B stores into a 4-B aligned array).  2 us faster than
+// eight lanes of u16 accesses on the 1M-datagram ring (29.2 vs 31.1 us; the
+// pass fetches the same 128-B line per image either way, whatever the load's
+// cache bits: scripts/receive_fused_probe.py --wide, profiles/r03/
+// receive_header_wide.log).
+template <bool FIXED>
+__global__ void __launch_bounds__(kBlock) header_extract_kernel(HeaderArgs a) {
+  const uint64_t step = static_cast<uint64_t>(gridDim.x) * kBlock;
+  const bool out16 = (reinterpret_cast<uintptr_t>(a.out) & 15u) == 0;
+  for (uint64_t t = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x; t < a.count * 2; t += step) {
+    const uint64_t k = t >> 1;
+    const uint32_t h = static_cast<uint32_t>(t & 1);
+    const uint8_t *p = a.arena + (FIXED ? k * a.stride : a.offsets[k]) + 16 * h;
+    dev::u32x4 v;
+    if ((reinterpret_cast<uintptr_t>(p) & 15u) == 0) {
+      v = *reinterpret_cast<const dev::u32x4 *>(p);
+    } else {  // images are 2-B aligned
+      const uint16_t *q = reinterpret_cast<const uint16_t *>(p);
+      v = dev::u32x4{q[0] | (static_cast<uint32_t>(q[1]) << 16), q[2] | (static_cast<uint32_t>(q[3]) << 16),
+                     q[4] | (static_cast<uint32_t>(q[5]) << 16), q[6] | (static_cast<uint32_t>(q[7]) << 16)};
+    }
+    // dwords 4h..4h+3 of TcpHeaderN2H (dev::n2h_selector): 0/4, 1/5 byte
+    // reversed, 2/6 the upper u16 swapped, 3 the two ports, 7 the urgent pointer
+    const dev::u32x4 o{dev::n2h_dword(v.x, 0x00010203u), dev::n2h_dword(v.y, 0x00010203u),
+                       dev::n2h_dword(v.z, 0x02030100u), dev::n2h_dword(v.w, h ? 0x02030100u : 0x02030001u)};
+    if (out16) {
+      reinterpret_cast<dev::u32x4 *>(a.out)[t] = o;
+    } else {
+      uint32_t *d = reinterpret_cast<uint32_t *>(a.out) + 4 * t;
+      d[0] = o.x, d[1] = o.y, d[2] = o.z, d[3] = o.w;
+    }
+  }
+}
+
+template <bool FIXED>
+hipError_t launch_extract(const HeaderArgs &a, uint32_t num_cus, hipStream_t s) {
+  static const uint32_t per_cu = dev::resident_blocks_per_cu(header_extract_kernel<FIXED>);
+  uint64_t blocks = (a.count * 2 + kBlock - 1) / kBlock;
+  const uint64_t cap = static_cast<uint64_t>(per_cu) * num_cus * 8;
+  if (blocks > cap) blocks = cap;
+  hipLaunchKernelGGL((header_extract_kernel<FIXED>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0, s, a);
+  return hipGetLastError();
+}
+
 template <bool FIXED, bool EXTRACT, bool WT = false>
 hipError_t launch_one(const HeaderArgs &a, uint32_t num_cus, hipStream_t s) {
   static const uint32_t per_cu = dev::resident_blocks_per_cu(header_swap_kernel<FIXED, EXTRACT, WT>);
@@ -313,11 +403,16 @@ hipError_t launch_patch_fields(const PatchArgs &a, uint32_t num_cus, hipStream_t
 hipError_t launch_header_swap(const HeaderArgs &a, uint32_t num_cus, hipStream_t stream) {
   if (a.count == 0) return hipSuccess;
 #ifdef TCPCK_PROBE
+  if (a.out && (a.store_bits & 2)) {  // the wide form: 16-B aligned images and array, arena < 4 GiB
+    if ((reinterpret_cast<uintptr_t>(a.arena) & 15u) || (reinterpret_cast<uintptr_t>(a.out) & 15u) ||
+        (!a.offsets && (a.stride & 15u)))
+      return hipErrorInvalidValue;
+    return a.offsets ? wide_by_policy<false>(a, num_cus, stream) : wide_by_policy<true>(a, num_cus, stream);
+  }
   if (a.out && a.store_bits)
     return a.offsets ? launch_one<false, true, true>(a, num_cus, stream) : launch_one<true, true, true>(a, num_cus, stream);
 #endif
-  if (a.out)
-    return a.offsets ? launch_one<false, true>(a, num_cus, stream) : launch_one<true, true>(a, num_cus, stream);
+  if (a.out) return a.offsets ? launch_extract<false>(a, num_cus, stream) : launch_extract<true>(a, num_cus, stream);
   return a.offsets ? launch_one<false, false>(a, num_cus, stream) : launch_one<true, false>(a, num_cus, stream);
 }
 
