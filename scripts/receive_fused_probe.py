@@ -136,7 +136,8 @@ def wide(ctx, s, rng, n):
               sorted=True, stream=s)
     res = {}
     for label, p in (("two passes", TWO), ("wide default", TWO | (1 << 25)), ("wide nt", TWO | (1 << 25) | (1 << 28)),
-                     ("wide sc0 sc1", TWO | (1 << 25) | (2 << 28)), ("wide sc1", TWO | (1 << 25) | (3 << 28))):
+                     ("wide sc0 sc1", TWO | (1 << 25) | (2 << 28)), ("wide sc1", TWO | (1 << 25) | (3 << 28)),
+                     ("header first", TWO | (1 << 24)), ("hdr first wide", TWO | (1 << 24) | (1 << 25))):
         ms = b2b(lambda: ctx.batch_receive(a, n, ok, hdr, kernel=S, param=p, **kw), s)
         torch.cuda.synchronize()
         res[label] = (ok.clone(), hdr.clone())

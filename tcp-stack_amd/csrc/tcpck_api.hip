@@ -272,6 +272,11 @@ constexpr int kProbeHdrWriteThrough = 1 << 27;  // probe builds: the header pass
 // buffer load each, cache bits (bits 28-29: 0 default, 1 nt, 2 sc0 sc1, 3 sc1)
 constexpr int kProbeHdrWide = 1 << 25;
 #ifdef TCPCK_PROBE
+// probe builds, RECEIVE with TCPCK_PARAM_RECEIVE_TWO_PASS: the header pass
+// first, its lines left in the caches for the VERIFY stream that follows
+constexpr int kProbeHdrFirst = 1 << 24;
+#endif
+#ifdef TCPCK_PROBE
 constexpr int kReceiveConcurrent = 1 << 26;  // probe builds: the header pass beside VERIFY on a side stream
 #endif
 // RECEIVE with an explicit kernel: the probe build fuses the headers into any
@@ -715,6 +720,20 @@ hipError_t run_var(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const uint6
   }
   const uint32_t hdr_bits = (param & kProbeHdrWide) ? 2u | ((static_cast<uint32_t>(param) >> 28 & 3u) << 4) : 0u;
   param &= ~(TCPCK_PARAM_FILL_UPDATE | TCPCK_PARAM_FILL_INSTREAM);
+#ifdef TCPCK_PROBE
+  if (op == TCPCK_OP_RECEIVE && hdr && (param & kProbeHdrFirst) && (param & TCPCK_PARAM_RECEIVE_TWO_PASS)) {
+    tcpck::HeaderArgs h{};
+    h.arena = arena;
+    h.offsets = off;
+    h.count = count;
+    h.out = hdr;
+    h.store_bits = hdr_bits;
+    const hipError_t eh = tcpck::launch_header_swap(h, static_cast<uint32_t>(ctx->num_cus), s);
+    if (eh != hipSuccess) return eh;
+    return run_var_impl(ctx, TCPCK_OP_VERIFY, mode, arena, off, len, base, count, out, layout, kernel,
+                        param & ~(kProbeHdrFirst | TCPCK_PARAM_RECEIVE_TWO_PASS), s);
+  }
+#endif
   bool hdr_done = false, patch = false;
   const hipError_t e =
       run_var_impl(ctx, op, mode, arena, off, len, base, count, out, layout, kernel, param, s, hdr, &hdr_done, &patch);
