@@ -71,7 +71,9 @@ CONFIGS = {
 }
 STRONG = {"c5"}  # configs whose total work is fixed as N grows; the rest are per-GPU (weak)
 # the other BASELINE configs, then the §8f ops, timed inside the default (C2) run, and their keys in its line
-EXTRAS = (("c3", "c3"), ("c4", "c4"), ("c5", "c5_strong"), ("fill", "fill"), ("slots", "slots"),
+# (C5 first: timed after C3/C4 had allocated and freed 19 GB, the same launches ran 2.5 % slower than
+# in a process of their own -- 1.737 vs 1.695 ms, profiles/r03/c5_order_probe.log)
+EXTRAS = (("c5", "c5_strong"), ("c3", "c3"), ("c4", "c4"), ("fill", "fill"), ("slots", "slots"),
           ("receive", "receive"), ("segment", "segment"))
 # round-2 ops (not BASELINE configs; same contract, their own metric):
 EXTRA = {
