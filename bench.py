@@ -71,10 +71,11 @@ CONFIGS = {
 }
 STRONG = {"c5"}  # configs whose total work is fixed as N grows; the rest are per-GPU (weak)
 # the other BASELINE configs, then the §8f ops, timed inside the default (C2) run, and their keys in its line
-# (C5 first: timed after C3/C4 had allocated and freed 19 GB, the same launches ran 2.5 % slower than
-# in a process of their own -- 1.737 vs 1.695 ms, profiles/r03/c5_order_probe.log)
-EXTRAS = (("c5", "c5_strong"), ("c3", "c3"), ("c4", "c4"), ("fill", "fill"), ("slots", "slots"),
-          ("receive", "receive"), ("segment", "segment"))
+# (the big C3 / C4 arenas last: C5 timed after C3/C4 had allocated and freed 19 GB ran 2.5 % slower
+# than in a process of its own -- 1.737 vs 1.695 ms, profiles/r03/c5_order_probe.log; in this order
+# every config matches its own process within 1 %, profiles/r03/bench_order_probe.log)
+EXTRAS = (("c5", "c5_strong"), ("fill", "fill"), ("slots", "slots"), ("receive", "receive"),
+          ("segment", "segment"), ("c3", "c3"), ("c4", "c4"))
 # round-2 ops (not BASELINE configs; same contract, their own metric):
 EXTRA = {
     # the device-resident receive arena: 1M 2048-B slots, one datagram per slot

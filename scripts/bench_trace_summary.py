@@ -10,7 +10,7 @@ steps; the settle and warm-up launches come before them) are averaged; the
 config's per-step time is the sum over its groups.
 
     python scripts/bench_trace_summary.py gpurun_out/prof_all/run_kernel_trace.csv --last 20 \\
-        --names c2,c5_strong,c3,c4,fill,slots,receive,segment
+        --names c2,c5_strong,fill,slots,receive,segment,c3,c4
 """
 import argparse
 import csv
