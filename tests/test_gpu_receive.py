@@ -456,7 +456,8 @@ def test_batch_receive_sstream_variants(ctx, variant):
 # ---- RECEIVE with the headers written by sstream itself (one launch) -------------------
 
 @pytest.mark.parametrize("variant", [0, 1, 2, 4, 8, 16, 17, 18, 32, 33, 34, 36, 40, 96, 98, 1 << 30])
-@pytest.mark.parametrize("layout", ["ring", "ring-mis", "ring-short", "unordered", "fixed-slots", "fixed-mis"])
+@pytest.mark.parametrize("layout", ["ring", "ring-mis", "ring-short", "ring-64", "unordered", "fixed-slots",
+                                    "fixed-mis", "fixed-64"])
 @pytest.mark.parametrize("hdr_mis", [0, 4])
 def test_batch_receive_fused_hdr(ctx, variant, layout, hdr_mis):
     """tcpck_batch_receive_ex on KERNEL_SSTREAM: each wave writes its run's
@@ -465,8 +466,10 @@ def test_batch_receive_fused_hdr(ctx, variant, layout, hdr_mis):
     + 64 with nt stores -- runs holding a misaligned or < 32-B image fall back
     to the per-run conversion; 1 << 30: the separate header pass instead).
     Rings (16-B and 2-B aligned starts), unordered offsets (the per-image
-    fallback), fixed slots; header arrays 16-B and only 4-B aligned; both
-    modes.  Verdicts, every header byte, the arena unchanged."""
+    fallback), fixed slots; 64-256-B rings and 64-B fixed images (+ 32: every
+    run's records staged in LDS, up to 17 images per step); header arrays 16-B
+    and only 4-B aligned; both modes.  Verdicts, every header byte, the arena
+    unchanged."""
     import tcpck
     from oracle import ref16 as R
     rng = np.random.default_rng(variant % 97 + 10 * len(layout) + hdr_mis)
@@ -478,7 +481,9 @@ def test_batch_receive_fused_hdr(ctx, variant, layout, hdr_mis):
     if layout == "unordered":
         off = off[rng.permutation(n)].copy()
     if layout.startswith("fixed"):
-        ln[:] = 1492
+        ln[:] = 64 if layout == "fixed-64" else 1492
+    if layout == "ring-64":  # every image >= 64 B, up to 17 per compacted step
+        ln = (rng.integers(32, 129, n) * 2).astype(np.uint32)
     if layout == "ring-short":  # some runs hold images below 32 B (headers past the image end)
         ln[rng.integers(0, n, 40)] = (rng.integers(1, 16, 40) * 2).astype(np.uint32)
     a = rng.integers(0, 256, n * slot + 64, dtype=np.uint8)
@@ -491,7 +496,7 @@ def test_batch_receive_fused_hdr(ctx, variant, layout, hdr_mis):
     hbuf = torch.full((n * 32 + 16,), 0xEE, dtype=torch.uint8, device="cuda")
     hdr = hbuf.data_ptr() + hdr_mis
     if layout.startswith("fixed"):
-        ctx.batch_receive(buf.data_ptr() + mis, n, ok, hdr, stride=slot, length=1492, mode=mode,
+        ctx.batch_receive(buf.data_ptr() + mis, n, ok, hdr, stride=slot, length=int(ln[0]), mode=mode,
                           kernel=tcpck.KERNEL_SSTREAM, param=variant)
     else:
         ctx.batch_receive(buf.data_ptr() + mis, n, ok, hdr, offsets=dev(off), lengths=dev(ln), mode=mode,
