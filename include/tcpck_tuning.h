@@ -54,7 +54,12 @@ extern "C" {
                                   20 = the policy's; 22: 18 with every step read
                                   with the default policy; 23/24: 20 with 8/2
                                   steps in flight; 25: 20's FILL with the fields
-                                  stored by the 64-B block pass, AUTO's FILL)
+                                  stored by the write-through 2-B field pass,
+                                  AUTO's FILL; 26: 20 with write-through field
+                                  stores in the stream; 27/28: 20's FILL writing
+                                  each field's whole 64-B block from the stream
+                                  (28: a short run's blocks after its last load),
+                                  stride >= 128)
                                   | (blocks per CU cap << 8)
                                   | (grid oversubscription << 16: 0 = by batch
                                   size, 1 = none, M = M x the resident grid)    */
