@@ -26,11 +26,13 @@ def build(variant: str) -> str:
     deps = [SRC] + [os.path.join(ROOT, "include", "tcp_stack", f) for f in ("tcp-header.h", "packet-batch.h")]
     if os.path.exists(exe) and all(os.path.getmtime(exe) >= os.path.getmtime(d) for d in deps):
         return exe
+    tmp = f"{exe}.{os.getpid()}.tmp"
     flags = ["-O1", "-g", "-fsanitize=address,undefined", "-fno-sanitize-recover=all"] if variant == "asan" else ["-O2"]
     cmd = (["g++", "-std=c++17", "-Wall", "-Wextra", "-Werror"] + flags +
-           ["-I", os.path.join(ROOT, "include"), SRC, "-o", exe, "-L", LIBDIR, "-ltcpck",
+           ["-I", os.path.join(ROOT, "include"), SRC, "-o", tmp, "-L", LIBDIR, "-ltcpck",
             f"-Wl,-rpath,{LIBDIR}", "-Wl,-rpath-link,/opt/rocm/lib"])
     subprocess.run(cmd, check=True)
+    os.replace(tmp, exe)  # atomic: a parallel test process never runs a half-written binary
     return exe
 
 
