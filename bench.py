@@ -501,7 +501,7 @@ def cpu_baseline(host_arena, gpu_res, kind, count, L, budget_s, var_layout):
         one, _, _ = passes(pk, 1, 1, 0.5)
         pk.close()
         out.update({"value": round(med, 2), "kind": kind_s, "one_thread_GiBs": round(one, 2),
-                    "passes_GiBs": [round(r, 1) for r in rates],
+                    "passes_GiBs": [round(r, 1) for r in rates], "best_GiBs": round(max(rates), 2),
                     "sample": sdesc + f"; median of 7 passes of {reps} sweeps on {nthr} threads; CalculateChecksum "
                               f"(tcp-header.h:252-263) built -O3 -march=x86-64-v3; results == GPU results: {match}"})
         if R.RefLib.available("O0"):

@@ -8,7 +8,9 @@ and (round 3) each header emitted from the stream's registers as the step is
 consumed (variant 32; 96: with write-through sc0 sc1 nt stores), and the
 header pass with write-through array stores (1 << 27, probe build).
 VERIFY alone for reference.  Results compared byte for byte.  Median of
-back-to-back rounds."""
+back-to-back rounds.  (Before round 3's fix the VERIFY-only closure took the
+lengths' min/max on the host per call: its small-ring lines, ~300 us, were
+host-bound; the kernel takes 140 us, profiles/r03/receive_small_ring_trace.txt.)"""
 import os
 import sys
 import time
@@ -60,8 +62,8 @@ def case(ctx, s, name, n, slot, ln, fixed_len=None):
         if fixed_len:
             ctx.batch_fixed(tcpck.OP_VERIFY, a, slot, fixed_len, n, ok, stream=s)
         else:
-            ctx.batch_var(tcpck.OP_VERIFY, a, d_off, d_ln, n, ok, total_bytes=img, min_len=int(ln.min()),
-                          max_len=int(ln.max()), sorted=True, stream=s)
+            ctx.batch_var(tcpck.OP_VERIFY, a, d_off, d_ln, n, ok, total_bytes=img, min_len=kw["min_len"],
+                          max_len=kw["max_len"], sorted=True, stream=s)
 
     runs = [("VERIFY only", verify),
             ("two passes", lambda: ctx.batch_receive(a, n, ok, hdr, kernel=S, param=TWO, **kw)),
