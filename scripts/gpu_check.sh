@@ -16,7 +16,7 @@ step() {  # step <name> <timeout> <cmd...>
 }
 for s in ${STEPS:-tests smoke bench prof}; do
   case $s in
-    tests) step pytest 900 python -m pytest tests -m gpu -x -q ;;
+    tests) step pytest 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py ;;
     bench_c3) step bench_c3 600 python bench.py --config c3 --no-cpu-baseline ;;
