@@ -47,15 +47,6 @@ struct tcpck_ctx {
   std::mutex side_mu;
   hipStream_t side = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;
-
-  // packed fixed jumbo images streamed as pieces (run_pieces): the pieces'
-  // checksums, allocated on first use and grown; ws_done marks its last use so
-  // that a call on another stream waits for it
-  std::mutex ws_mu;
-  uint16_t *ws = nullptr;
-  uint64_t ws_bytes = 0;
-  hipEvent_t ws_done = nullptr;
-  hipStream_t ws_stream = nullptr;
 };
 
 namespace {
@@ -205,8 +196,6 @@ hipError_t ensure_side(tcpck_ctx *ctx) {
 #endif
 
 void free_stage(tcpck_ctx *ctx) {
-  if (ctx->ws) (void)hipFree(ctx->ws);
-  if (ctx->ws_done) (void)hipEventDestroy(ctx->ws_done);
   if (ctx->side) {
     (void)hipEventDestroy(ctx->fork);
     (void)hipEventDestroy(ctx->join);
@@ -255,12 +244,6 @@ constexpr uint64_t kFixedRunMaxLen = 4096;   // packed fixed: rstream up to here
 // same with runs >= 8 KiB (C3 86.3 -> 89.5%, profiles/r01/xcd_first_step_probe.log).
 constexpr int kRstreamPolicy = 20;       // v_dot2 sums, buffer loads, XCD-chunked order, L2-kept first step
 constexpr int kRstreamDeferFill = 25;    // FILL: kRstreamPolicy's stream to out, then the 2-B write-through field pass
-// CHECKSUM / VERIFY of packed fixed jumbo images as np = param >> 8 & 0xFF (x 8)
-// pieces each: kRstreamPolicy's stream over stride len / np, then
-// launch_piece_combine (run_pieces)
-constexpr int kRstreamPieces = 30;
-constexpr uint32_t kPieceBytes = 4096;   // AUTO: the piece length aimed at
-constexpr bool kAutoPieces = false;      // AUTO routes packed jumbo images to run_pieces
 constexpr int kVvPolicy = 4 | 8 | 16;    // size policy, XCD-chunked order, L2-kept first step
 constexpr int kSegXcdOrder = 1 << 24;    // seg: XCD-chunked order
 // FILL of small images: nearly every line holds a checksum field, so the
@@ -322,63 +305,6 @@ static bool jumbo_on_seg(int op, uint64_t len) {
   return op == TCPCK_OP_FILL ? fits && len > 24576 : fits;
 }
 
-// Packed fixed jumbo images as pieces: an image's word sum is the sum of its
-// pieces' word sums, so C4's 64-KiB images stream through rstream (the C2 /
-// C5 kernel) as np pieces of len / np bytes each into the ctx workspace, and
-// launch_piece_combine folds each image's np piece checksums into its checksum
-// or verdict, c = ~(sum ~c_j) mod 2^16 (tcp-header.h:252-263).  REF mode;
-// pieces of >= 512 B and a multiple of 16 B.
-bool pieces_apply(uint32_t len, uint32_t np) {
-  return np >= 8 && (np & 7u) == 0 && np <= 2040 && len % np == 0 && (len / np) % 16 == 0 && len / np >= 512;
-}
-// AUTO's piece count: the smallest multiple of 8 giving pieces of <= kPieceBytes (0: none)
-uint32_t pieces_for(uint32_t len) {
-  for (uint32_t np = 8; np <= 2040; np += 8)
-    if (len / np <= kPieceBytes && pieces_apply(len, np)) return np;
-  return 0;
-}
-
-hipError_t run_pieces(tcpck_ctx *ctx, int op, uint8_t *arena, uint32_t len, uint64_t count, void *out, uint32_t np,
-                      uint32_t oversub, hipStream_t s) {
-  if ((op != TCPCK_OP_CHECKSUM && op != TCPCK_OP_VERIFY) || !out || !pieces_apply(len, np)) return hipErrorInvalidValue;
-  if (count == 0) return hipSuccess;
-  const uint64_t need = count * np * sizeof(uint16_t);
-  std::lock_guard<std::mutex> g(ctx->ws_mu);
-  if (ctx->ws_bytes < need) {  // first use or a larger batch: hipFree waits for the last user
-    if (ctx->ws) (void)hipFree(ctx->ws);
-    ctx->ws = nullptr;
-    ctx->ws_bytes = 0;
-    void *p = nullptr;
-    if (hipMalloc(&p, need) != hipSuccess) return hipErrorOutOfMemory;
-    ctx->ws = static_cast<uint16_t *>(p);
-    ctx->ws_bytes = need;
-  }
-  hipError_t e = hipSuccess;
-  if (!ctx->ws_done)
-    e = hipEventCreateWithFlags(&ctx->ws_done, hipEventDisableTiming);
-  else if (ctx->ws_stream != s)
-    e = hipStreamWaitEvent(s, ctx->ws_done, 0);  // the previous call's combine has read the workspace
-  if (e != hipSuccess) return e;
-  tcpck::FixedStreamArgs a{};
-  a.mode = tcpck::kRef;
-  a.arena = arena;
-  a.stride = len / np;
-  a.count = count * np;
-  a.order = 0xFFu;
-  a.out = ctx->ws;
-  a.oversub = oversub;
-  const uint32_t num_cus = static_cast<uint32_t>(ctx->num_cus);
-  e = tcpck::launch_rstream(tcpck::kChecksum, kRstreamPolicy, a, num_cus, s);
-  if (e == hipSuccess)
-    e = tcpck::launch_piece_combine(op == TCPCK_OP_VERIFY ? tcpck::kVerify : tcpck::kChecksum, ctx->ws, np, count, out,
-                                    s);
-  if (e == hipSuccess) {
-    e = hipEventRecord(ctx->ws_done, s);
-    ctx->ws_stream = s;
-  }
-  return e;
-}
-
 hipError_t run_fixed_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t stride, uint32_t len,
                           uint64_t count, void *out, int kernel, int param, hipStream_t s, bool *patch,
                           uint8_t *hdr = nullptr, bool *hdr_done = nullptr) {
@@ -396,11 +322,6 @@ hipError_t run_fixed_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint
     // RFC 1071 on small packed images: vvstream's fixed mode with exact u32 prefix tables
     kernel = TCPCK_KERNEL_VVSTREAM;
     param = kVvPolicy;
-  }
-  if (kAutoPieces && kernel == TCPCK_KERNEL_AUTO && mode == TCPCK_MODE_REF && stride == len && len > kFixedRunMaxLen &&
-      (op == TCPCK_OP_CHECKSUM || op == TCPCK_OP_VERIFY || op == TCPCK_OP_RECEIVE) && out && pieces_for(len)) {
-    kernel = TCPCK_KERNEL_RSTREAM;
-    param = kRstreamPieces | static_cast<int>((pieces_for(len) / 8) << 8);
   }
   if (kernel == TCPCK_KERNEL_AUTO) {
     // jumbo images in slots with small gaps (9000 B in 9216-B slots): vvstream
@@ -512,9 +433,6 @@ hipError_t run_fixed_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint
     a.blocks_per_cu = static_cast<uint32_t>(param >> 8) & 0xFFu;
     a.oversub = static_cast<uint32_t>(param >> 16) & 0xFFu;
     int variant = param & 0xFF;
-    if (variant == kRstreamPieces)
-      return mode != TCPCK_MODE_REF ? hipErrorInvalidValue : run_pieces(ctx, op, arena, len, count, out, 8u * ((static_cast<uint32_t>(param) >> 8) & 0xFFu), a.oversub,
-                        s);
     if (variant == kRstreamDeferFill) {  // FILL: the policy's stream, the fields in a second pass
       if (op != TCPCK_OP_FILL || !out || stride < 30) return hipErrorInvalidValue;
       a.defer_field = 1;

@@ -108,11 +108,6 @@ hipError_t launch_gstream(int op, int variant, const GroupStreamArgs &a, uint32_
 // variant: 0 = 4 loads in flight, 1 = 2, 2 = 8, 3 = 4 with per-wave time stamps,
 // 4-8 issue-priority experiments, 9-13 v_dot2 sums and/or buffer loads (10 = policy)
 hipError_t launch_rstream(int op, int variant, const FixedStreamArgs &a, uint32_t num_cus, hipStream_t stream);
-// Packed fixed jumbo images streamed as np pieces each (rstream CHECKSUM over
-// stride = len / np), then combined: image k's checksum (kChecksum, u16) or
-// verdict (kVerify, u8) from pieces[k np .. k np + np) (16-B aligned; np a multiple of 8, <= 4096)
-hipError_t launch_piece_combine(int op, const uint16_t *pieces, uint32_t np, uint64_t count, void *out,
-                                hipStream_t stream);
 // ---- vvstream (prefix table), MODE_REF, all ops: packed variable layouts
 // (fixed = false) or fixed strides (fixed = true: a.stride >= a.len).
 // variant 0 U4 byte split, 1 U8, 2 U4 count split, 3 U8 (fixed: 0/2 U4, 1/3 U8),

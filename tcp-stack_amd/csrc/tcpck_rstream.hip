@@ -404,51 +404,4 @@ hipError_t launch_rstream(int op, int variant, const FixedStreamArgs &a, uint32_
   return hipErrorInvalidValue;
 }
 
-namespace {
-
-// Image k's checksum from its np piece checksums c_j (CalculateChecksum,
-// tcp-header.h:252-263, is ~(word sum mod 2^16), and the word sum of an image
-// is the sum of its pieces' word sums): c = ~(sum_j ~c_j) mod 2^16.  One lane
-// per image, whole 16-B loads (np a multiple of 8).
-template <int OP>
-__global__ void __launch_bounds__(kBlock) piece_combine_kernel(const uint16_t *__restrict__ pieces, uint32_t np,
-                                                               uint64_t count, void *out) {
-  const uint64_t k = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
-  if (k >= count) return;
-  const u32x4 *p = reinterpret_cast<const u32x4 *>(pieces + k * np);
-  uint32_t lo = 0, hi = 0;  // sums of the low / high u16 of each dword of ~c (< 2^16 x 2^16 / 2: no wrap)
-  for (uint32_t i = 0; i < np / 8; ++i) {
-    const u32x4 v = p[i];
-    const uint32_t w[4] = {~v.x, ~v.y, ~v.z, ~v.w};
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      lo += w[j] & 0xFFFFu;
-      hi += w[j] >> 16;
-    }
-  }
-  const uint16_t c = static_cast<uint16_t>(~(lo + hi));  // tcp-header.h:262
-  if constexpr (OP == kVerify)
-    static_cast<uint8_t *>(out)[k] = c == 0 ? 1 : 0;
-  else
-    static_cast<uint16_t *>(out)[k] = c;
-}
-
-}  // namespace
-
-hipError_t launch_piece_combine(int op, const uint16_t *pieces, uint32_t np, uint64_t count, void *out,
-                                hipStream_t stream) {
-  if (count == 0) return hipSuccess;
-  if (!pieces || !out || (reinterpret_cast<uintptr_t>(pieces) & 15u) || np == 0 || (np & 7u) || np > 4096)
-    return hipErrorInvalidValue;
-  const uint64_t blocks = (count + kBlock - 1) / kBlock;
-  if (blocks > 0xFFFFFFFFull) return hipErrorInvalidValue;
-  const dim3 g(static_cast<uint32_t>(blocks));
-  switch (op) {
-    case kChecksum: hipLaunchKernelGGL((piece_combine_kernel<kChecksum>), g, dim3(kBlock), 0, stream, pieces, np, count, out); break;
-    case kVerify: hipLaunchKernelGGL((piece_combine_kernel<kVerify>), g, dim3(kBlock), 0, stream, pieces, np, count, out); break;
-    default: return hipErrorInvalidValue;
-  }
-  return hipGetLastError();
-}
-
 }  // namespace tcpck

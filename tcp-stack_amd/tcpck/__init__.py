@@ -61,7 +61,7 @@ PROBE_EXPORTS = ("tcpck_ctx_set_debug", "tcpck_diag_stream")
 # Kernel params libtcpck.so runs (the AUTO policy's own choices, tcpck_api.hip
 # run_fixed_impl / run_var_impl); every other value needs libtcpck_probe.so.
 SEG_AUTO_SHAPES = (0, 1, 2, 7, 8, 9, 11)  # by length, G8/U2, G16/U6, W4, W8, W16, W2 (shape_for_len)
-RSTREAM_AUTO = (20, 25, 30)               # the policy; 25: its FILL with the field pass; 30: jumbo images as pieces (+ np/8 << 8)
+RSTREAM_AUTO = (20, 25)                   # the policy; 25: its FILL with the field-block pass
 GSTREAM_AUTO = (0, 0x80, 0x401)           # (+ 4: default block order)
 SSTREAM_AUTO = (0, 32, 128)               # the policy; + 32: RECEIVE headers from the stream; + 128: FILL's deferred fields
 
