@@ -3,7 +3,7 @@
 block): does reading every image from the same offset at the same time cost
 (the blocks in flight hold consecutive images, 64 KiB apart)?  The W-wave
 shapes can start image k's chunk walk at chunk ((k rot) mod (n / 64)) 64 and
-wrap (SegArgs::rot; seg param bit 25: rot 1, bit 26: rot 37).  CHECKSUM and
+wrap (SegArgs::rot = seg param bits 8-15).  CHECKSUM and
 FILL timed against AUTO, results (and FILL's fields) compared.  Back-to-back
 launches, median of 5 rounds of 10."""
 import os
@@ -46,8 +46,8 @@ def main():
         tcpck.synth_fixed(arena, L, L, n, seed=42, stream=s)
         alg = n * L + 2 * n
         res = {}
-        forms = [("AUTO", None), ("seg W-shape, XCD order", 1 << 24), ("+ rot 1", (1 << 24) | (1 << 25)),
-                 ("+ rot 37", (1 << 24) | (1 << 26)), ("rot 1, default order", 1 << 25)]
+        forms = [("AUTO", None), ("seg W-shape, XCD order", 1 << 24), ("+ rot 1", (1 << 24) | (1 << 8)),
+                 ("+ rot 37", (1 << 24) | (37 << 8)), ("+ rot 29", (1 << 24) | (29 << 8)), ("rot 1, default order", 1 << 8)]
         for label, p in forms:
             out = torch.empty(n, dtype=torch.int16, device="cuda")
             if p is None:
@@ -64,7 +64,7 @@ def main():
         print(f"L {L:6d}  results identical: {all(torch.equal(v, ref) for v in res.values())}", flush=True)
         if L == 65536:  # FILL: AUTO (seg W16 in-stream) against the rotated form
             fres = {}
-            for label, p in (("FILL AUTO", None), ("FILL + rot 1", (1 << 24) | (1 << 25))):
+            for label, p in (("FILL AUTO", None), ("FILL + rot 1", (1 << 24) | (1 << 8)), ("FILL + rot 29", (1 << 24) | (29 << 8))):
                 out = torch.empty(n, dtype=torch.int16, device="cuda")
                 if p is None:
                     fn = lambda: ctx.batch_fixed(tcpck.OP_FILL, arena, L, L, n, out, stream=s)

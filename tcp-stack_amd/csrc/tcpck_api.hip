@@ -246,6 +246,13 @@ constexpr int kRstreamPolicy = 20;       // v_dot2 sums, buffer loads, XCD-chunk
 constexpr int kRstreamDeferFill = 25;    // FILL: kRstreamPolicy's stream to out, then the 2-B write-through field pass
 constexpr int kVvPolicy = 4 | 8 | 16;    // size policy, XCD-chunked order, L2-kept first step
 constexpr int kSegXcdOrder = 1 << 24;    // seg: XCD-chunked order
+// seg W16 on packed jumbo images (C4): image k's chunk walk starts at 1-KiB
+// step (29 k) mod 64 and wraps (SegArgs::rot), so the blocks in flight --
+// consecutive images, 64 KiB apart -- read different offsets at the same time:
+// C4 90.4 -> 92.7 % (multipliers = 1 mod 16 gain nothing, the other odd ones
+// 91.8-92.9 %; W8 at 32 KiB loses 1-1.5 points, so W16 only;
+// scripts/c4_rot_sweep.py, profiles/r03/c4_rot_sweep*.log)
+constexpr int kSegW16Rot = 29;
 // FILL of small images: nearly every line holds a checksum field, so the
 // run kernels read every step with the default cache policy; the line is then
 // still in L2 when the field store lands and leaves as a whole line instead of
@@ -345,6 +352,9 @@ hipError_t run_fixed_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint
         stride > (1u << 24)) {
       kernel = TCPCK_KERNEL_SEG;
       param = kSegXcdOrder;  // shape by length
+      if (mode == TCPCK_MODE_REF && stride == len && len <= 65536 && op != TCPCK_OP_FILL &&
+          tcpck::shape_for_len(len) == tcpck::kShapeW16)
+        param |= kSegW16Rot << 8;
     } else if (stride > len) {
       // gapped fixed strides (e.g. MSS slots) (scripts/gap_probe.py,
       // profiles/r01/gap_probe.log): streaming the gaps with the images
@@ -497,6 +507,7 @@ hipError_t run_fixed_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint
   a.out = out;
   a.oversub = static_cast<uint32_t>(param >> 16) & 0xFFu;
   a.order = ((param >> 24) & 1u) ? 4u : 0xFFu;  // bit 24: XCD-chunked order, groups of 16 blocks
+  a.rot = static_cast<uint32_t>(param >> 8) & 0xFFu;  // bits 8-15: the W-wave shapes' rotation multiplier
   const auto shape = (param & 0xFF) > 0 ? static_cast<tcpck::SegShape>((param & 0xFF) - 1) : tcpck::shape_for_len(len);
   return tcpck::launch_seg(op, mode, true, shape, a, num_cus, s);
 }

@@ -38,6 +38,8 @@ struct SegArgs {
   uint32_t len;              // fixed layout: image length
   uint32_t oversub;          // grid = resident blocks x this (0/1: one block per resident slot)
   uint32_t order;            // block order (dev::ordered_block; 0xFF default)
+  uint32_t rot;              // W-wave shapes: image k's chunks read from chunk ((k rot) mod (n / 64)) 64 on,
+                             // wrapping (0: from chunk 0) -- concurrent blocks at different offsets
 };
 
 SegShape shape_for_len(uint64_t typical_len);

@@ -114,18 +114,26 @@ __global__ void __launch_bounds__(64 * W) jumbo_kernel(SegArgs a) {
     const int64_t span = lead + static_cast<int64_t>(len);
     const uint32_t nch = static_cast<uint32_t>((span + 15) >> 4);
     const int64_t field = (OP == kFill) ? lead + 28 : -64;
+    // a.rot: this image's chunks are read from chunk rot on, wrapping -- the
+    // blocks in flight (consecutive images at the same 64-KiB phase for C4)
+    // then read different offsets at the same time; whole 1 KiB wave steps stay
+    // contiguous (rot a multiple of 64 chunks)
+    const uint32_t rot = (a.rot && nch >= 128) ? ((static_cast<uint32_t>(k) * a.rot) % (nch >> 6)) << 6 : 0u;
     uint32_t acc = 0;
     for (uint32_t i0 = t; i0 < nch; i0 += T * U) {
       u32x4 v[U];
+      uint32_t ie[U];  // the chunk read, after the rotation
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const uint32_t i = i0 + u * T;
-        const uint32_t ic = i < nch ? i : nch - 1;  // clamp: always a legal address
+        const uint32_t r = i + rot;
+        ie[u] = i < nch ? (r >= nch ? r - nch : r) : nch + i;  // past the image: masked below
+        const uint32_t ic = i < nch ? ie[u] : nch - 1;  // clamp: always a legal address
         v[u] = dev::load16_nt(p0 + 16 * static_cast<uint64_t>(ic));
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int64_t rel = 16 * static_cast<int64_t>(i0 + u * T);
+        const int64_t rel = 16 * static_cast<int64_t>(ie[u]);
         const int32_t lo = static_cast<int32_t>(min(max(lead - rel, int64_t{0}), int64_t{16}));
         const int32_t hi = static_cast<int32_t>(min(max(span - rel, int64_t{0}), int64_t{16}));
         uint32_t wm = dev::word_mask(lo, hi);

@@ -709,3 +709,68 @@ def test_vvstream_rfc1071_fixed_fill(ctx, oracle_c, stride, length, count):
     np.testing.assert_array_equal(host(ok).astype(bool),
                                   oracle_c.batch(exp_arena, stride=stride, length=length, count=count, mode=1,
                                                  threads=8) == 0)
+
+
+# ---- seg W-wave shapes with the chunk-walk rotation (SegArgs::rot = param bits 8-15) ----
+# AUTO's C4 form (seg W16, rot 29, tcpck_api.hip kSegW16Rot): image k's chunks are
+# read from 1-KiB step (rot k) mod (chunks / 64) on, wrapping; every byte is still
+# summed once, so results are the unrotated ones (include/tcp-header.h:252-263).
+@pytest.mark.parametrize("shape", [11, 7, 8, 9])  # W2, W4, W8, W16
+@pytest.mark.parametrize("rot", [1, 29, 64, 255])
+@pytest.mark.parametrize("length,stride", [(65536, 65536), (65534, 65536), (49152, 49152), (40000, 40000),
+                                           (16384, 16384), (9000, 9216), (2048, 2048), (131072, 131072)])
+def test_seg_wave_shapes_rotated(ctx, oracle_c, shape, rot, length, stride):
+    import tcpck
+    from oracle import ref16 as R
+    count = max(3, min(300, (24 << 20) // stride))
+    rng = np.random.default_rng(length + 7 * rot + shape)
+    arena_np = rng.integers(0, 256, count * stride + 128, dtype=np.uint8)
+    arena_np[:length] = 0xFF
+    buf = dev(arena_np)
+    param = (1 << 24) | (rot << 8) | shape
+    for mis in (0, 2, 126):
+        out = torch.empty(count, dtype=torch.int16, device="cuda")
+        ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, buf.data_ptr() + mis, stride, length, count, out, tcpck.KERNEL_SEG, param)
+        exp = oracle_c.batch(arena_np[mis:], stride=stride, length=length, count=count, threads=8)
+        np.testing.assert_array_equal(host(out).view(np.uint16), exp)
+    # FILL in place, then VERIFY with a few images damaged
+    img = arena_np[:count * stride].copy()
+    a = dev(img)
+    out = torch.empty(count, dtype=torch.int16, device="cuda")
+    ctx.batch_fixed_ex(tcpck.OP_FILL, a, stride, length, count, out, tcpck.KERNEL_SEG, param)
+    exp_img = img.copy()
+    exp = np.array([R.fill_np(exp_img[k * stride:k * stride + length]) for k in range(count)], np.uint16)
+    np.testing.assert_array_equal(host(out).view(np.uint16), exp)
+    got = host(a)
+    np.testing.assert_array_equal(got, exp_img)
+    bad = np.sort(rng.choice(count, 3, replace=False))
+    for k in bad:
+        got[k * stride + int(rng.integers(0, length))] ^= 0x81
+    ok = torch.empty(count, dtype=torch.uint8, device="cuda")
+    ctx.batch_fixed_ex(tcpck.OP_VERIFY, dev(got), stride, length, count, ok, tcpck.KERNEL_SEG, param)
+    np.testing.assert_array_equal(np.nonzero(host(ok) == 0)[0], bad)
+
+
+@pytest.mark.parametrize("length", [49152, 57344, 65520, 65536])
+def test_auto_packed_w16_rotated(ctx, oracle_c, length):
+    """AUTO on packed jumbo images that take seg W16 (rot 29): CHECKSUM, VERIFY and RECEIVE's verdicts."""
+    import tcpck
+    from oracle import ref16 as R
+    count = 400
+    rng = np.random.default_rng(length)
+    img = rng.integers(0, 256, count * length, dtype=np.uint8)
+    out = torch.empty(count, dtype=torch.int16, device="cuda")
+    ctx.batch_fixed(tcpck.OP_CHECKSUM, dev(img), length, length, count, out)
+    np.testing.assert_array_equal(host(out).view(np.uint16),
+                                  oracle_c.batch(img, stride=length, length=length, count=count, threads=8))
+    for k in range(count):
+        R.fill_np(img[k * length:(k + 1) * length])
+    bad = np.sort(rng.choice(count, 7, replace=False))
+    for k in bad:
+        img[k * length + int(rng.integers(0, length))] ^= 0x10
+    ok = torch.empty(count, dtype=torch.uint8, device="cuda")
+    ctx.batch_fixed(tcpck.OP_VERIFY, dev(img), length, length, count, ok)
+    np.testing.assert_array_equal(np.nonzero(host(ok) == 0)[0], bad)
+    hdr = torch.empty(count * 32, dtype=torch.uint8, device="cuda")
+    ctx.batch_receive(dev(img), count, ok, hdr, stride=length, length=length)
+    np.testing.assert_array_equal(np.nonzero(host(ok) == 0)[0], bad)
