@@ -56,7 +56,11 @@ extern "C" {
 #define TCPCK_OP_CHECKSUM 0  /* out[k] (u16) = checksum of image k              */
 #define TCPCK_OP_FILL 1      /* zero bytes 28-29 of image k, compute, store the
                                 result there in place (send path); out[k] (u16)
-                                also receives it unless out == NULL.  len >= 30 */
+                                also receives it unless out == NULL.  len >= 30.
+                                Only bytes 28-29 change; for packed images of
+                                <= 128 B the kernel may store the image's other
+                                16-B chunks back unchanged (never bytes outside
+                                an image)                                       */
 #define TCPCK_OP_VERIFY 2    /* out[k] (u8) = (checksum of image k == 0)
                                 (receive path, socket-manager.h:182)            */
 #define TCPCK_OP_RECEIVE 3   /* ReceivePacket's front half (socket-manager.h:
