@@ -302,10 +302,12 @@ hipError_t launch_one(const FixedStreamArgs &a, uint32_t num_cus, hipStream_t st
   // runs of >= 4 KiB (4-8 KiB: C2 1M x 1492 B at 32x, C5 8M at 256x), up to 1024 x the resident grid
   uint64_t blocks = resident * dev::oversub_for(a.oversub, a.count * a.stride, resident * kWavesPerBlock, 1024);
   const uint64_t need = (a.count + kWavesPerBlock - 1) / kWavesPerBlock;  // >= 1 image per wave
-  // images of >= 4 KiB that the policy's grid would give fewer than two per
-  // wave: one each (4096 B at C2's size: 1.46 per wave, runs of 4 or 8 KiB,
-  // 89.3 % -> 91.2-91.8 % with one; scripts/pow2_probe.py, profiles/r03/pow2_probe.log)
-  if (!a.oversub && a.stride >= 4096 && a.count < 2 * blocks * kWavesPerBlock) blocks = need;
+  // images of >= 3.5 KiB that the policy's grid would give fewer than two per
+  // wave: one each (at C2's size 4096 B: 1.46 per wave, runs of 4 or 8 KiB,
+  // 89.3 % -> 91.2-91.9 % with one; 4000 B 91.3 -> 93.4 %; 3500 B 91.3 -> 92.0 %;
+  // 3000 B keeps the policy: 3-KiB runs 87.6 %; scripts/pow2_probe.py,
+  // scripts/run_len_probe.py, profiles/r03/pow2_probe.log, run_len_probe.log)
+  if (!a.oversub && a.stride >= 3584 && a.count < 2 * blocks * kWavesPerBlock) blocks = need;
   if (blocks > need) blocks = need;
   if (blocks == 0) return hipSuccess;
   FixedStreamArgs b = a;
