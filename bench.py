@@ -17,14 +17,19 @@ ONE JSON line with the driver's fields plus:
                 algorithmic bytes per launch (sum of image bytes + 2 B written
                 per image) / average launch time (HIP events on the launch
                 stream around the K launches, / K); traffic = PMC HBM bytes
-                per launch from the committed rocprofv3 pass
-                (profiles/pmc_summary.json), else null
+                per launch from the committed rocprofv3 passes
+                (profiles/pmc_summary.json) when they were captured on the
+                very libtcpck.so loaded (sha256 stamp), else null with the
+                reason in traffic_source
   c3, c4        (default C2 run only) BASELINE configs[2] and [3] timed the same
                 way in the same process, after C2: each rank its own batch
-  fill, slots,  (default C2 run only) the SURVEY §8f rows timed the same way:
-  receive,      send-side FILL on C2's layout, VERIFY and RECEIVE (verdicts +
-  segment       host-order headers) on a 1M-slot receive ring, the send stream
-                cut into checksummed MSS images; each with its own metric
+  fill,         (default C2 run only) the SURVEY §8f rows timed the same way:
+  fill_noout,   send-side FILL on C2's layout with and without a results
+  fill_c3,      buffer (the reference's call shape) and on C3's mix; C2 in
+  c2_rfc,       RFC 1071 mode; VERIFY and RECEIVE (verdicts + host-order
+  slots,        headers) on a 1M-slot receive ring, the send stream cut into
+  receive,      checksummed MSS images; each with its own metric
+  segment
   c5_strong     (default C2 run only) BASELINE configs[4]: ONE 8M x 1492-B batch
                 split over the N ranks with shard_range (8M images on one GPU
                 at N=1, 1M per GPU at N=8); value = all ranks' bytes / the
@@ -33,8 +38,10 @@ ONE JSON line with the driver's fields plus:
   cpu_baseline  the reference's own CalculateChecksum (oracle/_ref, built from
                 /root/reference/include/tcp-header.h) on the host cores over the
                 whole C2 arena (DRAM-sized: 6x the host L3), median of 7 passes
-                (rank 0, N=1 only); falls back to the in-repo C restatement
-                ("port") where oracle/_ref is absent
+                with min / max (rank 0, N=1 only); falls back to the in-repo C
+                restatement ("port") where oracle/_ref is absent.  The c3 key
+                carries one over the whole C3 arena, c4 over C4's first 2 GiB,
+                c2_rfc the RFC 1071 restatement ("port") over C2's arena
   e2e           host-memory rate incl. pinned hipMemcpyAsync H2D + D2H (not `value`)
   settle        untimed launches run before the W warm-up steps until --settle-ms
                 has passed (the idle GPU's clock ramp, scripts/transient.py)
@@ -74,8 +81,9 @@ STRONG = {"c5"}  # configs whose total work is fixed as N grows; the rest are pe
 # (the big C3 / C4 arenas last: C5 timed after C3/C4 had allocated and freed 19 GB ran 2.5 % slower
 # than in a process of its own -- 1.737 vs 1.695 ms, profiles/r03/c5_order_probe.log; in this order
 # every config matches its own process within 1 %, profiles/r03/bench_order_probe.log)
-EXTRAS = (("c5", "c5_strong"), ("fill", "fill"), ("slots", "slots"), ("receive", "receive"),
-          ("segment", "segment"), ("c3", "c3"), ("c4", "c4"))
+EXTRAS = (("c5", "c5_strong"), ("fill", "fill"), ("fill_noout", "fill_noout"), ("c2_rfc", "c2_rfc"),
+          ("slots", "slots"), ("receive", "receive"), ("segment", "segment"), ("c3", "c3"), ("fill_c3", "fill_c3"),
+          ("c4", "c4"))
 # round-2 ops (not BASELINE configs; same contract, their own metric):
 EXTRA = {
     # the device-resident receive arena: 1M 2048-B slots, one datagram per slot
@@ -88,6 +96,16 @@ EXTRA = {
     # the send path's insert (socket-manager.cc:9-10) on C2's layout: zero, compute, store in place
     "fill": ("send-side FILL on C2's layout: 1M x 1492-B images, fixed stride, checksum field zeroed, computed "
              "and stored in place, results also to a u16 array", "fill", 1 << 20, 1492),
+    # the same without a results buffer: the reference's call shape (socket-manager.cc:9-10 stores only into
+    # the packet); the library keeps its two-pass form through the context's results scratch
+    "fill_noout": ("send-side FILL on C2's layout without a results buffer (the reference's call shape): 1M x "
+                   "1492-B images, checksum field zeroed, computed and stored in place", "fill", 1 << 20, 1492),
+    # FILL on C3's mix (packed offsets): the send path's insert on variable-length segments
+    "fill_c3": ("send-side FILL on C3's mix: 4M images of 96/608/1492 B, packed, u64 offsets, fields stored in "
+                "place, results also to a u16 array", "fill_var", 4 << 20, None),
+    # the opt-in RFC 1071 arithmetic (end-around carry) on C2's batch
+    "c2_rfc": ("C2 in TCPCK_MODE_RFC1071 (opt-in one's-complement with end-around carry; not the reference's "
+               "arithmetic): 1M x 1492-B images, fixed stride", "fixed", 1 << 20, 1492),
     # the send path's producer: a 1.5 GB send stream cut into MSS segments
     "segment": ("send stream 1.5 GiB -> 1460-B segments in 1504-B slots (header template + payload, "
                 "checksum filled; tcpck_batch_segment)", "segment", (1460 << 20) + 2, 1460),
@@ -96,6 +114,8 @@ EXTRA = {
 
 IMAGE_BYTES = {"slots": "96/608/1492 in 2048-B slots", "receive": "96/608/1492 in 2048-B slots",
                "segment": "32 + 1460 in 1504-B slots"}
+MODES = {"c2_rfc": 1}  # TCPCK_MODE_RFC1071; every other config runs the reference arithmetic (0)
+NO_RESULTS = {"fill_noout"}  # steps that write no results array (only the fields in place)
 
 
 def log(*a):
@@ -162,6 +182,8 @@ class Workload:
         desc, kind, count, L = CONFIGS[name] if name in CONFIGS else EXTRA[name]
         self.name, self.desc, self.kind, self.L = name, desc, kind, L
         self.strong = name in STRONG
+        self.mode = MODES.get(name, 0)
+        mode = self.mode
         if self.strong:
             first, stop = shard_range(count, world, rank)  # independent contiguous shard, no exchange
             count = stop - first
@@ -211,16 +233,17 @@ class Workload:
             tcpck.synth_fixed(arena, L, L, count, seed=42, first_index=first, stream=stream)
             img_bytes = count * L
             self.extra_bytes = 2 * count  # the fields written in place (+2 per result below)
+            with_out = name not in NO_RESULTS
 
             def step(out):
-                ctx.batch_fixed(tcpck.OP_FILL, arena, L, L, count, out, stream=stream)
+                ctx.batch_fixed(tcpck.OP_FILL, arena, L, L, count, out if with_out else None, stream=stream)
         elif kind == "fixed":
             arena = torch.empty(count * L, dtype=torch.uint8, device="cuda")
             tcpck.synth_fixed(arena, L, L, count, seed=42, first_index=first, stream=stream)
             img_bytes = count * L
 
             def step(out):
-                ctx.batch_fixed(tcpck.OP_CHECKSUM, arena, L, L, count, out, stream=stream)
+                ctx.batch_fixed(tcpck.OP_CHECKSUM, arena, L, L, count, out, mode=mode, stream=stream)
         else:
             from synth_np import mixed_layout
             off, ln, total = mixed_layout(count, seed=42 + rank)
@@ -232,12 +255,20 @@ class Workload:
             lmin, lmax = int(ln.min()), int(ln.max())  # host-side layout hint, computed once
             self.layout = (off, ln)
 
-            def step(out):
-                ctx.batch_var(tcpck.OP_CHECKSUM, arena, d_off, d_ln, count, out, total_bytes=img_bytes,
-                              min_len=lmin, max_len=lmax, packed=True, stream=stream)
-        self.arena = arena if kind in ("fixed", "mixed", "fill", "slots", "receive") else None
+            if kind == "fill_var":
+                self.extra_bytes = 2 * count  # the fields written in place (+2 per result below)
+
+                def step(out):
+                    ctx.batch_var(tcpck.OP_FILL, arena, d_off, d_ln, count, out, total_bytes=img_bytes,
+                                  min_len=lmin, max_len=lmax, packed=True, stream=stream)
+            else:
+                def step(out):
+                    ctx.batch_var(tcpck.OP_CHECKSUM, arena, d_off, d_ln, count, out, total_bytes=img_bytes,
+                                  min_len=lmin, max_len=lmax, packed=True, stream=stream)
+        self.arena = arena if kind in ("fixed", "mixed", "fill", "fill_var", "slots", "receive") else None
         self.count, self.first, self.img_bytes = count, first, img_bytes
         self.verdicts = kind in ("slots", "receive")  # u8 results
+        self.results_written = name not in NO_RESULTS
         self.out = torch.empty(count, dtype=torch.uint8 if self.verdicts else torch.int16, device="cuda")
         self._step = step
         torch.cuda.synchronize()
@@ -248,7 +279,8 @@ class Workload:
     @property
     def algo_bytes(self) -> int:
         """Algorithmic bytes per launch: image bytes read + other bytes written + the results."""
-        return self.img_bytes + self.extra_bytes + (1 if self.verdicts else 2) * self.count
+        res = ((1 if self.verdicts else 2) * self.count) if self.results_written else 0
+        return self.img_bytes + self.extra_bytes + res
 
     def results(self) -> np.ndarray:
         import torch
@@ -320,8 +352,9 @@ def measure(w: Workload, args, world, stream, coll_dev):
 def roofline(w: Workload, launch_ms, launch_ms_all, traffic_key, world):
     algo = w.algo_bytes
     achieved = algo / (launch_ms * 1e-3) / 1e9
+    traffic, note = pmc_traffic(traffic_key) if world == 1 else (None, "PMC passes are single-GPU runs")
     r = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(traffic_key) if world == 1 else None,
+         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": note,
          "algorithmic_bytes_per_launch": algo, "avg_launch_ms": round(launch_ms, 5)}
     if world > 1:  # rank 0's kernel above; every GPU's fraction here (equal shards)
         r["per_gpu_frac"] = [round(algo / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) for ms in launch_ms_all]
@@ -333,11 +366,13 @@ def extra_config(name, key, ctx, stream, rank, world, args, coll_dev):
     import torch
     w = Workload(name, ctx, stream, rank, world)
     tmax, launch_ms, launch_ms_all, step_bytes, settle = measure(w, args, world, stream, coll_dev)
-    rec = {"workload": w.desc, "metric": metric_for(w.kind), "value": round(step_bytes * args.steps / tmax / GIB, 2),
+    rec = {"workload": w.desc, "metric": metric_for(w.kind, w.mode), "value": round(step_bytes * args.steps / tmax / GIB, 2),
            "unit": "GiB/s",
            "ms_per_step": round(tmax / args.steps * 1e3, 5), "scaling": "strong" if w.strong else "weak",
            "images_per_gpu": w.count, "bytes_per_gpu": w.img_bytes,
            "roofline": roofline(w, launch_ms, launch_ms_all, name, world), "settle": settle}
+    if name in CPU_EXTRA and rank == 0 and world == 1 and not args.no_cpu_baseline:
+        rec["cpu_baseline"] = cpu_baseline_for(w, CPU_EXTRA[name][1])
     if w.strong:
         # the 8M-image batch's bytes over the slowest GPU's kernel time
         rec["kernel_GiBs"] = round(step_bytes / (max(launch_ms_all) * 1e-3) / GIB, 2)
@@ -386,7 +421,7 @@ def main():
     # End to end through PCIe (never `value`): every rank at once, so the
     # driver's N-GPU runs also record the host-memory path's aggregate rate
     e2e = None
-    if not args.no_e2e and w.kind == "fixed" and not w.strong:
+    if not args.no_e2e and w.kind == "fixed" and not w.strong and w.mode == 0:
         if world > 1:
             dist.barrier()
         dt, ok = e2e_seconds(ctx, w.arena, res, w.count, w.L)
@@ -399,9 +434,9 @@ def main():
                    "results_match_device_path": ok_all}
 
     want_cpu = rank == 0 and world == 1 and not args.no_cpu_baseline and w.kind in ("fixed", "mixed")
-    host_arena = w.arena.cpu().numpy() if want_cpu else None
+    cpu_rec = cpu_baseline_for(w, args.cpu_seconds) if want_cpu else None  # before the extras free the arena
     rec = {
-        "metric": metric_for(w.kind), "value": round(value, 2), "unit": "GiB/s", "n_gpus": world,
+        "metric": metric_for(w.kind, w.mode), "value": round(value, 2), "unit": "GiB/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(tmax / args.steps * 1e3, 5),
         "higher_is_better": True,
         "scaling": "strong" if w.strong else "weak", "vs_baseline": None, "dtype": "u16",
@@ -413,7 +448,6 @@ def main():
         "roofline": roofline(w, launch_ms, launch_ms_all, args.config, world),
         "settle": settle,
     }
-    kind, count, L, layout = w.kind, w.count, w.L, w.layout
     del w
     torch.cuda.empty_cache()
 
@@ -422,8 +456,8 @@ def main():
         for name, key in EXTRAS:
             k, r = extra_config(name, key, ctx, stream, rank, world, args, coll_dev)
             rec[k] = r
-    if want_cpu:
-        rec["cpu_baseline"] = cpu_baseline(host_arena, res, kind, count, L, args.cpu_seconds, layout)
+    if cpu_rec is not None:
+        rec["cpu_baseline"] = cpu_rec
     if e2e is not None:
         rec["e2e"] = e2e
     if rank == 0:
@@ -434,10 +468,13 @@ def main():
     ctx.close()
 
 
-def metric_for(kind):
+def metric_for(kind, mode=0):
+    if mode == 1:
+        return ("GiB/s device-resident TCP checksum in RFC 1071 mode (opt-in end-around carry, not the reference's "
+                "arithmetic) over batched segments; % HBM roofline")
     if kind == "slots":
         return "GiB/s device-resident TCP verify over a slotted receive arena (image bytes); % HBM roofline"
-    if kind == "fill":
+    if kind in ("fill", "fill_var"):
         return "GiB/s device-resident TCP send-side fill (zero, checksum, store in place) over batched segments; % HBM roofline"
     if kind == "receive":
         return ("GiB/s device-resident TCP receive (verify + TcpHeaderN2H into a header array) over a slotted "
@@ -447,15 +484,35 @@ def metric_for(kind):
     return METRIC
 
 
+_LIB_SHA = None
+
+
+def lib_sha256() -> str:
+    """sha256 of the libtcpck.so this process loaded (the PMC stamps name it)."""
+    global _LIB_SHA
+    if _LIB_SHA is None:
+        import hashlib
+        import tcpck
+        with open(tcpck.LIB_PATH, "rb") as f:
+            _LIB_SHA = hashlib.sha256(f.read()).hexdigest()
+    return _LIB_SHA
+
+
 def pmc_traffic(config: str):
-    """HBM bytes per launch from the committed rocprofv3 PMC pass, if one exists."""
+    """(HBM bytes per launch, note) from the committed rocprofv3 PMC passes
+    (profiles/pmc_summary.json), or (None, why) when there is no pass for this
+    config or it was captured on another build of libtcpck.so than the one
+    loaded (each entry carries the library's sha256)."""
     p = os.path.join(ROOT, "profiles", "pmc_summary.json")
     try:
         with open(p) as f:
-            d = json.load(f)
-        return d[config]["hbm_bytes_per_launch"]
+            e = json.load(f)[config]
     except (OSError, KeyError, ValueError):
-        return None
+        return None, f"no PMC pass for {config} in profiles/pmc_summary.json"
+    if e.get("lib_sha256") != lib_sha256():
+        return None, (f"PMC pass captured on libtcpck.so sha256 {str(e.get('lib_sha256'))[:16]}, loaded "
+                      f"{lib_sha256()[:16]}: not this build")
+    return e["hbm_bytes_per_launch"], f"{e['source']} (libtcpck.so sha256 {lib_sha256()[:16]})"
 
 
 def cpu_threads() -> tuple[int, dict]:
@@ -469,66 +526,94 @@ def cpu_threads() -> tuple[int, dict]:
     return max(1, n), {"affinity_cpus": aff, "nproc": os.cpu_count(), "omp_num_threads": omp or None}
 
 
-def cpu_baseline(host_arena, gpu_res, kind, count, L, budget_s, var_layout):
-    """Reference CalculateChecksum on the host cores over the WHOLE batch (the
-    C2 arena is 1.56 GB, ~6x the host's 256 MB L3, so the passes stream from
-    DRAM like the GPU's): 5 timed passes of `reps` sweeps each, median."""
+def cpu_baseline(host_arena, gpu_res, sargs, sbytes, sdesc, budget_s, mode=0, secondary_o0=False):
+    """The reference's CalculateChecksum (oracle/_ref, tcp-header.h:252-263) on
+    the host cores over `host_arena` (sargs: stride/length/count or
+    offsets/lengths), every packet materialised once with MakeNetPacket:
+    7 timed passes of ~budget_s / 7 each, median, with min / max and every
+    pass.  RFC 1071 mode (not the reference's arithmetic) and a missing
+    oracle/_ref use the in-repo C restatement (oracle/ref16.c, "port")."""
     from oracle import ref16 as R
     nthr, counts = cpu_threads()
-    if kind == "fixed":
-        sargs = dict(stride=L, length=L, count=count)
-        sbytes = count * L
-    else:
-        off, ln = var_layout
-        sargs = dict(offsets=off, lengths=ln)
-        sbytes = int(ln.astype(np.int64).sum())
-    sdesc = f"all {count} images of the batch ({sbytes / 1e9:.2f} GB, host copy), MakeNetPacket once"
     out = {"unit": "GiB/s", "cores": nthr, **counts}
-    if R.RefLib.available("O3"):
-        kind_s = "reference"
+    n = int(sargs["count"]) if "count" in sargs else int(np.asarray(sargs["offsets"]).size)
+
+    def summary(rates):
+        return {"value": round(statistics.median(rates), 2), "min_GiBs": round(min(rates), 2),
+                "max_GiBs": round(max(rates), 2), "passes_GiBs": [round(r, 1) for r in rates]}
+
+    if mode == 0 and R.RefLib.available("O3"):
         pk = R.RefLib("O3").packets(host_arena, **sargs)  # MakeNetPacket once, outside timing
 
         def passes(lib_pk, threads, n_pass, target_s):
-            """Median GiB/s over n_pass timed passes of ~target_s each."""
+            """GiB/s of n_pass timed passes of ~target_s each."""
             t1 = lib_pk.run_reps(threads, 1)
             reps = max(1, int(target_s / max(t1, 1e-6)))
-            rates = [sbytes * reps / lib_pk.run_reps(threads, reps) / GIB for _ in range(n_pass)]
-            return statistics.median(rates), rates, reps
+            return [sbytes * reps / lib_pk.run_reps(threads, reps) / GIB for _ in range(n_pass)], reps
 
         got, _ = pk.run(nthr)
-        match = bool(np.array_equal(got, gpu_res[:count]))
-        med, rates, reps = passes(pk, nthr, 7, budget_s / 7)
-        one, _, _ = passes(pk, 1, 1, 0.5)
+        match = bool(np.array_equal(got, gpu_res[:n]))
+        rates, reps = passes(pk, nthr, 7, budget_s / 7)
+        one, _ = passes(pk, 1, 1, 0.5)
         pk.close()
-        out.update({"value": round(med, 2), "kind": kind_s, "one_thread_GiBs": round(one, 2),
-                    "passes_GiBs": [round(r, 1) for r in rates], "best_GiBs": round(max(rates), 2),
-                    "sample": sdesc + f"; median of 7 passes of {reps} sweeps on {nthr} threads; CalculateChecksum "
-                              f"(tcp-header.h:252-263) built -O3 -march=x86-64-v3; results == GPU results: {match}"})
-        if R.RefLib.available("O0"):
+        out.update(summary(rates))
+        out.update({"kind": "reference", "one_thread_GiBs": round(one[0], 2),
+                    "sample": sdesc + f"; 7 passes of {reps} sweeps on {nthr} threads (median; min/max beside it); "
+                              "CalculateChecksum (tcp-header.h:252-263) built -O3 -march=x86-64-v3; results == GPU "
+                              f"results: {match}"})
+        if secondary_o0 and R.RefLib.available("O0"):
             # secondary: the reference as its makefile builds it (-O0 -g, makefile:2), same threads
             p0 = R.RefLib("O0").packets(host_arena, **sargs)
-            med0, rates0, _ = passes(p0, nthr, 5, 0.3)
+            rates0, _ = passes(p0, nthr, 5, 0.3)
             p0.close()
-            out["reference_O0_GiBs"] = round(med0, 2)
+            out["reference_O0_GiBs"] = round(statistics.median(rates0), 2)
             out["reference_O0_note"] = f"-O0 -g build (makefile:2), median of 5 passes on {nthr} threads"
     else:
         c = R.Ref16C(build=False)
+        got = c.batch(host_arena, mode=mode, threads=nthr, **sargs)
         t0 = time.perf_counter()
-        got = c.batch(host_arena, threads=nthr, **sargs)
-        dt = []
-        for _ in range(5):
+        c.batch(host_arena, mode=mode, threads=nthr, **sargs)
+        t1 = max(time.perf_counter() - t0, 1e-6)
+        reps = max(1, int(budget_s / 7 / t1))
+        rates = []
+        for _ in range(7):
             t0 = time.perf_counter()
-            c.batch(host_arena, threads=nthr, **sargs)
-            dt.append(time.perf_counter() - t0)
-        out.update({"value": round(sbytes / statistics.median(dt) / GIB, 2), "kind": "port",
-                    "sample": sdesc + f"; oracle/ref16.c restatement, median of 5 passes; results == GPU "
-                              f"results: {bool(np.array_equal(got, gpu_res[:count]))}"})
-    log(f"cpu baseline: {out['value']} GiB/s on {nthr} threads ({out.get('one_thread_GiBs')} on 1)")
+            for _ in range(reps):
+                c.batch(host_arena, mode=mode, threads=nthr, **sargs)
+            rates.append(sbytes * reps / (time.perf_counter() - t0) / GIB)
+        out.update(summary(rates))
+        what = "RFC 1071 restatement (oracle/ref16.c oracle_rfc1071)" if mode else "oracle/ref16.c restatement"
+        out.update({"kind": "port", "sample": sdesc + f"; {what}, 7 passes of {reps} sweeps on {nthr} threads "
+                                                      f"(median; min/max beside it); results == GPU results: "
+                                                      f"{bool(np.array_equal(got, gpu_res[:n]))}"})
+    log(f"cpu baseline: {out['value']} GiB/s on {nthr} threads (min {out['min_GiBs']}, max {out['max_GiBs']})")
     try:
         out["cpu_model"] = open("/proc/cpuinfo").read().split("model name")[1].split("\n")[0].strip(": \t")
     except Exception:
         pass
     return out
+
+
+# CPU baselines beside the extra keys (rank 0, N = 1): (config -> images of the batch's head timed, seconds)
+CPU_EXTRA = {"c3": (None, 6.0), "c4": (32768, 6.0), "c2_rfc": (None, 4.0)}
+
+
+def cpu_baseline_for(w: "Workload", budget_s: float):
+    """cpu_baseline over the same bytes as workload w (C4: its first 2 GiB)."""
+    res = w.results()
+    if w.kind == "mixed":
+        off, ln = w.layout
+        host_arena = w.arena.cpu().numpy()
+        sbytes = int(ln.astype(np.int64).sum())
+        return cpu_baseline(host_arena, res, dict(offsets=off, lengths=ln), sbytes,
+                            f"all {w.count} images of the batch ({sbytes / 1e9:.2f} GB, host copy)", budget_s, w.mode)
+    n = CPU_EXTRA.get(w.name, (None,))[0] or w.count
+    host_arena = w.arena[:n * w.L].cpu().numpy()
+    sbytes = n * w.L
+    what = f"all {n} images of the batch" if n == w.count else f"the batch's first {n} images (a contiguous subset)"
+    return cpu_baseline(host_arena, res, dict(stride=w.L, length=w.L, count=n), sbytes,
+                        f"{what} ({sbytes / 1e9:.2f} GB, host copy)", budget_s, w.mode,
+                        secondary_o0=w.name == "c2")
 
 
 def e2e_seconds(ctx, arena, gpu_res, count, L):

@@ -13,17 +13,40 @@
 extern "C" {
 #endif
 
-/* tcpck_batch_fixed_ex kernel id: FILL's deferred field pass ALONE
- * (launch_patch_fields) -- each field's 64-B block read and written back whole
- * with d_out[k] (u16) patched in; no checksum is computed.  For timing the
- * pass apart from the stream (scripts/fill_drain_probe.py).  param = 1 + the
- * block stores' cache bits (sc0 1 | nt 2 | sc1 4), 0 = a plain store, | form
- * << 4: 0 the 64-B block, 1 the 16-B chunk, 2 the 2-B field, 3 the 128-B line,
- * 4-7 the 2-B write-through field with other thread maps, 12 the 32-B block;
- * 8 / 9 / 10 / 11 the 64-B / 128-B / 16-B / 32-B block written without
- * reading it (zeros around the field: destroys the images, whole-block write
- * timing only). */
+/* tcpck_batch_fixed_ex kernel id: FILL's deferred field pass ALONE, in one of
+ * its measured forms (launch_patch_fields' timing kernels) -- d_out[k] (u16)
+ * stored into image k's field; no checksum is computed.  For timing the pass
+ * apart from the stream (scripts/fill_drain_probe.py).  param = 1 + the
+ * stores' cache bits (sc0 1 | nt 2 | sc1 4), 0 = a plain C++ store, | form
+ * << 4: 0 the field's 64-B block read and written back whole, 1 the 16-B
+ * chunk, 2 the 2-B field, 3 the 128-B line, 4-7 the 2-B write-through field
+ * with other thread maps (cache bits ignored), 12 the 32-B block; 8 / 9 / 10 /
+ * 11 the 64-B / 128-B / 16-B / 32-B block written without reading it (zeros
+ * around the field: destroys the images, whole-block write timing only).
+ * param 0 is therefore the 64-B block with a plain store; the product's pass
+ * (one 2-B write-through store per image) is form 2 with bits sc0 sc1 nt,
+ * param 0x28. */
 #define TCPCK_KERNEL_PATCH 12
+
+/* tcpck_probe_receive_ex: tcpck_batch_receive_ex with the header pass in a
+ * measured form, chosen by a flags word of its own (param keeps
+ * tcpck_tuning.h's meaning):
+ *   HDR_FIRST   offset lists, with TCPCK_PARAM_RECEIVE_TWO_PASS: the header
+ *               pass before the VERIFY pass
+ *   CONCURRENT  the header pass on the context's side stream, beside VERIFY
+ *   HDR_WT      the header array stores written through (sc0 sc1 nt)
+ *   HDR_WIDE    two lanes per 16-B aligned image, one 16-B buffer load each,
+ *               with the load cache bits (flags >> CACHE_SHIFT) & 3: 0
+ *               default, 1 nt, 2 sc0 sc1, 3 sc1 */
+#define TCPCK_PROBE_RECEIVE_HDR_FIRST 1
+#define TCPCK_PROBE_RECEIVE_CONCURRENT 2
+#define TCPCK_PROBE_RECEIVE_HDR_WT 4
+#define TCPCK_PROBE_RECEIVE_HDR_WIDE 8
+#define TCPCK_PROBE_RECEIVE_CACHE_SHIFT 4
+int tcpck_probe_receive_ex(tcpck_ctx *ctx, int mode, void *d_arena, uint64_t stride, uint32_t len,
+                           const uint64_t *d_offsets, const uint32_t *d_lengths, uint64_t count, uint8_t *d_ok,
+                           void *d_hdr, const tcpck_layout *layout, int kernel, int param, int probe_flags,
+                           tcpck_stream stream);
 
 /* Device buffer of 4 x u64 per wave receiving {start, end} s_memrealtime
  * (100 MHz) stamps, HW_ID and XCC_ID from the rstream variants built with

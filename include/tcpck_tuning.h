@@ -9,14 +9,18 @@
  *                      policy picks, so here it accepts exactly AUTO's own
  *                      choices: SEG shapes 0 (by length), 1, 2, 7, 8, 9, 11;
  *                      RSTREAM variant 20 (FILL also 25); VVSTREAM variant 4
- *                      with any of the flags + 8 / + 16 / + 32; GSTREAM FILL
- *                      with 0, 0x80 or 0x401 (+ 4); SSTREAM 0 (RECEIVE also
- *                      + 32); tcpck_batch_segment_ex variant 0 (+ 8); with any
- *                      oversubscription / cap bits and the TCPCK_PARAM_* bits
- *                      below.  Any other value returns an error there
- *                      (hipErrorInvalidValue).
- *   libtcpck_probe.so  the same sources built with -DTCPCK_PROBE: every
- *                      variant documented below, plus tcpck_probe.h.
+ *                      with any of the flags + 8 / + 16 / + 32 / + 64;
+ *                      GSTREAM FILL with 0, 0x80 or 0x401 (+ 4); SSTREAM 0,
+ *                      + 32 (RECEIVE into a header array) and + 128 (FILL
+ *                      with a results buffer); tcpck_batch_segment_ex
+ *                      variant 0 (+ 8); with any oversubscription / cap bits
+ *                      and the TCPCK_PARAM_* bits below.  Any other value
+ *                      returns an error there (hipErrorInvalidValue).
+ *   libtcpck_probe.so  the same router and kernels built with -DTCPCK_PROBE
+ *                      (tcp-stack_amd/csrc/tcpck_ex_probe.hip in place of
+ *                      tcpck_ex.hip): every variant documented below, plus
+ *                      tcpck_probe.h.  With an explicit kernel its RECEIVE
+ *                      also fuses the headers into sstream's other forms.
  */
 #ifndef TCPCK_TUNING_H_
 #define TCPCK_TUNING_H_
@@ -75,7 +79,10 @@ extern "C" {
                                    run's first step read with the default cache
                                    policy; 28 = the policy's; + 32: FILL reads
                                    every step with the default policy, AUTO's
-                                   choice for images up to 448 B)
+                                   choice for images up to 448 B; + 64: FILL
+                                   with a results buffer writes the results
+                                   only and the write-through field pass
+                                   stores the fields)
                                    | (blocks per CU cap << 8: LDS padding)
                                    | (grid oversubscription << 16: 0 = by batch
                                    size, 1 = none, M = M x the resident grid)   */
@@ -104,11 +111,16 @@ extern "C" {
                                    images for offset lists); REF and RFC 1071
                                    (images < 128 KiB); param = variant (0:
                                    policy = 4 steps in flight, scattered block
-                                   order; 1: 4 steps in flight, 2: 8; + 4:
+                                   order; RECEIVE into a header array: + 32
+                                   each header from the stream's registers
+                                   (AUTO's for images up to 256 B); FILL with
+                                   a results buffer: + 128 the results only,
+                                   the write-through field pass stores the
+                                   fields (AUTO's from 512 B).  Probe library
+                                   only: 1: 4 steps in flight, 2: 8; + 4:
                                    default block order, + 8: scattered, else
-                                   XCD-chunked; RECEIVE into a header array
-                                   only: + 32 each header from the stream's
-                                   registers (AUTO), + 64 with nt stores; else
+                                   XCD-chunked; + 64 with + 32: write-through
+                                   header stores; without + 32 the headers are
                                    converted after the run's verdicts, + 16
                                    with the stream read with the default cache
                                    policy)
@@ -120,14 +132,22 @@ extern "C" {
  *                              derives each zero-field checksum from the old field
  *                              (c = ~(~C - f) mod 2^16) and stores it (AUTO takes
  *                              it for fixed layouts with stride > len and images
- *                              above 4 KiB; fixed layouts need stride >= 64)
- *   TCPCK_PARAM_FILL_INSTREAM  with TCPCK_KERNEL_AUTO: the field zeroed in the
- *                              stream instead (the kernel AUTO picks for FILL) */
+ *                              above 4 KiB, and for packed variable layouts of
+ *                              448 B .. 32 KiB typical images; fixed layouts
+ *                              need stride >= 30)
+ *   TCPCK_PARAM_FILL_INSTREAM  with TCPCK_KERNEL_AUTO: the field zeroed and
+ *                              stored in the stream instead -- neither the
+ *                              update form nor the deferred-field forms (rstream
+ *                              25, vvstream + 64, sstream + 128)
+ * Under TCPCK_KERNEL_AUTO a FILL without a results buffer (d_out NULL, the
+ * reference's call shape) writes its results into the context's scratch
+ * (tcpck_ctx_create allocates 16 MiB: 8M images per launch chunk), so it
+ * takes the same forms as a FILL with one. */
 #define TCPCK_PARAM_FILL_UPDATE (1 << 28)
 #define TCPCK_PARAM_FILL_INSTREAM (1 << 29)
 /* RECEIVE into a header array (tcpck_batch_receive_ex): where the VERIFY kernel
  * is sstream it writes the headers itself (see TCPCK_KERNEL_SSTREAM); this bit
- * keeps the separate header pass instead. */
+ * keeps the separate header pass instead, under TCPCK_KERNEL_AUTO too. */
 #define TCPCK_PARAM_RECEIVE_TWO_PASS (1 << 30)
 int tcpck_batch_fixed_ex(tcpck_ctx *ctx, int op, int mode, void *d_arena,
                          uint64_t stride, uint32_t len, uint64_t count, void *d_out,

@@ -139,6 +139,7 @@ for s in ${STEPS:-tests smoke bench prof}; do
     wtprobe) step segwt 600 python scripts/segment_probe.py --params 0,64,128 --cases 1460:1504,1024:1056 &&
       step gswt 600 python scripts/gstream_probe.py --ops fill --lengths 32,64,128 --gs 0x401,0x801,0xC01 ;;
     rtests) step rtests 900 python -u -m pytest tests/test_gpu_receive.py tests/test_gpu_rfc_long.py -x -q --timeout 300 --timeout-method thread ;;
+    new4) step new4 900 python -u -m pytest tests/test_gpu_full_paths.py -x -v --timeout 300 --timeout-method thread ;;
     tests_new) step tests_new 900 python -u -m pytest tests/test_gpu_c5.py tests/test_gpu_multi_ctx.py tests/test_drop_in.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
     bench_receive) step bench_receive 600 python bench.py --config receive ;;
     bench_fill) step bench_fill 600 python bench.py --config fill ;;
@@ -146,9 +147,12 @@ for s in ${STEPS:-tests smoke bench prof}; do
     bench_segment) step bench_segment 600 python bench.py --config segment ;;
     prof_fill) step prof_fill 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_fill -o run --output-format csv -- python3 bench.py --config fill --steps 10 --warmup 2 --no-cpu-baseline --no-e2e ;;
     prof_receive) step prof_receive 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_receive -o run --output-format csv -- python3 bench.py --config receive --steps 10 --warmup 2 --no-cpu-baseline --no-e2e ;;
-    pmc_c2|pmc_c3|pmc_c4|pmc_c5|pmc_slots|pmc_segment|pmc_receive|pmc_fill)  # separate FETCH_SIZE / WRITE_SIZE passes (TCC slots), kernel trace only
+    pmc_c2|pmc_c3|pmc_c4|pmc_c5|pmc_slots|pmc_segment|pmc_receive|pmc_fill|pmc_fill_noout|pmc_fill_c3|pmc_c2_rfc)
+      # separate FETCH_SIZE / WRITE_SIZE passes (TCC slots), kernel trace only; the library's sha256 beside each
       c=${s#pmc_}
+      sha256sum tcp-stack_amd/libtcpck.so > gpurun_out/pmc_${c}_fetch_lib.sha256
       step ${s}_fetch 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d gpurun_out/pmc_${c}_fetch -o run --output-format csv -- python3 bench.py --config $c --steps 3 --warmup 1 --settle-ms 0 --no-cpu-baseline --no-e2e --no-extras
+      sha256sum tcp-stack_amd/libtcpck.so > gpurun_out/pmc_${c}_write_lib.sha256
       step ${s}_write 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d gpurun_out/pmc_${c}_write -o run --output-format csv -- python3 bench.py --config $c --steps 3 --warmup 1 --settle-ms 0 --no-cpu-baseline --no-e2e --no-extras ;;
   esac
 done

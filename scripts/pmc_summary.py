@@ -4,6 +4,10 @@ Input: gpurun_out/pmc_<cfg>_{fetch,write}/run_counter_collection.csv from
 `STEPS="pmc_c2 pmc_c3 pmc_c4" bash scripts/gpu_check.sh` (one counter per pass:
 FETCH_SIZE and WRITE_SIZE do not fit one pass of the 4 TCC slots).
 
+Each config's two passes must carry the same libtcpck.so sha256 (written by
+gpu_check.sh beside the CSVs); the entry is stamped with it and bench.py uses
+it only while that very library is the one loaded.
+
 Units and corrections (/opt/skills/guides/MI355X_MICROARCH.md, HBM section):
 both counters are in KiB; on gfx950 FETCH_SIZE reports half the bytes of a
 wide coalesced streaming read (16 B/lane), so it is doubled; WRITE_SIZE is
@@ -22,7 +26,8 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KERNELS = ("rstream_kernel", "vvstream_kernel", "seg_kernel", "jumbo_kernel", "sstream_kernel", "segment_kernel",
-           "header_swap_kernel", "patch_fields_kernel")
+           "header_swap_kernel", "header_extract_kernel", "patch_fields_kernel", "gstream_kernel")
+CONFIGS = ("c2", "c3", "c4", "c5", "slots", "segment", "receive", "fill", "fill_noout", "fill_c3", "c2_rfc")
 
 
 def per_launch(path: str, counter: str):
@@ -53,12 +58,21 @@ def main(rnd: str = "r01", *only: str) -> None:
             summary = json.load(f)
     except (OSError, ValueError):
         summary = {}
-    for cfg in ("c2", "c3", "c4", "c5", "slots", "segment", "receive", "fill"):
+    for cfg in CONFIGS:
         if only and cfg not in only:
             continue
         fp = os.path.join(src, f"pmc_{cfg}_fetch", "run_counter_collection.csv")
         wp = os.path.join(src, f"pmc_{cfg}_write", "run_counter_collection.csv")
         if not (os.path.exists(fp) and os.path.exists(wp)):
+            continue
+        # the library both passes ran (scripts/gpu_check.sh writes its sha256 beside them)
+        shas = set()
+        for ph in ("fetch", "write"):
+            sp = os.path.join(src, f"pmc_{cfg}_{ph}_lib.sha256")
+            if os.path.exists(sp):
+                shas.add(open(sp).read().split()[0])
+        if len(shas) != 1:
+            print(f"{cfg}: skipped, library stamps {sorted(shas) or 'missing'}")
             continue
         kname, fetch_kib, n = per_launch(fp, "FETCH_SIZE")
         _, write_kib, _ = per_launch(wp, "WRITE_SIZE")
@@ -74,6 +88,7 @@ def main(rnd: str = "r01", *only: str) -> None:
             "hbm_bytes_per_launch": int(read_b + write_b),
             "correction": "read = 2 x FETCH_SIZE KiB (gfx950 half-count on 16-B/lane streams); write = WRITE_SIZE KiB",
             "source": f"profiles/{rnd}/pmc_{cfg}_{{fetch,write}}.csv",
+            "lib_sha256": shas.pop(),
         }
         shutil.copy(fp, os.path.join(dst, f"pmc_{cfg}_fetch.csv"))
         shutil.copy(wp, os.path.join(dst, f"pmc_{cfg}_write.csv"))

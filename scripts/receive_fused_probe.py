@@ -6,7 +6,8 @@ with the stream read nt (variant 0) or with the default cache policy
 (variant 16, the header lines still in L2 when the run's end re-reads them),
 and (round 3) each header emitted from the stream's registers as the step is
 consumed (variant 32; 96: with write-through sc0 sc1 nt stores), and the
-header pass with write-through array stores (1 << 27, probe build).
+header pass with write-through array stores (tcpck_probe_receive_ex's
+PROBE_RECEIVE_HDR_WT, probe build).
 VERIFY alone for reference.  Results compared byte for byte.  Median of
 back-to-back rounds.  (Before round 3's fix the VERIFY-only closure took the
 lengths' min/max on the host per call: its small-ring lines, ~300 us, were
@@ -71,10 +72,13 @@ def case(ctx, s, name, n, slot, ln, fixed_len=None):
             ("fused keep", lambda: ctx.batch_receive(a, n, ok, hdr, kernel=S, param=16, **kw)),
             ("in-stream", lambda: ctx.batch_receive(a, n, ok, hdr, kernel=S, param=32, **kw)),
             ("in-str WT", lambda: ctx.batch_receive(a, n, ok, hdr, kernel=S, param=96, **kw)),
-            ("2 passes WT", lambda: ctx.batch_receive(a, n, ok, hdr, kernel=S, param=TWO | (1 << 27), **kw)),
+            ("2 passes WT", lambda: ctx.batch_receive(a, n, ok, hdr, kernel=S, param=TWO,
+                                                      probe_flags=tcpck.PROBE_RECEIVE_HDR_WT, **kw)),
             ("2 passes KH", lambda: ctx.batch_receive(a, n, ok, hdr, kernel=S, param=TWO | 16, **kw)),
-            ("concurrent", lambda: ctx.batch_receive(a, n, ok, hdr, kernel=S, param=1 << 26, **kw)),
-            ("concurrent A", lambda: ctx.batch_receive(a, n, ok, hdr, kernel=0, param=1 << 26, **kw)),
+            ("concurrent", lambda: ctx.batch_receive(a, n, ok, hdr, kernel=S, param=0,
+                                                     probe_flags=tcpck.PROBE_RECEIVE_CONCURRENT, **kw)),
+            ("concurrent A", lambda: ctx.batch_receive(a, n, ok, hdr, kernel=0, param=0,
+                                                       probe_flags=tcpck.PROBE_RECEIVE_CONCURRENT, **kw)),
             ("AUTO", lambda: ctx.batch_receive(a, n, ok, hdr, **kw))]
     res = {}
     for label, fn in runs:
@@ -122,8 +126,9 @@ def sweep(ctx, s, rng, n):
 def wide(ctx, s, rng, n):
     """--wide: the receive ring's header pass as the product form (8 lanes per
     image, u16 loads) against two lanes per image with one 16-B load each and
-    the load cache bits default / nt / sc0 sc1 / sc1 (param 1 << 25 | form <<
-    28, probe build); time per RECEIVE step and the results compared."""
+    the load cache bits default / nt / sc0 sc1 / sc1 (tcpck_probe_receive_ex:
+    PROBE_RECEIVE_HDR_WIDE | form << 4, probe build); time per RECEIVE step and
+    the results compared."""
     mix = (np.asarray((64, 576, 1460), np.uint32)[rng.integers(0, 3, n)] + 32).astype(np.uint32)
     img = int(mix.astype(np.int64).sum())
     S = tcpck.KERNEL_SSTREAM
@@ -137,10 +142,10 @@ def wide(ctx, s, rng, n):
     kw = dict(offsets=d_off, lengths=d_ln, total_bytes=img, min_len=int(mix.min()), max_len=int(mix.max()),
               sorted=True, stream=s)
     res = {}
-    for label, p in (("two passes", TWO), ("wide default", TWO | (1 << 25)), ("wide nt", TWO | (1 << 25) | (1 << 28)),
-                     ("wide sc0 sc1", TWO | (1 << 25) | (2 << 28)), ("wide sc1", TWO | (1 << 25) | (3 << 28)),
-                     ("header first", TWO | (1 << 24)), ("hdr first wide", TWO | (1 << 24) | (1 << 25))):
-        ms = b2b(lambda: ctx.batch_receive(a, n, ok, hdr, kernel=S, param=p, **kw), s)
+    W, F = tcpck.PROBE_RECEIVE_HDR_WIDE, tcpck.PROBE_RECEIVE_HDR_FIRST
+    for label, f in (("two passes", 0), ("wide default", W), ("wide nt", W | (1 << 4)), ("wide sc0 sc1", W | (2 << 4)),
+                     ("wide sc1", W | (3 << 4)), ("header first", F), ("hdr first wide", F | W)):
+        ms = b2b(lambda: ctx.batch_receive(a, n, ok, hdr, kernel=S, param=TWO, probe_flags=f, **kw), s)
         torch.cuda.synchronize()
         res[label] = (ok.clone(), hdr.clone())
         print(f"ring 1M x 2048 (bench mix)   {label:14s} {ms * 1e3:8.1f} us", flush=True)

@@ -22,55 +22,32 @@
 
 #include "tcpck.h"
 #include "tcpck_tuning.h"
-#include "tcpck_probe.h"
 #include "tcpck_internal.h"
+#include "tcpck_api_internal.h"
 
 using tcpck::SegArgs;
+using tcpck::api::DeviceGuard;
+using tcpck::api::Hooks;
+using tcpck::api::hip_status;
 
-struct tcpck_ctx {
-  int device = 0;
-  int num_cus = 256;
-
-  // end-to-end (host batch) pipeline state, created lazily
-  std::mutex mu;
-  hipStream_t s[2] = {nullptr, nullptr};
-  uint8_t *stage[2] = {nullptr, nullptr};     // image bytes
-  uint8_t *stage_out[2] = {nullptr, nullptr}; // results
-  uint64_t *stage_off[2] = {nullptr, nullptr};
-  uint32_t *stage_len[2] = {nullptr, nullptr};
-  uint64_t stage_bytes = 0;
-  uint64_t stage_images = 0;
-  uint64_t chunk_bytes = 64ull << 20;
-  void *dbg = nullptr;  // tuning: per-wave time stamp buffer (tcpck_ctx_set_debug)
-
-  // RECEIVE's header pass run beside the VERIFY pass (created on first use)
-  std::mutex side_mu;
-  hipStream_t side = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr;
-};
-
-namespace {
+namespace tcpck {
+namespace api {
 
 int hip_status(hipError_t e) { return e == hipSuccess ? TCPCK_OK : TCPCK_EHIP - static_cast<int>(e); }
 
-// Saves the calling thread's current device, switches to ctx->device, restores.
-class DeviceGuard {
- public:
-  explicit DeviceGuard(int device) {
-    if (hipGetDevice(&prev_) != hipSuccess) prev_ = -1;
-    if (prev_ != device) ok_ = hipSetDevice(device);
-  }
-  ~DeviceGuard() {
-    if (prev_ >= 0) (void)hipSetDevice(prev_);
-  }
-  hipError_t status() const { return ok_; }
-  DeviceGuard(const DeviceGuard &) = delete;
-  DeviceGuard &operator=(const DeviceGuard &) = delete;
+DeviceGuard::DeviceGuard(int device) {
+  if (hipGetDevice(&prev_) != hipSuccess) prev_ = -1;
+  if (prev_ != device) ok_ = hipSetDevice(device);
+}
 
- private:
-  int prev_ = -1;
-  hipError_t ok_ = hipSuccess;
-};
+DeviceGuard::~DeviceGuard() {
+  if (prev_ >= 0) (void)hipSetDevice(prev_);
+}
+
+}  // namespace api
+}  // namespace tcpck
+
+namespace {
 
 size_t out_elem(int op) { return op == TCPCK_OP_VERIFY ? 1 : 2; }
 
@@ -171,31 +148,12 @@ int ensure_stage(tcpck_ctx *ctx, uint64_t bytes, uint64_t images) {
   return TCPCK_OK;
 }
 
-// The side stream and the two events that let RECEIVE's header pass run
-// concurrently with its VERIFY pass.  Created once per context, on first use.
-#ifdef TCPCK_PROBE
-hipError_t ensure_side(tcpck_ctx *ctx) {
-  std::lock_guard<std::mutex> lk(ctx->side_mu);
-  if (ctx->side) return hipSuccess;
-  hipStream_t st = nullptr;
-  hipEvent_t e0 = nullptr, e1 = nullptr;
-  hipError_t e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&e0, hipEventDisableTiming);
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&e1, hipEventDisableTiming);
-  if (e != hipSuccess) {
-    if (e1) (void)hipEventDestroy(e1);
-    if (e0) (void)hipEventDestroy(e0);
-    if (st) (void)hipStreamDestroy(st);
-    return e;
-  }
-  ctx->fork = e0;
-  ctx->join = e1;
-  ctx->side = st;
-  return hipSuccess;
-}
-#endif
-
 void free_stage(tcpck_ctx *ctx) {
+  if (ctx->scratch_ev) {
+    (void)hipEventSynchronize(ctx->scratch_ev);
+    (void)hipEventDestroy(ctx->scratch_ev);
+  }
+  if (ctx->scratch) (void)hipFree(ctx->scratch);
   if (ctx->side) {
     (void)hipEventDestroy(ctx->fork);
     (void)hipEventDestroy(ctx->join);
@@ -274,27 +232,10 @@ constexpr int kSstreamDeferFill = 128;   // sstream: kFill writes the results on
 constexpr uint64_t kDeferFillMinVar = 1024;
 constexpr int kSstreamHdrStream = 32;    // sstream RECEIVE: headers from the stream's registers
 constexpr uint64_t kHdrStreamMaxLen = 256;  // ... for (typical) images up to this length
-constexpr int kProbeHdrWriteThrough = 1 << 27;  // probe builds: the header pass's array stores written through
-// probe builds: the header pass as two lanes per 16-B aligned image, one 16-B
-// buffer load each, cache bits (bits 28-29: 0 default, 1 nt, 2 sc0 sc1, 3 sc1)
-constexpr int kProbeHdrWide = 1 << 25;
-#ifdef TCPCK_PROBE
-// probe builds, RECEIVE with TCPCK_PARAM_RECEIVE_TWO_PASS: the header pass
-// first, its lines left in the caches for the VERIFY stream that follows
-constexpr int kProbeHdrFirst = 1 << 24;
-#endif
-#ifdef TCPCK_PROBE
-constexpr int kReceiveConcurrent = 1 << 26;  // probe builds: the header pass beside VERIFY on a side stream
-#endif
-// RECEIVE with an explicit kernel: the probe build fuses the headers into any
-// kernel that can (sstream's after-the-run conversion, HDR 1); the product
-// carries only the stream-register form (+ kSstreamHdrStream) and otherwise
-// runs the header pass
-#ifdef TCPCK_PROBE
-constexpr bool kFuseAnyHdr = true;
-#else
-constexpr bool kFuseAnyHdr = false;
-#endif
+// RECEIVE: with an explicit kernel the product carries only the
+// stream-register form (+ kSstreamHdrStream) and otherwise runs the header
+// pass; the probe library can fuse the headers into any kernel that can
+// (Hooks::fuse_any_hdr: sstream's after-the-verdicts conversion, HDR 1)
 
 // Packed fixed images above 4 KiB: seg's W-wave shapes stream W KiB of an
 // image per step (shape_for_len: W = 2, 4, 8, 16 up to 8, 16, 32, 64 KiB), so
@@ -312,11 +253,20 @@ static bool jumbo_on_seg(int op, uint64_t len) {
   return op == TCPCK_OP_FILL ? fits && len > 24576 : fits;
 }
 
+// The caller's TCPCK_PARAM_* bits, read before AUTO's choice rewrites param.
+struct CallerBits {
+  bool two_pass;   // RECEIVE: keep the separate header pass
+  bool instream;   // FILL under AUTO: the field zeroed in the stream, no deferred field pass
+  explicit CallerBits(int param)
+      : two_pass((param & TCPCK_PARAM_RECEIVE_TWO_PASS) != 0), instream((param & TCPCK_PARAM_FILL_INSTREAM) != 0) {}
+};
+
 hipError_t run_fixed_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t stride, uint32_t len,
                           uint64_t count, void *out, int kernel, int param, hipStream_t s, bool *patch,
-                          uint8_t *hdr = nullptr, bool *hdr_done = nullptr) {
+                          const Hooks &hk, uint8_t *hdr = nullptr, bool *hdr_done = nullptr) {
   const uint32_t num_cus = static_cast<uint32_t>(ctx->num_cus);
   const bool auto_pick = kernel == TCPCK_KERNEL_AUTO;
+  const CallerBits caller(param);
   if (kernel == TCPCK_KERNEL_AUTO && mode == TCPCK_MODE_RFC1071 && stride == len && len >= 512 &&
       len <= kFixedRunMaxLen) {
     // RFC 1071 on packed fixed images: rstream's prefix is an exact u32 word
@@ -416,10 +366,12 @@ hipError_t run_fixed_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint
   // measured faster than any fused form for MSS-sized images (header stores
   // inside the read stream cost more than a separate pass: DESIGN.md "Receive
   // path", profiles/r03/receive_fused_probe.log)
-  if (auto_pick && op == TCPCK_OP_RECEIVE && hdr && kernel == TCPCK_KERNEL_SSTREAM && len <= kHdrStreamMaxLen)
+  // (TCPCK_PARAM_RECEIVE_TWO_PASS keeps the separate pass, AUTO included)
+  if (auto_pick && op == TCPCK_OP_RECEIVE && hdr && kernel == TCPCK_KERNEL_SSTREAM && len <= kHdrStreamMaxLen &&
+      !caller.two_pass)
     param |= kSstreamHdrStream;
-  const bool fuse_hdr = op == TCPCK_OP_RECEIVE && hdr && ((kFuseAnyHdr && !auto_pick) || (param & kSstreamHdrStream)) &&
-                        !(param & TCPCK_PARAM_RECEIVE_TWO_PASS);
+  const bool fuse_hdr = op == TCPCK_OP_RECEIVE && hdr && !caller.two_pass &&
+                        ((hk.fuse_any_hdr && !auto_pick) || (param & kSstreamHdrStream));
   if (op == TCPCK_OP_RECEIVE) op = TCPCK_OP_VERIFY;  // the header pass follows (run_fixed)
   // FILL on rstream with a results buffer: the stream writes only the results,
   // then a second pass stores each field with a write-through 2-B store.
@@ -427,7 +379,8 @@ hipError_t run_fixed_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint
   // Infinity Cache for the next stream to write back, cost ~70 us per 1M
   // images; written through to HBM in their own pass they cost 38 us (C2:
   // 280 -> 248 us, scripts/fill_drain_probe.py, profiles/r03/fill_*.log)
-  if (auto_pick && kernel == TCPCK_KERNEL_RSTREAM && op == TCPCK_OP_FILL && out && stride >= 30 &&
+  // (TCPCK_PARAM_FILL_INSTREAM keeps the in-stream form)
+  if (auto_pick && !caller.instream && kernel == TCPCK_KERNEL_RSTREAM && op == TCPCK_OP_FILL && out && stride >= 30 &&
       (param & 0xFF) == kRstreamPolicy)
     param = (param & ~0xFF) | kRstreamDeferFill;
   if (kernel == TCPCK_KERNEL_RSTREAM) {
@@ -439,7 +392,7 @@ hipError_t run_fixed_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint
     a.count = count;
     a.order = 0xFFu;  // default block order (variants 14-19 choose an XCD order)
     a.out = out;
-    a.dbg = static_cast<uint64_t *>(ctx->dbg);
+    a.dbg = static_cast<uint64_t *>(ctx->dbg);  // set by the probe library only
     a.blocks_per_cu = static_cast<uint32_t>(param >> 8) & 0xFFu;
     a.oversub = static_cast<uint32_t>(param >> 16) & 0xFFu;
     int variant = param & 0xFF;
@@ -462,7 +415,8 @@ hipError_t run_fixed_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint
     return tcpck::launch_gstream(op, param & 0xFFFF, a, num_cus, s);
   }
   if (kernel == TCPCK_KERNEL_SSTREAM) {  // fixed slots: stride % 16 == 0, stride >= len
-    if (auto_pick && op == TCPCK_OP_FILL && out && len >= kDeferFillMinLen) param |= kSstreamDeferFill;
+    if (auto_pick && !caller.instream && op == TCPCK_OP_FILL && out && len >= kDeferFillMinLen)
+      param |= kSstreamDeferFill;
     if (param & kSstreamDeferFill) *patch = true;
     if (count == 1) stride = (static_cast<uint64_t>(len) + 15) & ~uint64_t{15};  // one image: never read
     if (!tcpck::sstream_fixed_applies(stride, len) || (op == TCPCK_OP_FILL && len < 30) ||
@@ -484,7 +438,7 @@ hipError_t run_fixed_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint
   }
   if (kernel == TCPCK_KERNEL_VVSTREAM) {  // any even length: the prefix table takes any number of ends per step
     if (len == 0 || stride > (1u << 24) || (op == TCPCK_OP_FILL && len < 30)) return hipErrorInvalidValue;
-    if (auto_pick && op == TCPCK_OP_FILL && out && len >= kDeferFillMinLen) param |= kVvDeferFill;
+    if (auto_pick && !caller.instream && op == TCPCK_OP_FILL && out && len >= kDeferFillMinLen) param |= kVvDeferFill;
     if (param & kVvDeferFill) *patch = true;
     if (mode != TCPCK_MODE_REF && (len >= (1u << 17) || (param & 32))) return hipErrorInvalidValue;
     tcpck::RunArgs a{};
@@ -539,26 +493,13 @@ bool fill_by_update(int op, int mode, const void *out, int kernel, int param, bo
   return layout && (layout->flags & TCPCK_LAYOUT_PACKED) && typical >= kFillUpdateMinVar && typical <= kRunMaxLen;
 }
 
-hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t stride, uint32_t len,
-                     uint64_t count, void *out, int kernel, int param, hipStream_t s, uint8_t *hdr = nullptr) {
+hipError_t run_fixed_r(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t stride, uint32_t len,
+                       uint64_t count, void *out, int kernel, int param, hipStream_t s, uint8_t *hdr, const Hooks &hk) {
   bool patch = false;
-#ifdef TCPCK_PROBE
-  if (kernel == TCPCK_KERNEL_PATCH) {  // the deferred field pass alone (timing)
-    if (op != TCPCK_OP_FILL || !out || stride < 30) return hipErrorInvalidValue;
-    tcpck::PatchArgs pa{};
-    pa.arena = arena;
-    pa.stride = stride;
-    pa.count = count;
-    pa.sums = static_cast<uint16_t *>(out);
-    pa.hi = (count - 1) * stride + len;
-    pa.store_bits = static_cast<uint32_t>(param & 0xFF);  // 1 + sc0 1 | nt 2 | sc1 4 (0 = plain) | form << 4
-    return tcpck::launch_patch_fields(pa, static_cast<uint32_t>(ctx->num_cus), s);
-  }
-#endif
   if (stride >= 30 && fill_by_update(op, mode, out, kernel, param, true, stride, len)) {
     const int p = param & ~(TCPCK_PARAM_FILL_UPDATE | TCPCK_PARAM_FILL_INSTREAM);
     const hipError_t e = run_fixed_impl(ctx, TCPCK_OP_CHECKSUM, mode, arena, stride, len, count, out, kernel, p, s,
-                                        &patch);
+                                        &patch, hk);
     if (e != hipSuccess) return e;
     tcpck::PatchArgs pa{};
     pa.arena = arena;
@@ -570,11 +511,9 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
     pa.update = 1;
     return tcpck::launch_patch_fields(pa, static_cast<uint32_t>(ctx->num_cus), s);
   }
-  const uint32_t hdr_bits = (param & kProbeHdrWide) ? 2u | ((static_cast<uint32_t>(param) >> 28 & 3u) << 4) : 0u;
-  param &= ~(TCPCK_PARAM_FILL_UPDATE | TCPCK_PARAM_FILL_INSTREAM);
   bool hdr_done = false;
   const hipError_t e =
-      run_fixed_impl(ctx, op, mode, arena, stride, len, count, out, kernel, param, s, &patch, hdr, &hdr_done);
+      run_fixed_impl(ctx, op, mode, arena, stride, len, count, out, kernel, param, s, &patch, hk, hdr, &hdr_done);
   if (e != hipSuccess) return e;
   if (patch) {
     tcpck::PatchArgs p{};
@@ -592,18 +531,19 @@ hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t 
   h.stride = stride;
   h.count = count;
   h.out = hdr;
-  h.store_bits = ((param & kProbeHdrWriteThrough) ? 1u : 0u) |
-                 hdr_bits;
+  h.store_bits = hk.hdr_store_bits;
   return tcpck::launch_header_swap(h, static_cast<uint32_t>(ctx->num_cus), s);
 }
 
 hipError_t run_var_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const uint64_t *off, const uint32_t *len,
                         uint64_t base, uint64_t count, void *out, const tcpck_layout *layout, int kernel, int param,
-                        hipStream_t s, uint8_t *hdr = nullptr, bool *hdr_done = nullptr, bool *patch = nullptr) {
+                        hipStream_t s, const Hooks &hk, uint8_t *hdr = nullptr, bool *hdr_done = nullptr,
+                        bool *patch = nullptr) {
   const uint64_t typical = (layout && layout->total_bytes) ? layout->total_bytes / count : 1500;
   const bool packed = mode == TCPCK_MODE_REF && layout && (layout->flags & TCPCK_LAYOUT_PACKED);
   bool fuse_small = false;  // RECEIVE into a header array on a ring of small datagrams (below)
   const bool auto_pick = kernel == TCPCK_KERNEL_AUTO;
+  const CallerBits caller(param);
   // packed, reference mode: vvstream for every op (any image lengths; C3 89.1%
   // at 32x oversubscription, profiles/r01/c3_bench_r01_final.log).  The
   // packed flag must be true when set (tcpck.h); a wave whose lengths do not
@@ -633,7 +573,7 @@ hipError_t run_var_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const 
       // (41-58 % either way: the scattered field writes bound it)
       kernel = TCPCK_KERNEL_SSTREAM;
       param = 0;
-      if (op == TCPCK_OP_RECEIVE && hdr && typical <= kHdrStreamMaxLen) {
+      if (op == TCPCK_OP_RECEIVE && hdr && typical <= kHdrStreamMaxLen && !caller.two_pass) {
         fuse_small = true;
         param = kSstreamHdrStream;
       }
@@ -650,13 +590,14 @@ hipError_t run_var_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const 
   // sstream emits the headers from its stream (4M 32-254-B datagrams in 256-B
   // slots: 190 us against 259 with the header pass, 235 with the run's
   // headers re-read after its verdicts); otherwise the header pass follows
-  bool fuse_hdr = op == TCPCK_OP_RECEIVE && hdr && !(param & TCPCK_PARAM_RECEIVE_TWO_PASS) &&
-                  ((kFuseAnyHdr && !auto_pick) || fuse_small || (param & kSstreamHdrStream));
+  bool fuse_hdr = op == TCPCK_OP_RECEIVE && hdr && !caller.two_pass &&
+                  ((hk.fuse_any_hdr && !auto_pick) || fuse_small || (param & kSstreamHdrStream));
   if (op == TCPCK_OP_RECEIVE) op = TCPCK_OP_VERIFY;  // the header pass follows (run_var)
   if (kernel == TCPCK_KERNEL_VVSTREAM) {
     if (mode != TCPCK_MODE_REF && (param & 32)) return hipErrorInvalidValue;
     // (REF packed batches of typical >= 448 B take the update form in run_var)
-    if (auto_pick && op == TCPCK_OP_FILL && out && patch && typical >= kDeferFillMinVar) param |= kVvDeferFill;
+    if (auto_pick && !caller.instream && op == TCPCK_OP_FILL && out && patch && typical >= kDeferFillMinVar)
+      param |= kVvDeferFill;
     if (param & kVvDeferFill) {
       if (!patch) return hipErrorInvalidValue;
       *patch = true;
@@ -709,14 +650,14 @@ hipError_t run_var_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const 
   return tcpck::launch_seg(op, mode, false, shape, a, static_cast<uint32_t>(ctx->num_cus), s);
 }
 
-hipError_t run_var(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const uint64_t *off, const uint32_t *len,
-                   uint64_t base, uint64_t count, void *out, const tcpck_layout *layout, int kernel, int param,
-                   hipStream_t s, uint8_t *hdr = nullptr) {
+hipError_t run_var_r(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const uint64_t *off, const uint32_t *len,
+                     uint64_t base, uint64_t count, void *out, const tcpck_layout *layout, int kernel, int param,
+                     hipStream_t s, uint8_t *hdr, const Hooks &hk) {
   if (op == TCPCK_OP_RECEIVE && base != 0) return hipErrorInvalidValue;  // device batches only
   if (fill_by_update(op, mode, out, kernel, param, false, 0, 0, layout, count)) {
     const int p = param & ~(TCPCK_PARAM_FILL_UPDATE | TCPCK_PARAM_FILL_INSTREAM);
     const hipError_t e =
-        run_var_impl(ctx, TCPCK_OP_CHECKSUM, mode, arena, off, len, base, count, out, layout, kernel, p, s);
+        run_var_impl(ctx, TCPCK_OP_CHECKSUM, mode, arena, off, len, base, count, out, layout, kernel, p, s, hk);
     if (e != hipSuccess) return e;
     tcpck::PatchArgs pa{};
     pa.arena = arena;
@@ -729,25 +670,21 @@ hipError_t run_var(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const uint6
     pa.packed = (layout && (layout->flags & TCPCK_LAYOUT_PACKED)) ? 1u : 0u;
     return tcpck::launch_patch_fields(pa, static_cast<uint32_t>(ctx->num_cus), s);
   }
-  const uint32_t hdr_bits = (param & kProbeHdrWide) ? 2u | ((static_cast<uint32_t>(param) >> 28 & 3u) << 4) : 0u;
-  param &= ~(TCPCK_PARAM_FILL_UPDATE | TCPCK_PARAM_FILL_INSTREAM);
-#ifdef TCPCK_PROBE
-  if (op == TCPCK_OP_RECEIVE && hdr && (param & kProbeHdrFirst) && (param & TCPCK_PARAM_RECEIVE_TWO_PASS)) {
-    tcpck::HeaderArgs h{};
-    h.arena = arena;
-    h.offsets = off;
-    h.count = count;
-    h.out = hdr;
-    h.store_bits = hdr_bits;
+  tcpck::HeaderArgs h{};
+  h.arena = arena;
+  h.offsets = off;
+  h.count = count;
+  h.out = hdr;
+  h.store_bits = hk.hdr_store_bits;
+  if (op == TCPCK_OP_RECEIVE && hdr && hk.hdr_first && (param & TCPCK_PARAM_RECEIVE_TWO_PASS)) {
     const hipError_t eh = tcpck::launch_header_swap(h, static_cast<uint32_t>(ctx->num_cus), s);
     if (eh != hipSuccess) return eh;
     return run_var_impl(ctx, TCPCK_OP_VERIFY, mode, arena, off, len, base, count, out, layout, kernel,
-                        param & ~(kProbeHdrFirst | TCPCK_PARAM_RECEIVE_TWO_PASS), s);
+                        param & ~TCPCK_PARAM_RECEIVE_TWO_PASS, s, hk);
   }
-#endif
   bool hdr_done = false, patch = false;
-  const hipError_t e =
-      run_var_impl(ctx, op, mode, arena, off, len, base, count, out, layout, kernel, param, s, hdr, &hdr_done, &patch);
+  const hipError_t e = run_var_impl(ctx, op, mode, arena, off, len, base, count, out, layout, kernel, param, s, hk,
+                                    hdr, &hdr_done, &patch);
   if (e != hipSuccess) return e;
   if (patch) {  // the fields the stream left: write-through 2-B stores (launch_patch_fields)
     tcpck::PatchArgs pa{};
@@ -760,13 +697,6 @@ hipError_t run_var(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const uint6
     return tcpck::launch_patch_fields(pa, static_cast<uint32_t>(ctx->num_cus), s);
   }
   if (op != TCPCK_OP_RECEIVE || hdr_done) return e;
-  tcpck::HeaderArgs h{};
-  h.arena = arena;
-  h.offsets = off;
-  h.count = count;
-  h.out = hdr;
-  h.store_bits = ((param & kProbeHdrWriteThrough) ? 1u : 0u) |
-                 hdr_bits;
   return tcpck::launch_header_swap(h, static_cast<uint32_t>(ctx->num_cus), s);
 }
 
@@ -782,6 +712,142 @@ void patch_fields(uint8_t *arena, uint64_t k0, uint64_t n, const uint16_t *res,
 }
 
 }  // namespace
+
+// ---- the router's entry points (tcpck_api_internal.h) -------------------------
+namespace tcpck {
+namespace api {
+
+hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t stride, uint32_t len, uint64_t count,
+                     void *out, int kernel, int param, hipStream_t s, uint8_t *hdr, const Hooks &hk) {
+  return run_fixed_r(ctx, op, mode, arena, stride, len, count, out, kernel, param, s, hdr, hk);
+}
+
+hipError_t run_var(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const uint64_t *off, const uint32_t *len,
+                   uint64_t base, uint64_t count, void *out, const tcpck_layout *layout, int kernel, int param,
+                   hipStream_t s, uint8_t *hdr, const Hooks &hk) {
+  return run_var_r(ctx, op, mode, arena, off, len, base, count, out, layout, kernel, param, s, hdr, hk);
+}
+
+namespace {
+
+// FILL without a results buffer under AUTO (the reference's call shape,
+// socket-manager.cc:9-10): the results go to the ctx scratch so AUTO keeps
+// the forms that need them (rstream's deferred fields, vvstream's update pass:
+// C2 in-stream 69.3 % -> 76-77 %, C3 53.7 -> 62 %, profiles/r03/fill_forms.log).
+bool use_scratch(const tcpck_ctx *ctx, int op, const void *out, int kernel) {
+  return op == TCPCK_OP_FILL && !out && kernel == TCPCK_KERNEL_AUTO && ctx->scratch;
+}
+
+// launch(k0, n, results) for images [k0, k0 + n), n <= scratch_images.  Calls
+// are serialised per ctx; a stream other than the scratch's last user first
+// waits for that user's work (the event recorded after every use).
+template <typename Launch>
+hipError_t with_scratch(tcpck_ctx *ctx, uint64_t count, hipStream_t s, Launch launch) {
+  std::lock_guard<std::mutex> lk(ctx->scratch_mu);
+  hipError_t e = hipSuccess;
+  if (ctx->scratch_used && ctx->scratch_last != s) e = hipStreamWaitEvent(s, ctx->scratch_ev, 0);
+  for (uint64_t k0 = 0; k0 < count && e == hipSuccess; k0 += ctx->scratch_images)
+    e = launch(k0, std::min(ctx->scratch_images, count - k0), ctx->scratch);
+  const hipError_t er = hipEventRecord(ctx->scratch_ev, s);
+  if (er == hipSuccess) {
+    ctx->scratch_used = true;
+    ctx->scratch_last = s;
+  }
+  return e != hipSuccess ? e : er;
+}
+
+}  // namespace
+
+int batch_fixed_ex(tcpck_ctx *ctx, int op, int mode, void *d_arena, uint64_t stride, uint32_t len, uint64_t count,
+                   void *d_out, int kernel, int param, hipStream_t s, const Hooks &hk) {
+  if (!ctx || !valid_device_op_mode(op, mode)) return TCPCK_EINVAL;
+  if (count == 0) return TCPCK_OK;
+  // images start at even addresses: the kernels pair bytes into u16 words by address
+  if (!d_arena || (reinterpret_cast<uintptr_t>(d_arena) & 1) || (len & 1) || (stride & 1) ||
+      (count > 1 && stride < len))
+    return TCPCK_EINVAL;
+  if (!d_out && op != TCPCK_OP_FILL) return TCPCK_EINVAL;
+  if (op == TCPCK_OP_FILL && len < 30) return TCPCK_EINVAL;
+  if (op == TCPCK_OP_RECEIVE && len < TCPCK_HEADER_BYTES) return TCPCK_EINVAL;
+  if (count > 1 && stride > (UINT64_MAX - len) / (count - 1)) return TCPCK_EINVAL;
+  if (count == 1) stride = len;  // one image: its stride is never read; the run kernels assume stride >= len
+  DeviceGuard g(ctx->device);
+  if (g.status() != hipSuccess) return hip_status(g.status());
+  auto *arena = static_cast<uint8_t *>(d_arena);
+  if (use_scratch(ctx, op, d_out, kernel))
+    return hip_status(with_scratch(ctx, count, s, [&](uint64_t k0, uint64_t n, uint16_t *res) {
+      return run_fixed(ctx, op, mode, arena + k0 * stride, n == 1 ? len : stride, len, n, res, kernel, param, s,
+                       nullptr, hk);
+    }));
+  return hip_status(run_fixed(ctx, op, mode, arena, stride, len, count, d_out, kernel, param, s, nullptr, hk));
+}
+
+int batch_var_ex(tcpck_ctx *ctx, int op, int mode, void *d_arena, const uint64_t *d_offsets,
+                 const uint32_t *d_lengths, uint64_t count, void *d_out, const tcpck_layout *layout, int kernel,
+                 int param, hipStream_t s, const Hooks &hk) {
+  if (!ctx || !valid_device_op_mode(op, mode)) return TCPCK_EINVAL;
+  if (count == 0) return TCPCK_OK;
+  if (!d_arena || !d_offsets || !d_lengths || (reinterpret_cast<uintptr_t>(d_arena) & 1)) return TCPCK_EINVAL;
+  if (!d_out && op != TCPCK_OP_FILL) return TCPCK_EINVAL;
+  DeviceGuard g(ctx->device);
+  if (g.status() != hipSuccess) return hip_status(g.status());
+  auto *arena = static_cast<uint8_t *>(d_arena);
+  if (use_scratch(ctx, op, d_out, kernel))
+    return hip_status(with_scratch(ctx, count, s, [&](uint64_t k0, uint64_t n, uint16_t *res) {
+      tcpck_layout sub{};
+      if (layout) {
+        sub = *layout;  // a sub-range keeps the flags and the length bounds; the byte hint scales
+        sub.total_bytes = static_cast<uint64_t>(static_cast<unsigned __int128>(layout->total_bytes) * n / count);
+      }
+      return run_var(ctx, op, mode, arena, d_offsets + k0, d_lengths + k0, 0, n, res, layout ? &sub : nullptr, kernel,
+                     param, s, nullptr, hk);
+    }));
+  return hip_status(run_var(ctx, op, mode, arena, d_offsets, d_lengths, 0, count, d_out, layout, kernel, param, s,
+                            nullptr, hk));
+}
+
+int check_receive(const tcpck_ctx *ctx, int mode, const void *d_arena, uint64_t &stride, uint32_t len,
+                  const uint64_t *d_offsets, const uint32_t *d_lengths, uint64_t count, const uint8_t *d_ok,
+                  const void *d_hdr) {
+  if (!ctx || !valid_device_op_mode(TCPCK_OP_VERIFY, mode)) return TCPCK_EINVAL;
+  if (count == 0) return TCPCK_OK;
+  if (!d_arena || !d_ok || (reinterpret_cast<uintptr_t>(d_arena) & 1) || (reinterpret_cast<uintptr_t>(d_hdr) & 3))
+    return TCPCK_EINVAL;
+  if (count > (UINT64_MAX >> 6)) return TCPCK_EINVAL;
+  if (!d_offsets) {
+    if ((len & 1) || (stride & 1) || len < TCPCK_HEADER_BYTES || (count > 1 && stride < len)) return TCPCK_EINVAL;
+    if (count > 1 && stride > (UINT64_MAX - len) / (count - 1)) return TCPCK_EINVAL;
+    if (count == 1) stride = len;
+  } else if (!d_lengths) {
+    return TCPCK_EINVAL;
+  }
+  return TCPCK_OK;
+}
+
+int batch_receive_ex(tcpck_ctx *ctx, int mode, void *d_arena, uint64_t stride, uint32_t len,
+                     const uint64_t *d_offsets, const uint32_t *d_lengths, uint64_t count, uint8_t *d_ok,
+                     void *d_hdr, const tcpck_layout *layout, int kernel, int param, hipStream_t s,
+                     const Hooks &hk) {
+  if (!d_hdr) {  // TCPCK_OP_RECEIVE: the headers converted in place
+    return d_offsets ? batch_var_ex(ctx, TCPCK_OP_RECEIVE, mode, d_arena, d_offsets, d_lengths, count, d_ok, layout,
+                                    kernel, param, s, hk)
+                     : batch_fixed_ex(ctx, TCPCK_OP_RECEIVE, mode, d_arena, stride, len, count, d_ok, kernel, param,
+                                      s, hk);
+  }
+  const int rc = check_receive(ctx, mode, d_arena, stride, len, d_offsets, d_lengths, count, d_ok, d_hdr);
+  if (rc != TCPCK_OK || count == 0) return rc;
+  DeviceGuard g(ctx->device);
+  if (g.status() != hipSuccess) return hip_status(g.status());
+  auto *arena = static_cast<uint8_t *>(d_arena);
+  auto *hdr = static_cast<uint8_t *>(d_hdr);
+  return hip_status(d_offsets ? run_var(ctx, TCPCK_OP_RECEIVE, mode, arena, d_offsets, d_lengths, 0, count, d_ok,
+                                        layout, kernel, param, s, hdr, hk)
+                              : run_fixed(ctx, TCPCK_OP_RECEIVE, mode, arena, stride, len, count, d_ok, kernel,
+                                          param, s, hdr, hk));
+}
+
+}  // namespace api
+}  // namespace tcpck
 
 // helpers of tcpck_host_batch_*_multi
 namespace {
@@ -862,6 +928,22 @@ int tcpck_ctx_create(int device, tcpck_ctx **out) {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
     ctx->num_cus = prop.multiProcessorCount;
+  {
+    // the results scratch of FILL without a results buffer (tcpck_api_internal.h)
+    DeviceGuard g(device);
+    void *p = nullptr;
+    hipEvent_t ev = nullptr;
+    if (g.status() != hipSuccess || hipMalloc(&p, tcpck::api::kScratchImages * 2) != hipSuccess ||
+        hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+      if (p) (void)hipFree(p);
+      (void)hipGetLastError();
+      delete ctx;
+      return TCPCK_ENOMEM;
+    }
+    ctx->scratch = static_cast<uint16_t *>(p);
+    ctx->scratch_images = tcpck::api::kScratchImages;
+    ctx->scratch_ev = ev;
+  }
   *out = ctx;
   return TCPCK_OK;
 }
@@ -927,66 +1009,19 @@ uint16_t tcpck_update16(uint16_t checksum, uint16_t old_word, uint16_t new_word,
 // ---- batched, device-resident -------------------------------------------------
 int tcpck_batch_fixed(tcpck_ctx *ctx, int op, int mode, void *d_arena, uint64_t stride,
                       uint32_t len, uint64_t count, void *d_out, tcpck_stream stream) {
-  return tcpck_batch_fixed_ex(ctx, op, mode, d_arena, stride, len, count, d_out, TCPCK_KERNEL_AUTO, 0,
-                              stream);
+  return tcpck::api::batch_fixed_ex(ctx, op, mode, d_arena, stride, len, count, d_out, TCPCK_KERNEL_AUTO, 0,
+                                    static_cast<hipStream_t>(stream), Hooks{});
 }
 
 int tcpck_batch_var(tcpck_ctx *ctx, int op, int mode, void *d_arena, const uint64_t *d_offsets,
                     const uint32_t *d_lengths, uint64_t count, void *d_out,
                     const tcpck_layout *layout, tcpck_stream stream) {
-  return tcpck_batch_var_ex(ctx, op, mode, d_arena, d_offsets, d_lengths, count, d_out, layout,
-                            TCPCK_KERNEL_AUTO, 0, stream);
+  return tcpck::api::batch_var_ex(ctx, op, mode, d_arena, d_offsets, d_lengths, count, d_out, layout,
+                                  TCPCK_KERNEL_AUTO, 0, static_cast<hipStream_t>(stream), Hooks{});
 }
 
-#ifdef TCPCK_PROBE
-// measurement-only entry points (libtcpck_probe.so; include/tcpck_tuning.h)
-int tcpck_diag_stream(tcpck_ctx *ctx, int variant, const void *d_buf, uint64_t bytes, void *d_out,
-                      tcpck_stream stream) {
-  if (!ctx || !d_buf || !d_out || bytes < 4096) return TCPCK_EINVAL;
-  DeviceGuard g(ctx->device);
-  return hip_status(tcpck::launch_diag_stream(variant, static_cast<const uint8_t *>(d_buf), bytes,
-                                              static_cast<uint32_t *>(d_out), static_cast<uint32_t>(ctx->num_cus),
-                                              static_cast<hipStream_t>(stream)));
-}
-
-int tcpck_ctx_set_debug(tcpck_ctx *ctx, void *d_buf) {
-  if (!ctx) return TCPCK_EINVAL;
-  ctx->dbg = d_buf;
-  return TCPCK_OK;
-}
-#endif  // TCPCK_PROBE
-
-int tcpck_batch_fixed_ex(tcpck_ctx *ctx, int op, int mode, void *d_arena, uint64_t stride, uint32_t len,
-                         uint64_t count, void *d_out, int kernel, int param, tcpck_stream stream) {
-  if (!ctx || !valid_device_op_mode(op, mode)) return TCPCK_EINVAL;
-  if (count == 0) return TCPCK_OK;
-  // images start at even addresses: the kernels pair bytes into u16 words by address
-  if (!d_arena || (reinterpret_cast<uintptr_t>(d_arena) & 1) || (len & 1) || (stride & 1) ||
-      (count > 1 && stride < len))
-    return TCPCK_EINVAL;
-  if (!d_out && op != TCPCK_OP_FILL) return TCPCK_EINVAL;
-  if (op == TCPCK_OP_FILL && len < 30) return TCPCK_EINVAL;
-  if (op == TCPCK_OP_RECEIVE && len < TCPCK_HEADER_BYTES) return TCPCK_EINVAL;
-  if (count > 1 && stride > (UINT64_MAX - len) / (count - 1)) return TCPCK_EINVAL;
-  if (count == 1) stride = len;  // one image: its stride is never read; the run kernels assume stride >= len
-  DeviceGuard g(ctx->device);
-  if (g.status() != hipSuccess) return hip_status(g.status());
-  return hip_status(run_fixed(ctx, op, mode, static_cast<uint8_t *>(d_arena), stride, len, count, d_out,
-                              kernel, param, static_cast<hipStream_t>(stream)));
-}
-
-int tcpck_batch_var_ex(tcpck_ctx *ctx, int op, int mode, void *d_arena, const uint64_t *d_offsets,
-                       const uint32_t *d_lengths, uint64_t count, void *d_out, const tcpck_layout *layout,
-                       int kernel, int param, tcpck_stream stream) {
-  if (!ctx || !valid_device_op_mode(op, mode)) return TCPCK_EINVAL;
-  if (count == 0) return TCPCK_OK;
-  if (!d_arena || !d_offsets || !d_lengths || (reinterpret_cast<uintptr_t>(d_arena) & 1)) return TCPCK_EINVAL;
-  if (!d_out && op != TCPCK_OP_FILL) return TCPCK_EINVAL;
-  DeviceGuard g(ctx->device);
-  if (g.status() != hipSuccess) return hip_status(g.status());
-  return hip_status(run_var(ctx, op, mode, static_cast<uint8_t *>(d_arena), d_offsets, d_lengths, 0, count,
-                            d_out, layout, kernel, param, static_cast<hipStream_t>(stream)));
-}
+// (tcpck_batch_fixed_ex / tcpck_batch_var_ex / tcpck_batch_receive_ex, the
+// tuning entry points: tcpck_ex.hip, and tcpck_ex_probe.hip in the probe library)
 
 // ---- batched retransmit: ACK rewrite + incremental update ----------------------
 int tcpck_batch_set_ack(tcpck_ctx *ctx, int mode, void *d_arena, const uint64_t *d_offsets, uint64_t stride,
@@ -1017,67 +1052,8 @@ int tcpck_batch_set_ack(tcpck_ctx *ctx, int mode, void *d_arena, const uint64_t 
 int tcpck_batch_receive(tcpck_ctx *ctx, int mode, void *d_arena, uint64_t stride, uint32_t len,
                         const uint64_t *d_offsets, const uint32_t *d_lengths, uint64_t count, uint8_t *d_ok,
                         void *d_hdr, const tcpck_layout *layout, tcpck_stream stream) {
-  return tcpck_batch_receive_ex(ctx, mode, d_arena, stride, len, d_offsets, d_lengths, count, d_ok, d_hdr, layout,
-                                TCPCK_KERNEL_AUTO, 0, stream);
-}
-
-int tcpck_batch_receive_ex(tcpck_ctx *ctx, int mode, void *d_arena, uint64_t stride, uint32_t len,
-                           const uint64_t *d_offsets, const uint32_t *d_lengths, uint64_t count, uint8_t *d_ok,
-                           void *d_hdr, const tcpck_layout *layout, int kernel, int param, tcpck_stream stream) {
-  if (!d_hdr) {
-    return d_offsets ? tcpck_batch_var_ex(ctx, TCPCK_OP_RECEIVE, mode, d_arena, d_offsets, d_lengths, count, d_ok,
-                                          layout, kernel, param, stream)
-                     : tcpck_batch_fixed_ex(ctx, TCPCK_OP_RECEIVE, mode, d_arena, stride, len, count, d_ok, kernel,
-                                            param, stream);
-  }
-  if (!ctx || !valid_device_op_mode(TCPCK_OP_VERIFY, mode)) return TCPCK_EINVAL;
-  if (count == 0) return TCPCK_OK;
-  if (!d_arena || !d_ok || (reinterpret_cast<uintptr_t>(d_arena) & 1) || (reinterpret_cast<uintptr_t>(d_hdr) & 3))
-    return TCPCK_EINVAL;
-  if (count > (UINT64_MAX >> 6)) return TCPCK_EINVAL;
-  if (!d_offsets) {
-    if ((len & 1) || (stride & 1) || len < TCPCK_HEADER_BYTES || (count > 1 && stride < len)) return TCPCK_EINVAL;
-    if (count > 1 && stride > (UINT64_MAX - len) / (count - 1)) return TCPCK_EINVAL;
-    if (count == 1) stride = len;
-  } else if (!d_lengths) {
-    return TCPCK_EINVAL;
-  }
-  DeviceGuard g(ctx->device);
-  if (g.status() != hipSuccess) return hip_status(g.status());
-  auto *arena = static_cast<uint8_t *>(d_arena);
-  auto *hdr = static_cast<uint8_t *>(d_hdr);
-  const auto s = static_cast<hipStream_t>(stream);
-#ifdef TCPCK_PROBE
-  if (param & kReceiveConcurrent) {
-    // the header pass on the context's side stream, beside the VERIFY pass on
-    // the caller's: it reads the same arena, writes only the header array
-    hipError_t e = ensure_side(ctx);
-    if (e != hipSuccess) return hip_status(e);
-    std::lock_guard<std::mutex> lk(ctx->side_mu);  // one fork / join at a time per context
-    tcpck::HeaderArgs h{};
-    h.arena = arena;
-    h.offsets = d_offsets;
-    h.stride = stride;
-    h.count = count;
-    h.out = hdr;
-    e = hipEventRecord(ctx->fork, s);
-    if (e == hipSuccess) e = hipStreamWaitEvent(ctx->side, ctx->fork, 0);
-    if (e == hipSuccess) e = tcpck::launch_header_swap(h, static_cast<uint32_t>(ctx->num_cus), ctx->side);
-    if (e == hipSuccess) {
-      const int p = param & ~kReceiveConcurrent;
-      e = d_offsets ? run_var(ctx, TCPCK_OP_VERIFY, mode, arena, d_offsets, d_lengths, 0, count, d_ok, layout, kernel,
-                              p, s)
-                    : run_fixed(ctx, TCPCK_OP_VERIFY, mode, arena, stride, len, count, d_ok, kernel, p, s);
-    }
-    const hipError_t e2 = hipEventRecord(ctx->join, ctx->side);
-    const hipError_t e3 = e2 == hipSuccess ? hipStreamWaitEvent(s, ctx->join, 0) : e2;
-    return hip_status(e != hipSuccess ? e : e3);
-  }
-#endif
-  return hip_status(d_offsets ? run_var(ctx, TCPCK_OP_RECEIVE, mode, arena, d_offsets, d_lengths, 0, count, d_ok,
-                                        layout, kernel, param, s, hdr)
-                              : run_fixed(ctx, TCPCK_OP_RECEIVE, mode, arena, stride, len, count, d_ok, kernel,
-                                          param, s, hdr));
+  return tcpck::api::batch_receive_ex(ctx, mode, d_arena, stride, len, d_offsets, d_lengths, count, d_ok, d_hdr,
+                                      layout, TCPCK_KERNEL_AUTO, 0, static_cast<hipStream_t>(stream), Hooks{});
 }
 
 // ---- header byte order: TcpHeaderN2H / TcpHeaderH2N in place -----------------------
@@ -1170,8 +1146,8 @@ int tcpck_host_batch_fixed(tcpck_ctx *ctx, int op, int mode, void *h_arena, uint
     hipStream_t s = ctx->s[slot];
     e = hipMemcpyAsync(ctx->stage[slot], arena + k0 * stride, bytes, hipMemcpyHostToDevice, s);
     if (e != hipSuccess) break;
-    e = run_fixed(ctx, op, mode, ctx->stage[slot], stride, len, n, ctx->stage_out[slot], TCPCK_KERNEL_AUTO,
-                  0, s);
+    e = tcpck::api::run_fixed(ctx, op, mode, ctx->stage[slot], stride, len, n, ctx->stage_out[slot],
+                              TCPCK_KERNEL_AUTO, 0, s, nullptr, Hooks{});
     if (e != hipSuccess) break;
     e = hipMemcpyAsync(out_bytes + k0 * es, ctx->stage_out[slot], n * es, hipMemcpyDeviceToHost, s);
   }
@@ -1243,8 +1219,8 @@ int tcpck_host_batch_var(tcpck_ctx *ctx, int op, int mode, void *h_arena, const 
     if (e == hipSuccess)
       e = hipMemcpyAsync(ctx->stage_len[slot], h_lengths + k0, n * 4, hipMemcpyHostToDevice, s);
     if (e != hipSuccess) break;
-    e = run_var(ctx, op, mode, ctx->stage[slot], ctx->stage_off[slot], ctx->stage_len[slot], lo, n,
-                ctx->stage_out[slot], &lay, TCPCK_KERNEL_AUTO, 0, s);
+    e = tcpck::api::run_var(ctx, op, mode, ctx->stage[slot], ctx->stage_off[slot], ctx->stage_len[slot], lo, n,
+                            ctx->stage_out[slot], &lay, TCPCK_KERNEL_AUTO, 0, s, nullptr, Hooks{});
     if (e != hipSuccess) break;
     e = hipMemcpyAsync(out_bytes + k0 * es, ctx->stage_out[slot], n * es, hipMemcpyDeviceToHost, s);
     k0 = k1;

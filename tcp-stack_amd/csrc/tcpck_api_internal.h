@@ -1,0 +1,107 @@
+// tcpck_api_internal.h -- the context and the batch router shared by the C-ABI
+// layer (tcpck_api.hip), its tuning entry points (tcpck_ex.hip in libtcpck.so)
+// and their measurement twins (tcpck_ex_probe.hip in libtcpck_probe.so).  Not
+// installed.
+//
+// The router (tcpck::api::batch_*_ex) is the product's kernel policy and
+// nothing else; the probe library passes it a Hooks value to reach the
+// measured alternatives (header pass forms, fused headers on explicit kernels),
+// the product library always passes Hooks{}.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <mutex>
+
+#include "tcpck.h"
+
+struct tcpck_ctx {
+  int device = 0;
+  int num_cus = 256;
+
+  // end-to-end (host batch) pipeline state, created lazily
+  std::mutex mu;
+  hipStream_t s[2] = {nullptr, nullptr};
+  uint8_t *stage[2] = {nullptr, nullptr};     // image bytes
+  uint8_t *stage_out[2] = {nullptr, nullptr}; // results
+  uint64_t *stage_off[2] = {nullptr, nullptr};
+  uint32_t *stage_len[2] = {nullptr, nullptr};
+  uint64_t stage_bytes = 0;
+  uint64_t stage_images = 0;
+  uint64_t chunk_bytes = 64ull << 20;
+
+  // FILL without a results buffer (the reference's insert stores only into the
+  // packet, socket-manager.cc:9-10): the results go to this ctx-owned scratch,
+  // allocated at tcpck_ctx_create, so AUTO keeps its two-pass forms (the stream
+  // writes the results, the write-through field pass stores them).  Batches of
+  // more images run in chunks.  `scratch_ev` is recorded after every use; a
+  // call on another stream than the last user's waits for it first.
+  std::mutex scratch_mu;
+  uint16_t *scratch = nullptr;
+  uint64_t scratch_images = 0;
+  hipEvent_t scratch_ev = nullptr;
+  hipStream_t scratch_last = nullptr;
+  bool scratch_used = false;
+
+  // probe library only (tcpck_ex_probe.hip): per-wave time stamp buffer, and the
+  // side stream + events of the concurrent RECEIVE form
+  void *dbg = nullptr;
+  std::mutex side_mu;
+  hipStream_t side = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+};
+
+namespace tcpck {
+namespace api {
+
+constexpr uint64_t kScratchImages = 8ull << 20;  // 16 MiB of u16 results: C5's 8M images in one chunk
+
+// Measurement hooks (libtcpck_probe.so only; the product passes Hooks{}).
+struct Hooks {
+  bool fuse_any_hdr = false;     // RECEIVE, explicit kernel: fuse the headers into any kernel that can
+                                 // (sstream's after-the-verdicts conversion, HDR 1)
+  bool hdr_first = false;        // offset lists, RECEIVE + TCPCK_PARAM_RECEIVE_TWO_PASS: header pass first
+  uint32_t hdr_store_bits = 0;   // HeaderArgs::store_bits of the header pass
+};
+
+int hip_status(hipError_t e);
+
+// Saves the calling thread's current device, switches to `device`, restores.
+class DeviceGuard {
+ public:
+  explicit DeviceGuard(int device);
+  ~DeviceGuard();
+  hipError_t status() const { return ok_; }
+  DeviceGuard(const DeviceGuard &) = delete;
+  DeviceGuard &operator=(const DeviceGuard &) = delete;
+
+ private:
+  int prev_ = -1;
+  hipError_t ok_ = hipSuccess;
+};
+
+// The validated device-batch entry points (tcpck_tuning.h semantics).
+int batch_fixed_ex(tcpck_ctx *ctx, int op, int mode, void *d_arena, uint64_t stride, uint32_t len, uint64_t count,
+                   void *d_out, int kernel, int param, hipStream_t stream, const Hooks &hk);
+int batch_var_ex(tcpck_ctx *ctx, int op, int mode, void *d_arena, const uint64_t *d_offsets,
+                 const uint32_t *d_lengths, uint64_t count, void *d_out, const tcpck_layout *layout, int kernel,
+                 int param, hipStream_t stream, const Hooks &hk);
+int batch_receive_ex(tcpck_ctx *ctx, int mode, void *d_arena, uint64_t stride, uint32_t len,
+                     const uint64_t *d_offsets, const uint32_t *d_lengths, uint64_t count, uint8_t *d_ok,
+                     void *d_hdr, const tcpck_layout *layout, int kernel, int param, hipStream_t stream,
+                     const Hooks &hk);
+// batch_receive_ex's checks without the launch (TCPCK_OK or the error status)
+int check_receive(const tcpck_ctx *ctx, int mode, const void *d_arena, uint64_t &stride, uint32_t len,
+                  const uint64_t *d_offsets, const uint32_t *d_lengths, uint64_t count, const uint8_t *d_ok,
+                  const void *d_hdr);
+
+// The routed launches behind them (device already selected, arguments valid).
+hipError_t run_fixed(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t stride, uint32_t len, uint64_t count,
+                     void *out, int kernel, int param, hipStream_t s, uint8_t *hdr, const Hooks &hk);
+hipError_t run_var(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const uint64_t *off, const uint32_t *len,
+                   uint64_t base, uint64_t count, void *out, const tcpck_layout *layout, int kernel, int param,
+                   hipStream_t s, uint8_t *hdr, const Hooks &hk);
+
+}  // namespace api
+}  // namespace tcpck

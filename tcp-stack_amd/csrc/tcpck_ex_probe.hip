@@ -1,0 +1,155 @@
+// tcpck_ex_probe.hip -- libtcpck_probe.so's tuning entry points
+// (include/tcpck_tuning.h) and its measurement-only ones (include/tcpck_probe.h).
+//
+// Built only into the probe library, in place of tcpck_ex.hip: the product
+// router (tcpck::api, tcpck_api.hip) with the measurement hooks switched on,
+// so that the router itself carries no probe switches.
+//   * tcpck_batch_fixed_ex: also TCPCK_KERNEL_PATCH, FILL's field pass alone;
+//   * tcpck_batch_receive_ex: with an explicit kernel, the headers fused into
+//     any kernel that can (sstream's after-the-verdicts conversion, HDR 1);
+//   * tcpck_probe_receive_ex: the header pass forms (TCPCK_PROBE_RECEIVE_*);
+//   * tcpck_ctx_set_debug, tcpck_diag_stream.
+#include <hip/hip_runtime.h>
+
+#include <mutex>
+
+#include "tcpck.h"
+#include "tcpck_probe.h"
+#include "tcpck_tuning.h"
+#include "tcpck_internal.h"
+#include "tcpck_api_internal.h"
+
+using tcpck::api::DeviceGuard;
+using tcpck::api::Hooks;
+using tcpck::api::hip_status;
+
+namespace {
+
+Hooks probe_hooks(int flags) {
+  Hooks h;
+  h.fuse_any_hdr = true;
+  h.hdr_first = (flags & TCPCK_PROBE_RECEIVE_HDR_FIRST) != 0;
+  h.hdr_store_bits = ((flags & TCPCK_PROBE_RECEIVE_HDR_WT) ? 1u : 0u) |
+                     ((flags & TCPCK_PROBE_RECEIVE_HDR_WIDE)
+                          ? 2u | ((static_cast<uint32_t>(flags) >> TCPCK_PROBE_RECEIVE_CACHE_SHIFT & 3u) << 4)
+                          : 0u);
+  return h;
+}
+
+// The side stream and the two events that let RECEIVE's header pass run
+// concurrently with its VERIFY pass.  Created once per context, on first use
+// (freed by tcpck_ctx_destroy).
+hipError_t ensure_side(tcpck_ctx *ctx) {
+  if (ctx->side) return hipSuccess;
+  hipStream_t st = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  hipError_t e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&e0, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&e1, hipEventDisableTiming);
+  if (e != hipSuccess) {
+    if (e1) (void)hipEventDestroy(e1);
+    if (e0) (void)hipEventDestroy(e0);
+    if (st) (void)hipStreamDestroy(st);
+    return e;
+  }
+  ctx->fork = e0;
+  ctx->join = e1;
+  ctx->side = st;
+  return hipSuccess;
+}
+
+}  // namespace
+
+extern "C" {
+
+int tcpck_batch_fixed_ex(tcpck_ctx *ctx, int op, int mode, void *d_arena, uint64_t stride, uint32_t len,
+                         uint64_t count, void *d_out, int kernel, int param, tcpck_stream stream) {
+  if (kernel == TCPCK_KERNEL_PATCH) {  // the deferred field pass alone (timing)
+    if (!ctx || op != TCPCK_OP_FILL || !d_arena || !d_out || count == 0 || stride < 30 || len > stride)
+      return TCPCK_EINVAL;
+    DeviceGuard g(ctx->device);
+    if (g.status() != hipSuccess) return hip_status(g.status());
+    tcpck::PatchArgs pa{};
+    pa.arena = static_cast<uint8_t *>(d_arena);
+    pa.stride = stride;
+    pa.count = count;
+    pa.sums = static_cast<uint16_t *>(d_out);
+    pa.hi = (count - 1) * stride + len;
+    pa.probe_form = 1;
+    pa.store_bits = static_cast<uint32_t>(param & 0xFF);  // 1 + sc0 1 | nt 2 | sc1 4 (0 = plain) | form << 4
+    return hip_status(tcpck::launch_patch_fields(pa, static_cast<uint32_t>(ctx->num_cus),
+                                                 static_cast<hipStream_t>(stream)));
+  }
+  return tcpck::api::batch_fixed_ex(ctx, op, mode, d_arena, stride, len, count, d_out, kernel, param,
+                                    static_cast<hipStream_t>(stream), probe_hooks(0));
+}
+
+int tcpck_batch_var_ex(tcpck_ctx *ctx, int op, int mode, void *d_arena, const uint64_t *d_offsets,
+                       const uint32_t *d_lengths, uint64_t count, void *d_out, const tcpck_layout *layout,
+                       int kernel, int param, tcpck_stream stream) {
+  return tcpck::api::batch_var_ex(ctx, op, mode, d_arena, d_offsets, d_lengths, count, d_out, layout, kernel, param,
+                                  static_cast<hipStream_t>(stream), probe_hooks(0));
+}
+
+int tcpck_batch_receive_ex(tcpck_ctx *ctx, int mode, void *d_arena, uint64_t stride, uint32_t len,
+                           const uint64_t *d_offsets, const uint32_t *d_lengths, uint64_t count, uint8_t *d_ok,
+                           void *d_hdr, const tcpck_layout *layout, int kernel, int param, tcpck_stream stream) {
+  return tcpck_probe_receive_ex(ctx, mode, d_arena, stride, len, d_offsets, d_lengths, count, d_ok, d_hdr, layout,
+                                kernel, param, 0, stream);
+}
+
+int tcpck_probe_receive_ex(tcpck_ctx *ctx, int mode, void *d_arena, uint64_t stride, uint32_t len,
+                           const uint64_t *d_offsets, const uint32_t *d_lengths, uint64_t count, uint8_t *d_ok,
+                           void *d_hdr, const tcpck_layout *layout, int kernel, int param, int probe_flags,
+                           tcpck_stream stream) {
+  const Hooks hk = probe_hooks(probe_flags);
+  const auto s = static_cast<hipStream_t>(stream);
+  if (!(probe_flags & TCPCK_PROBE_RECEIVE_CONCURRENT) || !d_hdr)
+    return tcpck::api::batch_receive_ex(ctx, mode, d_arena, stride, len, d_offsets, d_lengths, count, d_ok, d_hdr,
+                                        layout, kernel, param, s, hk);
+  // the header pass on the context's side stream, beside the VERIFY pass on
+  // the caller's: it reads the same arena, writes only the header array
+  int rc = tcpck::api::check_receive(ctx, mode, d_arena, stride, len, d_offsets, d_lengths, count, d_ok, d_hdr);
+  if (rc != TCPCK_OK || count == 0) return rc;
+  DeviceGuard g(ctx->device);
+  if (g.status() != hipSuccess) return hip_status(g.status());
+  std::lock_guard<std::mutex> lk(ctx->side_mu);  // one fork / join at a time per context
+  hipError_t e = ensure_side(ctx);
+  if (e != hipSuccess) return hip_status(e);
+  auto *arena = static_cast<uint8_t *>(d_arena);
+  tcpck::HeaderArgs h{};
+  h.arena = arena;
+  h.offsets = d_offsets;
+  h.stride = stride;
+  h.count = count;
+  h.out = static_cast<uint8_t *>(d_hdr);
+  h.store_bits = hk.hdr_store_bits;
+  e = hipEventRecord(ctx->fork, s);
+  if (e == hipSuccess) e = hipStreamWaitEvent(ctx->side, ctx->fork, 0);
+  if (e == hipSuccess) e = tcpck::launch_header_swap(h, static_cast<uint32_t>(ctx->num_cus), ctx->side);
+  if (e == hipSuccess)
+    e = d_offsets ? tcpck::api::run_var(ctx, TCPCK_OP_VERIFY, mode, arena, d_offsets, d_lengths, 0, count, d_ok,
+                                        layout, kernel, param, s, nullptr, hk)
+                  : tcpck::api::run_fixed(ctx, TCPCK_OP_VERIFY, mode, arena, stride, len, count, d_ok, kernel, param,
+                                          s, nullptr, hk);
+  const hipError_t e2 = hipEventRecord(ctx->join, ctx->side);
+  const hipError_t e3 = e2 == hipSuccess ? hipStreamWaitEvent(s, ctx->join, 0) : e2;
+  return hip_status(e != hipSuccess ? e : e3);
+}
+
+int tcpck_diag_stream(tcpck_ctx *ctx, int variant, const void *d_buf, uint64_t bytes, void *d_out,
+                      tcpck_stream stream) {
+  if (!ctx || !d_buf || !d_out || bytes < 4096) return TCPCK_EINVAL;
+  DeviceGuard g(ctx->device);
+  return hip_status(tcpck::launch_diag_stream(variant, static_cast<const uint8_t *>(d_buf), bytes,
+                                              static_cast<uint32_t *>(d_out), static_cast<uint32_t>(ctx->num_cus),
+                                              static_cast<hipStream_t>(stream)));
+}
+
+int tcpck_ctx_set_debug(tcpck_ctx *ctx, void *d_buf) {
+  if (!ctx) return TCPCK_EINVAL;
+  ctx->dbg = d_buf;
+  return TCPCK_OK;
+}
+
+}  // extern "C"

@@ -361,7 +361,8 @@ hipError_t launch_patch_fields(const PatchArgs &a, uint32_t num_cus, hipStream_t
   if (a.count == 0) return hipSuccess;
   if (!a.sums) return hipErrorInvalidValue;
 #ifdef TCPCK_PROBE
-  if (a.store_bits && !a.update && !a.offsets) {  // timing forms (TCPCK_KERNEL_PATCH param)
+  if (a.probe_form) {  // timing forms (TCPCK_KERNEL_PATCH param)
+    if (a.update || a.offsets) return hipErrorInvalidValue;
     if ((a.store_bits >> 4) >= 4 && (a.store_bits >> 4) < 8) {  // the 2-B write-through pass with other maps
       static const uint32_t per_cu = 8;
       const int map = static_cast<int>(a.store_bits >> 4) - 4;

@@ -162,8 +162,9 @@ struct HeaderArgs {
   uint64_t stride;
   uint64_t count;
   uint8_t *out;             // null: convert in place; else header k -> out[32k, 32k + 32), arena untouched
-  uint32_t store_bits;      // probe builds, EXTRACT: 1 = write-through (sc0 sc1 nt) array stores;
-                            // 2 = two lanes per image, 16-B loads with cache bits form (bits 4-5)
+  uint32_t store_bits;      // probe builds (tcpck_probe_receive_ex), EXTRACT: 1 = write-through
+                            // (sc0 sc1 nt) array stores; 2 = two lanes per image, 16-B loads with
+                            // cache bits form (bits 4-5)
 };
 hipError_t launch_header_swap(const HeaderArgs &a, uint32_t num_cus, hipStream_t stream);
 
@@ -189,7 +190,8 @@ struct PatchArgs {
   uint64_t lo, hi;          // probe block forms: byte range (relative to arena) their writes may cover
   uint32_t update;          // 1: sums hold CHECKSUM results, derive FILL's from the old field
   uint32_t packed;          // offset lists: the PACKED contract holds (unused by the 2-B pass)
-  uint32_t store_bits;      // probe builds: 1 + store cache bits (sc0 1, nt 2, sc1 4; 0 plain) | granularity << 4
+  uint32_t probe_form;      // probe builds (TCPCK_KERNEL_PATCH): a timing form chosen by store_bits
+  uint32_t store_bits;      // probe forms: 1 + store cache bits (sc0 1, nt 2, sc1 4; 0 plain) | granularity << 4
 };
 hipError_t launch_patch_fields(const PatchArgs &a, uint32_t num_cus, hipStream_t stream);
 

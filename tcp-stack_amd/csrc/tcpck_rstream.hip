@@ -30,8 +30,9 @@
 //     the RFC 1071 prefix is an exact word sum); they go into bytes 28-29
 //     (tcp-header.h:177); kVerify stores checksum == 0.
 //     With FixedStreamArgs::defer_field, kFill writes only the results, and
-//     launch_patch_fields (tcpck_header.hip) stores the fields afterwards as
-//     whole 64-B blocks (the AUTO choice when there is a results buffer).
+//     launch_patch_fields (tcpck_header.hip) stores the fields afterwards,
+//     one write-through 2-B store per image (AUTO's choice; FILL without a
+//     results buffer uses the context's scratch for them).
 #include "tcpck_device.h"
 
 namespace tcpck {

@@ -57,11 +57,16 @@ SEG_SHAPES = {1: "G8/U2", 2: "G16/U6", 3: "G64/U4", 4: "G64/U2", 5: "G32/U3", 6:
 # include/tcpck_tuning.h: in libtcpck.so (AUTO's kernels only) and libtcpck_probe.so
 TUNING_EXPORTS = ("tcpck_batch_fixed_ex", "tcpck_batch_var_ex", "tcpck_batch_segment_ex", "tcpck_batch_receive_ex")
 # include/tcpck_tuning.h, measurement only: libtcpck_probe.so
-PROBE_EXPORTS = ("tcpck_ctx_set_debug", "tcpck_diag_stream")
+PROBE_EXPORTS = ("tcpck_ctx_set_debug", "tcpck_diag_stream", "tcpck_probe_receive_ex")
+# include/tcpck_probe.h: tcpck_probe_receive_ex's flags word (the header pass forms)
+PROBE_RECEIVE_HDR_FIRST = 1    # offset lists, with PARAM_RECEIVE_TWO_PASS: header pass first
+PROBE_RECEIVE_CONCURRENT = 2   # header pass on a side stream beside VERIFY
+PROBE_RECEIVE_HDR_WT = 4       # header array stores written through
+PROBE_RECEIVE_HDR_WIDE = 8     # two lanes per image, 16-B loads with cache bits (flags >> 4) & 3
 # Kernel params libtcpck.so runs (the AUTO policy's own choices, tcpck_api.hip
 # run_fixed_impl / run_var_impl); every other value needs libtcpck_probe.so.
 SEG_AUTO_SHAPES = (0, 1, 2, 7, 8, 9, 11)  # by length, G8/U2, G16/U6, W4, W8, W16, W2 (shape_for_len)
-RSTREAM_AUTO = (20, 25)                   # the policy; 25: its FILL with the field-block pass
+RSTREAM_AUTO = (20, 25)                   # the policy; 25: its FILL with the write-through 2-B field pass
 GSTREAM_AUTO = (0, 0x80, 0x401)           # (+ 4: default block order)
 SSTREAM_AUTO = (0, 32, 128)               # the policy; + 32: RECEIVE headers from the stream; + 128: FILL's deferred fields
 
@@ -171,6 +176,8 @@ def lib(probe: bool = False) -> ctypes.CDLL:
         "tcpck_batch_var_ex": (i32, [vp, i32, i32, vp, vp, vp, u64, vp, ctypes.POINTER(Layout), i32, i32, vp]),
         "tcpck_ctx_set_debug": (i32, [vp, vp]),
         "tcpck_diag_stream": (i32, [vp, i32, vp, u64, vp, vp]),
+        "tcpck_probe_receive_ex": (i32, [vp, i32, vp, u64, u32, vp, vp, u64, vp, vp, ctypes.POINTER(Layout), i32, i32,
+                                         i32, vp]),
     }
     for name, (res, args) in sig.items():
         if name in PROBE_EXPORTS and not probe:
@@ -323,16 +330,20 @@ class Context:
     def batch_receive(self, arena, count: int, ok, hdr=None, stride: int = 0, length: int = 0, offsets=None,
                       lengths=None, mode: int = MODE_REF, total_bytes: int = 0, min_len: int = 0, max_len: int = 0,
                       packed: bool = False, sorted: bool = False, stream=None, kernel: int | None = None,
-                      param: int = 0) -> None:
+                      param: int = 0, probe_flags: int | None = None) -> None:
         """ReceivePacket's front half for a batch (tcpck_batch_receive): ok[k] = verdict on the
         network-order image; headers in host order in place (hdr None) or into hdr (32 B per image,
         the arena left as received).  Fixed layout (stride, length) or offsets + lengths.
-        kernel/param: tcpck_batch_receive_ex (include/tcpck_tuning.h)."""
+        kernel/param: tcpck_batch_receive_ex (include/tcpck_tuning.h); probe_flags (probe contexts
+        only): tcpck_probe_receive_ex's header pass forms (PROBE_RECEIVE_*, include/tcpck_probe.h)."""
         lay = Layout(total_bytes, min_len, max_len,
                      (LAYOUT_PACKED if packed else 0) | (LAYOUT_SORTED if sorted else 0), 0)
         args = (self._h, mode, _ptr(arena), stride, length, _ptr(offsets), _ptr(lengths), count, _ptr(ok), _ptr(hdr),
                 ctypes.byref(lay))
-        if kernel is None:
+        if probe_flags is not None:
+            _check(self._L.tcpck_probe_receive_ex(*args, kernel or KERNEL_AUTO, param, probe_flags, _stream(stream)),
+                   "tcpck_probe_receive_ex")
+        elif kernel is None:
             _check(self._L.tcpck_batch_receive(*args, _stream(stream)), "tcpck_batch_receive")
         else:
             _check(self._L.tcpck_batch_receive_ex(*args, kernel, param, _stream(stream)), "tcpck_batch_receive_ex")

@@ -31,7 +31,24 @@ def test_c5_is_the_strong_split():
 def test_extras_order():
     names = [n for n, _ in bench.EXTRAS]
     assert names[0] == "c5"
-    assert names[-2:] == ["c3", "c4"]
+    assert names[-3:] == ["c3", "fill_c3", "c4"]
+
+
+def test_pmc_traffic_belongs_to_the_loaded_library(tmp_path, monkeypatch):
+    """A PMC entry counts only when its sha256 stamp is the loaded libtcpck.so's
+    (traffic from a kernel the product no longer ran)."""
+    import json
+    sha = bench.lib_sha256()
+    entry = {"hbm_bytes_per_launch": 123, "source": "profiles/rX/pmc_c2_{fetch,write}.csv"}
+    (tmp_path / "profiles").mkdir()
+    for stamp, want in ((sha, 123), ("0" * 64, None), (None, None)):
+        e = dict(entry, lib_sha256=stamp) if stamp else dict(entry)
+        (tmp_path / "profiles" / "pmc_summary.json").write_text(json.dumps({"c2": e}))
+        monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+        got, note = bench.pmc_traffic("c2")
+        assert got == want, note
+    got, note = bench.pmc_traffic("c9")
+    assert got is None and "no PMC pass" in note
 
 
 def test_metric_per_kind():
