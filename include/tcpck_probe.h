@@ -37,12 +37,17 @@ extern "C" {
  *   HDR_WT      the header array stores written through (sc0 sc1 nt)
  *   HDR_WIDE    two lanes per 16-B aligned image, one 16-B buffer load each,
  *               with the load cache bits (flags >> CACHE_SHIFT) & 3: 0
- *               default, 1 nt, 2 sc0 sc1, 3 sc1 */
+ *               default, 1 nt, 2 sc0 sc1, 3 sc1
+ *   ORDER       (flags >> ORDER_SHIFT) & 3, the product's header pass in
+ *               another image order: 1 XCD-chunked blocks, 2 blocks scattered
+ *               over the batch, 3 each block's images 1/128 of the batch
+ *               apart (0: in order) */
 #define TCPCK_PROBE_RECEIVE_HDR_FIRST 1
 #define TCPCK_PROBE_RECEIVE_CONCURRENT 2
 #define TCPCK_PROBE_RECEIVE_HDR_WT 4
 #define TCPCK_PROBE_RECEIVE_HDR_WIDE 8
 #define TCPCK_PROBE_RECEIVE_CACHE_SHIFT 4
+#define TCPCK_PROBE_RECEIVE_ORDER_SHIFT 8
 int tcpck_probe_receive_ex(tcpck_ctx *ctx, int mode, void *d_arena, uint64_t stride, uint32_t len,
                            const uint64_t *d_offsets, const uint32_t *d_lengths, uint64_t count, uint8_t *d_ok,
                            void *d_hdr, const tcpck_layout *layout, int kernel, int param, int probe_flags,

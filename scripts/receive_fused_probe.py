@@ -154,6 +154,40 @@ def wide(ctx, s, rng, n):
           flush=True)
 
 
+def order(ctx, s, rng, n):
+    """--order (round 4): the receive ring's header pass with the images in
+    another order (tcpck_probe_receive_ex ORDER: 1 XCD-chunked blocks, 2 blocks
+    scattered over the batch, 3 each block's images 1/128 of the batch apart)
+    against the product's in-order pass, and VERIFY alone; per RECEIVE step,
+    the header pass = RECEIVE - VERIFY.  Results compared."""
+    mix = (np.asarray((64, 576, 1460), np.uint32)[rng.integers(0, 3, n)] + 32).astype(np.uint32)
+    img = int(mix.astype(np.int64).sum())
+    S = tcpck.KERNEL_SSTREAM
+    slot = 2048
+    off = np.arange(n, dtype=np.uint64) * np.uint64(slot)
+    a = torch.empty(n * slot, dtype=torch.uint8, device="cuda")
+    d_off, d_ln = torch.from_numpy(off).cuda(), torch.from_numpy(mix).cuda()
+    tcpck.synth_var(a, d_off, d_ln, int(mix.max()), n, seed=42)
+    ok = torch.empty(n, dtype=torch.uint8, device="cuda")
+    hdr = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
+    kw = dict(offsets=d_off, lengths=d_ln, total_bytes=img, min_len=int(mix.min()), max_len=int(mix.max()),
+              sorted=True, stream=s)
+    ver = b2b(lambda: ctx.batch_var_ex(tcpck.OP_VERIFY, a, d_off, d_ln, n, ok, kernel=S, param=0, total_bytes=img,
+                                       min_len=int(mix.min()), max_len=int(mix.max()), sorted=True, stream=s), s)
+    print(f"ring 1M x 2048 (bench mix)   VERIFY only    {ver * 1e3:8.1f} us", flush=True)
+    res = {}
+    for label, f in (("in order", 0), ("XCD-chunked", 1 << 8), ("scattered", 2 << 8), ("transposed", 3 << 8),
+                     ("in order", 0)):
+        ms = b2b(lambda: ctx.batch_receive(a, n, ok, hdr, kernel=S, param=TWO, probe_flags=f, **kw), s)
+        torch.cuda.synchronize()
+        res[label] = (ok.clone(), hdr.clone())
+        print(f"ring 1M x 2048 (bench mix)   {label:14s} {ms * 1e3:8.1f} us  header pass {(ms - ver) * 1e3:6.1f} us",
+              flush=True)
+    ref = res["in order"]
+    print("results identical:", all(torch.equal(v[0], ref[0]) and torch.equal(v[1], ref[1]) for v in res.values()),
+          flush=True)
+
+
 def main():
     ctx = tcpck.Context(0, probe=True)
     s = torch.cuda.current_stream()
@@ -164,6 +198,9 @@ def main():
         return
     if "--sweep" in sys.argv:
         sweep(ctx, s, rng, n)
+        return
+    if "--order" in sys.argv:
+        order(ctx, s, rng, n)
         return
     mix = (np.asarray((64, 576, 1460), np.uint32)[rng.integers(0, 3, n)] + 32).astype(np.uint32)
     case(ctx, s, "ring 1M x 2048 (bench mix)", n, 2048, mix)

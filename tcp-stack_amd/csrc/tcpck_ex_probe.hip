@@ -32,7 +32,8 @@ Hooks probe_hooks(int flags) {
   h.hdr_store_bits = ((flags & TCPCK_PROBE_RECEIVE_HDR_WT) ? 1u : 0u) |
                      ((flags & TCPCK_PROBE_RECEIVE_HDR_WIDE)
                           ? 2u | ((static_cast<uint32_t>(flags) >> TCPCK_PROBE_RECEIVE_CACHE_SHIFT & 3u) << 4)
-                          : 0u);
+                          : 0u) |
+                     ((static_cast<uint32_t>(flags) >> TCPCK_PROBE_RECEIVE_ORDER_SHIFT & 3u) << 8);
   return h;
 }
 

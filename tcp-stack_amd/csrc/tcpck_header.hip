@@ -116,13 +116,29 @@ hipError_t wide_by_policy(const HeaderArgs &a, uint32_t num_cus, hipStream_t s) 
 // pass fetches the same 128-B line per image either way, whatever the load's
 // cache bits: scripts/receive_fused_probe.py --wide, profiles/r03/
 // receive_header_wide.log).
-template <bool FIXED>
+//
+// ORDER (probe builds, tcpck_probe_receive_ex's ORDER field; 0 = the
+// product's): which images a block reads together, i.e. which header lines are
+// in flight at once -- 1: XCD-chunked block order (groups of 16 blocks per
+// XCD), 2: multiplicative block scatter (the blocks in flight spread over the
+// whole batch), 3: each block's 128 images 1/128 of the batch apart.
+template <bool FIXED, int ORDER = 0>
 __global__ void __launch_bounds__(kBlock) header_extract_kernel(HeaderArgs a) {
   const uint64_t step = static_cast<uint64_t>(gridDim.x) * kBlock;
   const bool out16 = (reinterpret_cast<uintptr_t>(a.out) & 15u) == 0;
-  for (uint64_t t = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x; t < a.count * 2; t += step) {
-    const uint64_t k = t >> 1;
+  uint32_t bid = blockIdx.x;
+  if constexpr (ORDER == 1) bid = dev::ordered_block(blockIdx.x, gridDim.x, 4u);
+  if constexpr (ORDER == 2) bid = static_cast<uint32_t>((uint64_t{blockIdx.x} * 2654435761ull) % gridDim.x);
+  const uint64_t n2 = a.count * 2;
+  for (uint64_t t = static_cast<uint64_t>(bid) * kBlock + threadIdx.x; t < n2; t += step) {
+    uint64_t k = t >> 1;
     const uint32_t h = static_cast<uint32_t>(t & 1);
+    if constexpr (ORDER == 3) {
+      // t's image as a 128 x (count / 128) transpose: lane pair i of block
+      // group g reads image i * (count / 128) + g; the tail stays in order
+      const uint64_t rows = a.count >> 7, body = rows << 7;
+      if (k < body) k = (k & 127u) * rows + (k >> 7);
+    }
     const uint8_t *p = a.arena + (FIXED ? k * a.stride : a.offsets[k]) + 16 * h;
     dev::u32x4 v;
     if ((reinterpret_cast<uintptr_t>(p) & 15u) == 0) {
@@ -136,22 +152,23 @@ __global__ void __launch_bounds__(kBlock) header_extract_kernel(HeaderArgs a) {
     // reversed, 2/6 the upper u16 swapped, 3 the two ports, 7 the urgent pointer
     const dev::u32x4 o{dev::n2h_dword(v.x, 0x00010203u), dev::n2h_dword(v.y, 0x00010203u),
                        dev::n2h_dword(v.z, 0x02030100u), dev::n2h_dword(v.w, h ? 0x02030100u : 0x02030001u)};
+    const uint64_t r = (k << 1) | h;  // header k's half h (== t in order)
     if (out16) {
-      reinterpret_cast<dev::u32x4 *>(a.out)[t] = o;
+      reinterpret_cast<dev::u32x4 *>(a.out)[r] = o;
     } else {
-      uint32_t *d = reinterpret_cast<uint32_t *>(a.out) + 4 * t;
+      uint32_t *d = reinterpret_cast<uint32_t *>(a.out) + 4 * r;
       d[0] = o.x, d[1] = o.y, d[2] = o.z, d[3] = o.w;
     }
   }
 }
 
-template <bool FIXED>
+template <bool FIXED, int ORDER = 0>
 hipError_t launch_extract(const HeaderArgs &a, uint32_t num_cus, hipStream_t s) {
-  static const uint32_t per_cu = dev::resident_blocks_per_cu(header_extract_kernel<FIXED>);
+  static const uint32_t per_cu = dev::resident_blocks_per_cu(header_extract_kernel<FIXED, ORDER>);
   uint64_t blocks = (a.count * 2 + kBlock - 1) / kBlock;
   const uint64_t cap = static_cast<uint64_t>(per_cu) * num_cus * 8;
   if (blocks > cap) blocks = cap;
-  hipLaunchKernelGGL((header_extract_kernel<FIXED>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0, s, a);
+  hipLaunchKernelGGL((header_extract_kernel<FIXED, ORDER>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0, s, a);
   return hipGetLastError();
 }
 
@@ -409,6 +426,13 @@ hipError_t launch_header_swap(const HeaderArgs &a, uint32_t num_cus, hipStream_t
         (!a.offsets && (a.stride & 15u)))
       return hipErrorInvalidValue;
     return a.offsets ? wide_by_policy<false>(a, num_cus, stream) : wide_by_policy<true>(a, num_cus, stream);
+  }
+  if (a.out && (a.store_bits >> 8) & 3u) {  // the array form in another image order
+    switch ((a.store_bits >> 8) & 3u) {
+      case 1: return a.offsets ? launch_extract<false, 1>(a, num_cus, stream) : launch_extract<true, 1>(a, num_cus, stream);
+      case 2: return a.offsets ? launch_extract<false, 2>(a, num_cus, stream) : launch_extract<true, 2>(a, num_cus, stream);
+      default: return a.offsets ? launch_extract<false, 3>(a, num_cus, stream) : launch_extract<true, 3>(a, num_cus, stream);
+    }
   }
   if (a.out && a.store_bits)
     return a.offsets ? launch_one<false, true, true>(a, num_cus, stream) : launch_one<true, true, true>(a, num_cus, stream);

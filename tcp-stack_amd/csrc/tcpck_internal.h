@@ -164,7 +164,7 @@ struct HeaderArgs {
   uint8_t *out;             // null: convert in place; else header k -> out[32k, 32k + 32), arena untouched
   uint32_t store_bits;      // probe builds (tcpck_probe_receive_ex), EXTRACT: 1 = write-through
                             // (sc0 sc1 nt) array stores; 2 = two lanes per image, 16-B loads with
-                            // cache bits form (bits 4-5)
+                            // cache bits form (bits 4-5); bits 8-9: the array form's image order
 };
 hipError_t launch_header_swap(const HeaderArgs &a, uint32_t num_cus, hipStream_t stream);
 

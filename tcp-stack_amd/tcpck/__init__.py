@@ -63,6 +63,7 @@ PROBE_RECEIVE_HDR_FIRST = 1    # offset lists, with PARAM_RECEIVE_TWO_PASS: head
 PROBE_RECEIVE_CONCURRENT = 2   # header pass on a side stream beside VERIFY
 PROBE_RECEIVE_HDR_WT = 4       # header array stores written through
 PROBE_RECEIVE_HDR_WIDE = 8     # two lanes per image, 16-B loads with cache bits (flags >> 4) & 3
+PROBE_RECEIVE_ORDER_SHIFT = 8  # (flags >> 8) & 3: header pass image order (1 XCD-chunked, 2 scattered, 3 transposed)
 # Kernel params libtcpck.so runs (the AUTO policy's own choices, tcpck_api.hip
 # run_fixed_impl / run_var_impl); every other value needs libtcpck_probe.so.
 SEG_AUTO_SHAPES = (0, 1, 2, 7, 8, 9, 11)  # by length, G8/U2, G16/U6, W4, W8, W16, W2 (shape_for_len)
