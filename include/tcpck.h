@@ -101,7 +101,13 @@ const char *tcpck_strerror(int status);
 /* 1 when the library's gfx950 code object can run on `device`, else 0. */
 int tcpck_device_supported(int device);
 
-/* ---- context: one per device; owns no hidden global HIP state ------------ */
+/* ---- context: one per device; owns no hidden global HIP state ------------
+ * tcpck_ctx_create allocates the context's 16-MiB results scratch on `device`
+ * (TCPCK_ENOMEM if it cannot): a FILL without a results buffer writes its
+ * results there, 8M images per launch chunk, so the reference's call shape
+ * (socket-manager.cc:9-10 stores into the packet only) runs the same two-pass
+ * forms as a FILL with one.  Such FILLs are serialised per context; one on
+ * another stream than the scratch's last user first waits for that user. */
 int tcpck_ctx_create(int device, tcpck_ctx **out);
 int tcpck_ctx_destroy(tcpck_ctx *ctx);
 int tcpck_ctx_device(const tcpck_ctx *ctx);
@@ -122,7 +128,8 @@ uint16_t tcpck_update16(uint16_t checksum, uint16_t old_word, uint16_t new_word,
  * Fixed stride: image k is d_arena[k*stride, k*stride + len).
  * d_arena even (the u16 words of an image sit at even addresses, as in any
  * malloc'd TcpPacket buffer); stride and len even (stride >= len); count images.
- * d_out: u16[count] (CHECKSUM/FILL) or u8[count] (VERIFY).
+ * d_out: u16[count] (CHECKSUM/FILL) or u8[count] (VERIFY); FILL takes NULL
+ * (the results then go to the context's scratch, see tcpck_ctx_create).
  * Asynchronous on `stream`; nothing is allocated; no host synchronisation. */
 int tcpck_batch_fixed(tcpck_ctx *ctx, int op, int mode, void *d_arena,
                       uint64_t stride, uint32_t len, uint64_t count, void *d_out,

@@ -139,6 +139,8 @@ for s in ${STEPS:-tests smoke bench prof}; do
     wtprobe) step segwt 600 python scripts/segment_probe.py --params 0,64,128 --cases 1460:1504,1024:1056 &&
       step gswt 600 python scripts/gstream_probe.py --ops fill --lengths 32,64,128 --gs 0x401,0x801,0xC01 ;;
     rtests) step rtests 900 python -u -m pytest tests/test_gpu_receive.py tests/test_gpu_rfc_long.py -x -q --timeout 300 --timeout-method thread ;;
+    fmall) step fmall 300 python scripts/fill_mall_probe.py &&
+      step fmall_trace 300 rocprofv3 --kernel-trace --stats -d gpurun_out/fmall_trace -o run --output-format csv -- python3 scripts/fill_mall_probe.py ;;
     rorder) step rorder 300 python scripts/receive_fused_probe.py --order ;;
     prof_fill_c3) step prof_fill_c3 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_fill_c3 -o run --output-format csv -- python3 bench.py --config fill_c3 --steps 10 --warmup 2 --no-cpu-baseline --no-e2e ;;
     new4) step new4 900 python -u -m pytest tests/test_gpu_full_paths.py -x -v --timeout 300 --timeout-method thread ;;

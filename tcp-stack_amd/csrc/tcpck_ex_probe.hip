@@ -4,7 +4,9 @@
 // Built only into the probe library, in place of tcpck_ex.hip: the product
 // router (tcpck::api, tcpck_api.hip) with the measurement hooks switched on,
 // so that the router itself carries no probe switches.
-//   * tcpck_batch_fixed_ex: also TCPCK_KERNEL_PATCH, FILL's field pass alone;
+//   * tcpck_batch_fixed_ex: also TCPCK_KERNEL_PATCH, FILL's field pass alone,
+//     and RSTREAM 29 / 30, FILL's deferred stream alone (29: the field blocks
+//     read with the default cache policy);
 //   * tcpck_batch_receive_ex: with an explicit kernel, the headers fused into
 //     any kernel that can (sstream's after-the-verdicts conversion, HDR 1);
 //   * tcpck_probe_receive_ex: the header pass forms (TCPCK_PROBE_RECEIVE_*);
@@ -80,6 +82,25 @@ int tcpck_batch_fixed_ex(tcpck_ctx *ctx, int op, int mode, void *d_arena, uint64
     pa.store_bits = static_cast<uint32_t>(param & 0xFF);  // 1 + sc0 1 | nt 2 | sc1 4 (0 = plain) | form << 4
     return hip_status(tcpck::launch_patch_fields(pa, static_cast<uint32_t>(ctx->num_cus),
                                                  static_cast<hipStream_t>(stream)));
+  }
+  if (kernel == TCPCK_KERNEL_RSTREAM && ((param & 0xFF) == 29 || (param & 0xFF) == 30)) {
+    // FILL's deferred stream ALONE (timing): results to d_out, the fields left
+    // for a TCPCK_KERNEL_PATCH pass the caller times separately
+    if (!ctx || op != TCPCK_OP_FILL || mode != TCPCK_MODE_REF || !d_arena || !d_out || count == 0 || stride != len ||
+        len < 64)
+      return TCPCK_EINVAL;
+    DeviceGuard g(ctx->device);
+    if (g.status() != hipSuccess) return hip_status(g.status());
+    tcpck::FixedStreamArgs a{};
+    a.mode = tcpck::kRef;
+    a.arena = static_cast<uint8_t *>(d_arena);
+    a.stride = stride;
+    a.count = count;
+    a.out = d_out;
+    a.order = 0xFFu;
+    a.defer_field = 1;
+    return hip_status(tcpck::launch_rstream(tcpck::kFill, param & 0xFF, a, static_cast<uint32_t>(ctx->num_cus),
+                                            static_cast<hipStream_t>(stream)));
   }
   return tcpck::api::batch_fixed_ex(ctx, op, mode, d_arena, stride, len, count, d_out, kernel, param,
                                     static_cast<hipStream_t>(stream), probe_hooks(0));

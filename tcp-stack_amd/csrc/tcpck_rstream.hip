@@ -55,6 +55,10 @@ using dev::u32x4;
 // from the stream's own registers with the checksum in place, write-through
 // (sc0 sc1 nt) -- a whole-block store needs no read-modify-write of the line,
 // a 2-B store does (scripts/fill_drain_probe.py, profiles/r03/fill_blind.log);
+// bit 7 (kFill, probe): the chunks of each field's 64-B block read with the
+// default cache policy (the rest nt), so a field pass after the stream finds
+// the block in the caches (the memory-side Infinity Cache holds C2's 1M field
+// lines: 128 MB) and can write it back whole without reading HBM;
 // a.order (runtime): the block order, dev::ordered_block -- with the XCD
 // orders each XCD streams compact regions instead of every eighth run
 // (measured +4% at C2; the HBM bytes do not change), and
@@ -109,8 +113,24 @@ __global__ void __launch_bounds__(kBlock) rstream_kernel(FixedStreamArgs a) {
 
   // buffer flavour: records cover whole chunks of the run; steps past it read 0
   const auto rsrc = dev::make_rsrc(base, (last_chunk + 1) << 4);
+  // FLAV bit 7: the next field whose block the load walk has not yet passed
+  // (steps are loaded in order, so one scalar walker serves every load)
+  uint32_t nl = lead + 28;
   auto load_step = [&](uint32_t st) -> u32x4 {
-    if constexpr (FLAV & 2) {
+    if constexpr ((FLAV & 128) != 0 && OP == kFill) {
+      const uint32_t sb = st << 10;
+      uint64_t m = 0;  // lanes holding a chunk of a field block of this step
+      while (nl < sb + 1024 && nl < span) {
+        m |= uint64_t{0xF} << (((nl & ~63u) - sb) >> 4);  // blocks are 64-B aligned inside the 1-KiB step
+        nl += S;
+      }
+      if ((m >> lane) & 1u) {
+        typedef unsigned v4u __attribute__((ext_vector_type(4)));
+        const v4u v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, static_cast<int>(lane << 4), static_cast<int>(sb), 0);
+        return u32x4{v.x, v.y, v.z, v.w};
+      }
+      return dev::load16_buf_nt(rsrc, lane << 4, sb);
+    } else if constexpr (FLAV & 2) {
       if constexpr (FLAV & 8) {  // default cache policy for every step (FILL: the field's line stays in L2)
         typedef unsigned v4u __attribute__((ext_vector_type(4)));
         const v4u v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, static_cast<int>(lane << 4), static_cast<int>(st << 10), 0);
@@ -386,6 +406,14 @@ hipError_t launch_rstream(int op, int variant, const FixedStreamArgs &a, uint32_
       FixedStreamArgs b = a;
       b.order = 4u;
       return dispatch<4, false, 0, 103>(op, b, num_cus, stream);
+    }
+    case 29: case 30: {  // FILL's deferred stream alone (a.defer_field): 29 with the field blocks read
+                         // with the default policy (FLAV bit 7), 30 the policy's stream (timing)
+      if (op != kFill || !a.defer_field || a.stride < 64) return hipErrorInvalidValue;
+      FixedStreamArgs b = a;
+      b.order = 4u;
+      return variant == 29 ? launch_one<4, kFill, false, 0, 135>(b, num_cus, stream)
+                           : launch_one<4, kFill, false, 0, 7>(b, num_cus, stream);
     }
     case 26: {  // 20 with the FILL field stores write-through streaming (sc0 sc1 nt, FLAV bit 4)
       FixedStreamArgs b = a;
