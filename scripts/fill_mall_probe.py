@@ -21,6 +21,8 @@ rounds of 20 steps after a settle):
               0x05 sc1, 0x07 sc1 nt... 0x08 sc0 sc1 nt)
   s30+p08     control: the block pass without the default-policy reads
   s29 / s30 / checksum   the streams alone
+  .../C       the same over the batch in C pieces, each piece's pass right
+              after its stream (the pieces' field lines fit the caches)
 
 Every FILL sequence's arena is compared with AUTO's."""
 import os
@@ -63,11 +65,19 @@ def main():
     R, P = tcpck.KERNEL_RSTREAM, tcpck.KERNEL_PATCH
     algo = n * L + 4 * n  # image bytes + fields + results
 
-    def seq(stream_v, patch_p):
+    def seq(stream_v, patch_p, chunks=1):
+        """The stream then the pass, over the batch in `chunks` pieces (each
+        piece's pass right after its stream: its blocks read at most 1/chunks
+        of the batch ago)."""
+        m = n // chunks
+        a0, o0 = arena.data_ptr(), out.data_ptr()
+
         def f():
-            ctx.batch_fixed_ex(tcpck.OP_FILL, arena, L, L, n, out, R, stream_v, stream=s)
-            if patch_p is not None:
-                ctx.batch_fixed_ex(tcpck.OP_FILL, arena, L, L, n, out, P, patch_p, stream=s)
+            for c in range(chunks):
+                a, o = a0 + c * m * L, o0 + 2 * c * m
+                ctx.batch_fixed_ex(tcpck.OP_FILL, a, L, L, m, o, R, stream_v, stream=s)
+                if patch_p is not None:
+                    ctx.batch_fixed_ex(tcpck.OP_FILL, a, L, L, m, o, P, patch_p, stream=s)
         return f
 
     ctx.batch_fixed(tcpck.OP_FILL, arena, L, L, n, out, stream=s)
@@ -78,6 +88,8 @@ def main():
              ("s29+p08", seq(29, 0x08), True), ("s29+p00", seq(29, 0x00), True), ("s29+p03", seq(29, 0x03), True),
              ("s29+p05", seq(29, 0x05), True), ("s29+p07", seq(29, 0x07), True), ("s30+p08", seq(30, 0x08), True),
              ("s30+p00", seq(30, 0x00), True),
+             ("s29+p08/4", seq(29, 0x08, 4), True), ("s29+p08/8", seq(29, 0x08, 8), True),
+             ("s30+p28/8", seq(30, 0x28, 8), True), ("s29+p28/8", seq(29, 0x28, 8), True),
              ("s29", seq(29, None), False), ("s30", seq(30, None), False),
              ("checksum", lambda: ctx.batch_fixed(tcpck.OP_CHECKSUM, arena, L, L, n, out, stream=s), False),
              ("auto", lambda: ctx.batch_fixed(tcpck.OP_FILL, arena, L, L, n, out, stream=s), True)]

@@ -214,6 +214,39 @@ def test_fill_noout_var_chunks_past_scratch(ctx, oracle_c, packed):
     np.testing.assert_array_equal(host(a), want)
 
 
+@pytest.mark.parametrize("count", [1, 2, 3, 65, 4097])
+@pytest.mark.parametrize("length", [30, 96, 1492, 9000, 65536])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_fill_noout_small_batches(ctx, oracle_c, count, length, mode):
+    """out=None on tiny and odd-sized batches through every AUTO route (fixed
+    packed, and the same bytes as a packed offset list): arena byte-exact."""
+    import tcpck
+    rng = np.random.default_rng(count * 7 + length + mode)
+    a_h = rng.integers(0, 256, count * length + 2, dtype=np.uint8)[2:]  # (an even, not 16-B aligned start)
+    offs = np.arange(count, dtype=np.int64) * length
+    want = expected_fill(a_h, offs, np.full(count, length), oracle_c, mode)
+    buf = dev(a_h)
+    ctx.batch_fixed(tcpck.OP_FILL, buf, length, length, count, None, mode=mode)
+    np.testing.assert_array_equal(host(buf), want)
+    buf = dev(a_h)
+    ln = np.full(count, length, np.uint32)
+    ctx.batch_var(tcpck.OP_FILL, buf, dev(offs.astype(np.uint64)), dev(ln), count, None, mode=mode,
+                  total_bytes=count * length, min_len=length, max_len=length, packed=True)
+    np.testing.assert_array_equal(host(buf), want)
+
+
+def test_fill_noout_explicit_kernel_stays_in_stream(ctx, oracle_c):
+    """The scratch is AUTO's: an explicit kernel with out=None keeps its own
+    in-stream form (tcpck_tuning.h) -- the same arena either way."""
+    import tcpck
+    count, L = 4096, 1492
+    a = torch.empty(count * L, dtype=torch.uint8, device="cuda")
+    tcpck.synth_fixed(a, L, L, count, seed=49)
+    want = expected_fill(host(a), np.arange(count, dtype=np.int64) * L, np.full(count, L), oracle_c)
+    ctx.batch_fixed_ex(tcpck.OP_FILL, a, L, L, count, None, tcpck.KERNEL_RSTREAM, 20)
+    np.testing.assert_array_equal(host(a), want)
+
+
 def test_fill_noout_two_streams_in_turn(ctx, oracle_c):
     """The scratch shared by FILLs on two streams (each waits for the other's
     last use): both arenas byte-exact."""
