@@ -112,6 +112,10 @@ def test_fuzz_fixed(ctx, oracle_c, seed):
         exp_arena = check_fill(view, offs, lens, mode, run)
         np.testing.assert_array_equal(host(buf)[mis:], exp_arena, err_msg=f"{stride}/{length}x{count} fill arena")
         np.testing.assert_array_equal(host(buf)[:mis], arena_np[:mis])
+        # the reference's call shape: no results buffer (the context's scratch)
+        buf.copy_(dev(arena_np))
+        ctx.batch_fixed(tcpck.OP_FILL, ptr, stride, length, count, None, mode=mode)
+        np.testing.assert_array_equal(host(buf)[mis:], exp_arena, err_msg=f"{stride}/{length}x{count} fill, no out")
     if length >= 32 and mis % 2 == 0:
         check_receive(ctx, arena_np, mis, np.arange(count, dtype=np.int64) * stride, np.full(count, length, np.uint32),
                       mode, seed, dict(stride=stride, length=length))
@@ -175,6 +179,9 @@ def test_fuzz_var(ctx, oracle_c, seed):
             return host(out).view(np.uint16)
         exp_arena = check_fill(view, off, ln, mode, run)
         np.testing.assert_array_equal(host(buf)[mis:], exp_arena, err_msg=f"{kind}/{dist} fill arena")
+        buf.copy_(dev(arena_np))  # again with no results buffer (the context's scratch)
+        ctx.batch_var(tcpck.OP_FILL, ptr, d_off, d_ln, count, None, mode=mode, **hints)
+        np.testing.assert_array_equal(host(buf)[mis:], exp_arena, err_msg=f"{kind}/{dist} fill arena, no out")
     if ln.min() >= 32 and kind != "unordered":  # RECEIVE's in-place headers must not overlap
         check_receive(ctx, arena_np, mis, off.astype(np.int64), ln, mode, seed,
                       dict(offsets=d_off, lengths=d_ln, **hints))
