@@ -14,6 +14,9 @@ step() {  # step <name> <timeout> <cmd...>
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "fatal rc=$rc, stopping"; exit $rc; fi
   return 0
 }
+if [[ " ${STEPS:-} " == *" pmc_all "* ]]; then  # every bench key's two PMC passes, in bench order
+  STEPS="${STEPS/pmc_all/pmc_c2 pmc_c5 pmc_fill pmc_fill_noout pmc_c2_rfc pmc_slots pmc_receive pmc_segment pmc_c3 pmc_fill_c3 pmc_c4}"
+fi
 for s in ${STEPS:-tests smoke bench prof}; do
   case $s in
     tests) step pytest 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ;;
@@ -119,7 +122,7 @@ for s in ${STEPS:-tests smoke bench prof}; do
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-e2e --no-extras ;;
     prof_all)  # the driver's default bench command (C2 + the c3 / c4 / c5_strong keys) under the kernel trace
       step prof_all 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_all -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-e2e &&
-      python3 scripts/bench_trace_summary.py gpurun_out/prof_all/run_kernel_trace.csv --last 20 --names c2,c5_strong,fill,slots,receive,segment,c3,c4 > gpurun_out/prof_all_summary.txt ;;
+      python3 scripts/bench_trace_summary.py gpurun_out/prof_all/run_kernel_trace.csv --last 20 --names c2,c5_strong,fill,fill_noout,c2_rfc,slots,receive,segment,c3,fill_c3,c4 > gpurun_out/prof_all_summary.txt ;;
     fdrain) step fdrain 300 rocprofv3 --kernel-trace -d gpurun_out/fdrain -o run --output-format csv -- python3 scripts/fill_drain_probe.py &&
       step fdrain_w 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d gpurun_out/fdrain_w -o run --output-format csv -- python3 scripts/fill_drain_probe.py --phases stream,fill,patch,instream --steps 10 &&
       step fdrain_f 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d gpurun_out/fdrain_f -o run --output-format csv -- python3 scripts/fill_drain_probe.py --phases stream,fill,patch,instream --steps 10 ;;
