@@ -106,8 +106,8 @@ int tcpck_device_supported(int device);
  * (TCPCK_ENOMEM if it cannot): a FILL without a results buffer writes its
  * results there, 8M images per launch chunk, so the reference's call shape
  * (socket-manager.cc:9-10 stores into the packet only) runs the same two-pass
- * forms as a FILL with one.  Such FILLs are serialised per context; one on
- * another stream than the scratch's last user first waits for that user. */
+ * forms as a FILL with one.  Such FILLs are serialised per context: each
+ * waits (on its stream, asynchronously) for the previous one's work. */
 int tcpck_ctx_create(int device, tcpck_ctx **out);
 int tcpck_ctx_destroy(tcpck_ctx *ctx);
 int tcpck_ctx_device(const tcpck_ctx *ctx);

@@ -739,20 +739,19 @@ bool use_scratch(const tcpck_ctx *ctx, int op, const void *out, int kernel) {
 }
 
 // launch(k0, n, results) for images [k0, k0 + n), n <= scratch_images.  Calls
-// are serialised per ctx; a stream other than the scratch's last user first
-// waits for that user's work (the event recorded after every use).
+// are serialised per ctx, and each first waits for the previous use's event
+// (recorded after every use): always, not only when the stream differs -- a
+// destroyed stream's handle can come back for a new stream while the old one's
+// work still runs.
 template <typename Launch>
 hipError_t with_scratch(tcpck_ctx *ctx, uint64_t count, hipStream_t s, Launch launch) {
   std::lock_guard<std::mutex> lk(ctx->scratch_mu);
   hipError_t e = hipSuccess;
-  if (ctx->scratch_used && ctx->scratch_last != s) e = hipStreamWaitEvent(s, ctx->scratch_ev, 0);
+  if (ctx->scratch_used) e = hipStreamWaitEvent(s, ctx->scratch_ev, 0);
   for (uint64_t k0 = 0; k0 < count && e == hipSuccess; k0 += ctx->scratch_images)
     e = launch(k0, std::min(ctx->scratch_images, count - k0), ctx->scratch);
   const hipError_t er = hipEventRecord(ctx->scratch_ev, s);
-  if (er == hipSuccess) {
-    ctx->scratch_used = true;
-    ctx->scratch_last = s;
-  }
+  if (er == hipSuccess) ctx->scratch_used = true;
   return e != hipSuccess ? e : er;
 }
 

@@ -35,13 +35,12 @@ struct tcpck_ctx {
   // packet, socket-manager.cc:9-10): the results go to this ctx-owned scratch,
   // allocated at tcpck_ctx_create, so AUTO keeps its two-pass forms (the stream
   // writes the results, the write-through field pass stores them).  Batches of
-  // more images run in chunks.  `scratch_ev` is recorded after every use; a
-  // call on another stream than the last user's waits for it first.
+  // more images run in chunks.  `scratch_ev` is recorded after every use and
+  // every later use waits for it first.
   std::mutex scratch_mu;
   uint16_t *scratch = nullptr;
   uint64_t scratch_images = 0;
   hipEvent_t scratch_ev = nullptr;
-  hipStream_t scratch_last = nullptr;
   bool scratch_used = false;
 
   // probe library only (tcpck_ex_probe.hip): per-wave time stamp buffer, and the
