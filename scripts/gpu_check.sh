@@ -146,6 +146,7 @@ for s in ${STEPS:-tests smoke bench prof}; do
       step fmall_trace 300 rocprofv3 --kernel-trace --stats -d gpurun_out/fmall_trace -o run --output-format csv -- python3 scripts/fill_mall_probe.py ;;
     fuzzlong) step fuzzlong 900 env TCPCK_FUZZ_BASE=200000 TCPCK_FUZZ_SEEDS=1500 python -u -m pytest tests/test_gpu_fuzz.py -x -q --timeout 300 --timeout-method thread ;;
     bench_fill_noout) step bench_fill_noout 300 python bench.py --config fill_noout ;;
+    copysize) step copysize 300 python scripts/copy_size_probe.py ;;
     rorder) step rorder 300 python scripts/receive_fused_probe.py --order ;;
     prof_fill_c3) step prof_fill_c3 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_fill_c3 -o run --output-format csv -- python3 bench.py --config fill_c3 --steps 10 --warmup 2 --no-cpu-baseline --no-e2e ;;
     new4) step new4 900 python -u -m pytest tests/test_gpu_full_paths.py -x -v --timeout 300 --timeout-method thread ;;
