@@ -261,20 +261,16 @@ struct CallerBits {
       : two_pass((param & TCPCK_PARAM_RECEIVE_TWO_PASS) != 0), instream((param & TCPCK_PARAM_FILL_INSTREAM) != 0) {}
 };
 
-hipError_t run_fixed_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t stride, uint32_t len,
-                          uint64_t count, void *out, int kernel, int param, hipStream_t s, bool *patch,
-                          const Hooks &hk, uint8_t *hdr = nullptr, bool *hdr_done = nullptr) {
-  const uint32_t num_cus = static_cast<uint32_t>(ctx->num_cus);
-  const bool auto_pick = kernel == TCPCK_KERNEL_AUTO;
-  const CallerBits caller(param);
-  if (kernel == TCPCK_KERNEL_AUTO && mode == TCPCK_MODE_RFC1071 && stride == len && len >= 512 &&
-      len <= kFixedRunMaxLen) {
+// AUTO's kernel for a fixed layout: sets kernel (from TCPCK_KERNEL_AUTO) and
+// its param (measurements in DESIGN.md section 4).
+void pick_fixed(int op, int mode, const uint8_t *arena, uint64_t stride, uint32_t len, int &kernel, int &param) {
+  if (mode == TCPCK_MODE_RFC1071 && stride == len && len >= 512 && len <= kFixedRunMaxLen) {
     // RFC 1071 on packed fixed images: rstream's prefix is an exact u32 word
     // sum, so its image differences fold like any sum (C2 in RFC 1071 mode at
     // the REF rate instead of seg's; profiles/r02/rfc_probe.log)
     kernel = TCPCK_KERNEL_RSTREAM;
     param = kRstreamPolicy;
-  } else if (kernel == TCPCK_KERNEL_AUTO && mode == TCPCK_MODE_RFC1071 && stride == len && len >= 2 && len < 512 &&
+  } else if (mode == TCPCK_MODE_RFC1071 && stride == len && len >= 2 && len < 512 &&
              (op != TCPCK_OP_FILL || len >= 30)) {
     // RFC 1071 on small packed images: vvstream's fixed mode with exact u32 prefix tables
     kernel = TCPCK_KERNEL_VVSTREAM;
@@ -360,6 +356,15 @@ hipError_t run_fixed_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint
       param = kRstreamPolicy;
     }
   }
+}
+
+hipError_t run_fixed_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t stride, uint32_t len,
+                          uint64_t count, void *out, int kernel, int param, hipStream_t s, bool *patch,
+                          const Hooks &hk, uint8_t *hdr = nullptr, bool *hdr_done = nullptr) {
+  const uint32_t num_cus = static_cast<uint32_t>(ctx->num_cus);
+  const bool auto_pick = kernel == TCPCK_KERNEL_AUTO;
+  const CallerBits caller(param);
+  if (auto_pick) pick_fixed(op, mode, arena, stride, len, kernel, param);
   // RECEIVE into a header array: for small images in slots sstream emits each
   // host-order header from the stream's registers (one launch, the header
   // bytes read once); elsewhere the header pass follows the VERIFY pass, which
@@ -535,15 +540,13 @@ hipError_t run_fixed_r(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_
   return tcpck::launch_header_swap(h, static_cast<uint32_t>(ctx->num_cus), s);
 }
 
-hipError_t run_var_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const uint64_t *off, const uint32_t *len,
-                        uint64_t base, uint64_t count, void *out, const tcpck_layout *layout, int kernel, int param,
-                        hipStream_t s, const Hooks &hk, uint8_t *hdr = nullptr, bool *hdr_done = nullptr,
-                        bool *patch = nullptr) {
+// AUTO's kernel for an offset list: sets kernel (from TCPCK_KERNEL_AUTO) and
+// its param; fuse_small: RECEIVE into a header array on a ring of small
+// datagrams, the headers from sstream's registers (below).
+void pick_var(int op, int mode, const tcpck_layout *layout, uint64_t count, bool hdr, bool two_pass, int &kernel,
+              int &param, bool &fuse_small) {
   const uint64_t typical = (layout && layout->total_bytes) ? layout->total_bytes / count : 1500;
   const bool packed = mode == TCPCK_MODE_REF && layout && (layout->flags & TCPCK_LAYOUT_PACKED);
-  bool fuse_small = false;  // RECEIVE into a header array on a ring of small datagrams (below)
-  const bool auto_pick = kernel == TCPCK_KERNEL_AUTO;
-  const CallerBits caller(param);
   // packed, reference mode: vvstream for every op (any image lengths; C3 89.1%
   // at 32x oversubscription, profiles/r01/c3_bench_r01_final.log).  The
   // packed flag must be true when set (tcpck.h); a wave whose lengths do not
@@ -573,7 +576,7 @@ hipError_t run_var_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const 
       // (41-58 % either way: the scattered field writes bound it)
       kernel = TCPCK_KERNEL_SSTREAM;
       param = 0;
-      if (op == TCPCK_OP_RECEIVE && hdr && typical <= kHdrStreamMaxLen && !caller.two_pass) {
+      if (op == TCPCK_OP_RECEIVE && hdr && typical <= kHdrStreamMaxLen && !two_pass) {
         fuse_small = true;
         param = kSstreamHdrStream;
       }
@@ -586,6 +589,17 @@ hipError_t run_var_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const 
       param = kVvPolicy | (op == TCPCK_OP_FILL && typical <= kFillKeepMaxLen ? kVvKeep : 0);
     }
   }
+}
+
+hipError_t run_var_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const uint64_t *off, const uint32_t *len,
+                        uint64_t base, uint64_t count, void *out, const tcpck_layout *layout, int kernel, int param,
+                        hipStream_t s, const Hooks &hk, uint8_t *hdr = nullptr, bool *hdr_done = nullptr,
+                        bool *patch = nullptr) {
+  const uint64_t typical = (layout && layout->total_bytes) ? layout->total_bytes / count : 1500;
+  bool fuse_small = false;  // RECEIVE into a header array on a ring of small datagrams (pick_var)
+  const bool auto_pick = kernel == TCPCK_KERNEL_AUTO;
+  const CallerBits caller(param);
+  if (auto_pick) pick_var(op, mode, layout, count, hdr != nullptr, caller.two_pass, kernel, param, fuse_small);
   // RECEIVE into a header array (as run_fixed_impl): on rings of small images
   // sstream emits the headers from its stream (4M 32-254-B datagrams in 256-B
   // slots: 190 us against 259 with the header pass, 235 with the run's
@@ -805,6 +819,58 @@ int batch_var_ex(tcpck_ctx *ctx, int op, int mode, void *d_arena, const uint64_t
                             nullptr, hk));
 }
 
+namespace {
+
+// RECEIVE into a header array where AUTO's VERIFY is the slot stream and its
+// header pass would follow (MSS-sized rings and slots): the stream sums each
+// image's tail only -- bytes [128, len), SSArgs::skip / a shifted fixed arena
+// -- into the ctx scratch (CHECKSUM), and the header pass, which reads every
+// image's first line anyway, sums the head, combines the two into the verdict
+// and converts the header (launch_header_combine).  VERIFY + the extract pass
+// read each image's first line twice; this reads it once.
+hipError_t receive_combined(tcpck_ctx *ctx, int mode, uint8_t *arena, uint64_t stride, uint32_t len,
+                            const uint64_t *off, const uint32_t *lens, uint64_t count, uint8_t *ok, uint8_t *hdr,
+                            const tcpck_layout *layout, hipStream_t s) {
+  const uint32_t num_cus = static_cast<uint32_t>(ctx->num_cus);
+  return with_scratch(ctx, count, s, [&](uint64_t k0, uint64_t n, uint16_t *res) {
+    tcpck::RunArgs r{};
+    r.mode = mode == TCPCK_MODE_REF ? tcpck::kRef : tcpck::kRfc1071;
+    r.count = n;
+    r.out = res;
+    tcpck::CombineArgs c{};
+    c.count = n;
+    c.tail = res;
+    c.ok = ok + k0;
+    c.hdr = hdr + 32 * k0;
+    c.mode = r.mode;
+    hipError_t e;
+    if (off) {
+      r.arena = arena;
+      r.offsets = off + k0;
+      r.lengths = lens + k0;
+      const uint64_t bytes =
+          layout ? static_cast<uint64_t>(static_cast<unsigned __int128>(layout->total_bytes) * n / count) : 0;
+      r.total_bytes = bytes > 2 * tcpck::kHeadBytes * n ? bytes - tcpck::kHeadBytes * n : 0;  // the tails' bytes
+      r.skip = tcpck::kHeadBytes;
+      e = tcpck::launch_sstream(tcpck::kChecksum, 0, false, r, num_cus, s);
+      c.arena = arena;
+      c.offsets = off + k0;
+      c.lengths = lens + k0;
+    } else {
+      r.arena = arena + k0 * stride + tcpck::kHeadBytes;
+      r.len = len - tcpck::kHeadBytes;
+      r.stride = n == 1 ? (static_cast<uint64_t>(r.len) + 15) & ~uint64_t{15} : stride;  // one image: never read
+      e = tcpck::launch_sstream(tcpck::kChecksum, 0, true, r, num_cus, s);
+      c.arena = arena + k0 * stride;
+      c.stride = stride;
+      c.len = len;
+    }
+    return e != hipSuccess ? e : tcpck::launch_header_combine(c, num_cus, s);
+  });
+}
+
+}  // namespace
+
 int check_receive(const tcpck_ctx *ctx, int mode, const void *d_arena, uint64_t &stride, uint32_t len,
                   const uint64_t *d_offsets, const uint32_t *d_lengths, uint64_t count, const uint8_t *d_ok,
                   const void *d_hdr) {
@@ -839,6 +905,21 @@ int batch_receive_ex(tcpck_ctx *ctx, int mode, void *d_arena, uint64_t stride, u
   if (g.status() != hipSuccess) return hip_status(g.status());
   auto *arena = static_cast<uint8_t *>(d_arena);
   auto *hdr = static_cast<uint8_t *>(d_hdr);
+  if (kernel == TCPCK_KERNEL_AUTO && !(param & TCPCK_PARAM_RECEIVE_TWO_PASS) && ctx->scratch) {
+    // AUTO's VERIFY kernel; the slot stream without its register-header form -> the combined form
+    int k = TCPCK_KERNEL_AUTO, p = 0;
+    bool fused = false, combined;
+    if (d_offsets) {
+      pick_var(TCPCK_OP_RECEIVE, mode, layout, count, true, false, k, p, fused);
+      combined = k == TCPCK_KERNEL_SSTREAM && !fused;
+    } else {
+      pick_fixed(TCPCK_OP_RECEIVE, mode, arena, stride, len, k, p);
+      combined = k == TCPCK_KERNEL_SSTREAM && len > kHdrStreamMaxLen;
+    }
+    if (combined)
+      return hip_status(receive_combined(ctx, mode, arena, stride, len, d_offsets, d_lengths, count, d_ok, hdr, layout,
+                                         s));
+  }
   return hip_status(d_offsets ? run_var(ctx, TCPCK_OP_RECEIVE, mode, arena, d_offsets, d_lengths, 0, count, d_ok,
                                         layout, kernel, param, s, hdr, hk)
                               : run_fixed(ctx, TCPCK_OP_RECEIVE, mode, arena, stride, len, count, d_ok, kernel,
