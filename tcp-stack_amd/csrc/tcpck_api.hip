@@ -325,9 +325,11 @@ void pick_fixed(int op, int mode, const uint8_t *arena, uint64_t stride, uint32_
         kernel = TCPCK_KERNEL_SEG;
         param = (tcpck::kShapeSmall + 1) | kSegXcdOrder;
       }
-    } else if (op == TCPCK_OP_FILL && tcpck::gstream_applies(arena, stride, len)) {
-      // send-path FILL of power-of-two images, 32 B (pure ACKs) .. 1 KiB, and
-      // of the other multiples of 16 B up to 240 B:
+    } else if (op == TCPCK_OP_FILL && len <= 512 && tcpck::gstream_applies(arena, stride, len)) {
+      // send-path FILL of power-of-two images, 32 B (pure ACKs) .. 512 B, and
+      // of the other multiples of 16 B up to 240 B (1 KiB: rstream's deferred
+      // fields since round 3's write-through field pass, 277 vs 299 us for
+      // 1.5M images; 512 B stays: 345 vs 406 us, profiles/r04/fill_line_probe.log):
       // gstream; up to 256 B every line holds a checksum field, and reading
       // the lines with the default cache policy keeps them in L2 until the
       // field store lands, so they leave as whole lines rather than masked
@@ -819,58 +821,6 @@ int batch_var_ex(tcpck_ctx *ctx, int op, int mode, void *d_arena, const uint64_t
                             nullptr, hk));
 }
 
-namespace {
-
-// RECEIVE into a header array where AUTO's VERIFY is the slot stream and its
-// header pass would follow (MSS-sized rings and slots): the stream sums each
-// image's tail only -- bytes [128, len), SSArgs::skip / a shifted fixed arena
-// -- into the ctx scratch (CHECKSUM), and the header pass, which reads every
-// image's first line anyway, sums the head, combines the two into the verdict
-// and converts the header (launch_header_combine).  VERIFY + the extract pass
-// read each image's first line twice; this reads it once.
-hipError_t receive_combined(tcpck_ctx *ctx, int mode, uint8_t *arena, uint64_t stride, uint32_t len,
-                            const uint64_t *off, const uint32_t *lens, uint64_t count, uint8_t *ok, uint8_t *hdr,
-                            const tcpck_layout *layout, hipStream_t s) {
-  const uint32_t num_cus = static_cast<uint32_t>(ctx->num_cus);
-  return with_scratch(ctx, count, s, [&](uint64_t k0, uint64_t n, uint16_t *res) {
-    tcpck::RunArgs r{};
-    r.mode = mode == TCPCK_MODE_REF ? tcpck::kRef : tcpck::kRfc1071;
-    r.count = n;
-    r.out = res;
-    tcpck::CombineArgs c{};
-    c.count = n;
-    c.tail = res;
-    c.ok = ok + k0;
-    c.hdr = hdr + 32 * k0;
-    c.mode = r.mode;
-    hipError_t e;
-    if (off) {
-      r.arena = arena;
-      r.offsets = off + k0;
-      r.lengths = lens + k0;
-      const uint64_t bytes =
-          layout ? static_cast<uint64_t>(static_cast<unsigned __int128>(layout->total_bytes) * n / count) : 0;
-      r.total_bytes = bytes > 2 * tcpck::kHeadBytes * n ? bytes - tcpck::kHeadBytes * n : 0;  // the tails' bytes
-      r.skip = tcpck::kHeadBytes;
-      e = tcpck::launch_sstream(tcpck::kChecksum, 0, false, r, num_cus, s);
-      c.arena = arena;
-      c.offsets = off + k0;
-      c.lengths = lens + k0;
-    } else {
-      r.arena = arena + k0 * stride + tcpck::kHeadBytes;
-      r.len = len - tcpck::kHeadBytes;
-      r.stride = n == 1 ? (static_cast<uint64_t>(r.len) + 15) & ~uint64_t{15} : stride;  // one image: never read
-      e = tcpck::launch_sstream(tcpck::kChecksum, 0, true, r, num_cus, s);
-      c.arena = arena + k0 * stride;
-      c.stride = stride;
-      c.len = len;
-    }
-    return e != hipSuccess ? e : tcpck::launch_header_combine(c, num_cus, s);
-  });
-}
-
-}  // namespace
-
 int check_receive(const tcpck_ctx *ctx, int mode, const void *d_arena, uint64_t &stride, uint32_t len,
                   const uint64_t *d_offsets, const uint32_t *d_lengths, uint64_t count, const uint8_t *d_ok,
                   const void *d_hdr) {
@@ -905,21 +855,6 @@ int batch_receive_ex(tcpck_ctx *ctx, int mode, void *d_arena, uint64_t stride, u
   if (g.status() != hipSuccess) return hip_status(g.status());
   auto *arena = static_cast<uint8_t *>(d_arena);
   auto *hdr = static_cast<uint8_t *>(d_hdr);
-  if (kernel == TCPCK_KERNEL_AUTO && !(param & TCPCK_PARAM_RECEIVE_TWO_PASS) && ctx->scratch) {
-    // AUTO's VERIFY kernel; the slot stream without its register-header form -> the combined form
-    int k = TCPCK_KERNEL_AUTO, p = 0;
-    bool fused = false, combined;
-    if (d_offsets) {
-      pick_var(TCPCK_OP_RECEIVE, mode, layout, count, true, false, k, p, fused);
-      combined = k == TCPCK_KERNEL_SSTREAM && !fused;
-    } else {
-      pick_fixed(TCPCK_OP_RECEIVE, mode, arena, stride, len, k, p);
-      combined = k == TCPCK_KERNEL_SSTREAM && len > kHdrStreamMaxLen;
-    }
-    if (combined)
-      return hip_status(receive_combined(ctx, mode, arena, stride, len, d_offsets, d_lengths, count, d_ok, hdr, layout,
-                                         s));
-  }
   return hip_status(d_offsets ? run_var(ctx, TCPCK_OP_RECEIVE, mode, arena, d_offsets, d_lengths, 0, count, d_ok,
                                         layout, kernel, param, s, hdr, hk)
                               : run_fixed(ctx, TCPCK_OP_RECEIVE, mode, arena, stride, len, count, d_ok, kernel,

@@ -185,68 +185,6 @@ hipError_t launch_one(const HeaderArgs &a, uint32_t num_cus, hipStream_t s) {
   return hipGetLastError();
 }
 
-// ---- RECEIVE's combined form: head sums + verdicts + headers (CombineArgs) ----
-//
-// Eight lanes per image, lane g holding bytes [16 g, 16 g + 16) of the image's
-// head (its first min(len, 128) bytes): one 16-B load when the image is 16-B
-// aligned and the chunk lies inside it, else u16 loads of the words it has.
-// The lanes' word sums (exact u32) meet by xor-shuffles inside the 8-lane
-// group; lane 0 adds the tail's folded sum and stores the verdict, lanes 0 and
-// 1 the host-order header halves (as header_extract_kernel).  The pass reads
-// the same line per image as the extract pass it replaces, and the tail stream
-// before it reads one line less per image than VERIFY would.
-template <bool FIXED, int MODE>
-__global__ void __launch_bounds__(kBlock) header_combine_kernel(CombineArgs a) {
-  const uint64_t step = static_cast<uint64_t>(gridDim.x) * kBlock;
-  const bool out16 = (reinterpret_cast<uintptr_t>(a.hdr) & 15u) == 0;
-  const uint64_t n8 = a.count * 8;
-  for (uint64_t t = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x; t < n8; t += step) {
-    const uint64_t k = t >> 3;
-    const uint32_t g = static_cast<uint32_t>(t & 7);
-    const uint32_t len = FIXED ? a.len : a.lengths[k];
-    const uint32_t hl = len < kHeadBytes ? len : kHeadBytes;
-    const uint8_t *p = a.arena + (FIXED ? k * a.stride : a.offsets[k]) + 16 * g;
-    dev::u32x4 v{0u, 0u, 0u, 0u};
-    if (16 * g + 16 <= hl && (reinterpret_cast<uintptr_t>(p) & 15u) == 0) {
-      v = *reinterpret_cast<const dev::u32x4 *>(p);
-    } else if (16 * g < hl) {  // the image's last head words, or a 2-B aligned image
-      const uint16_t *q = reinterpret_cast<const uint16_t *>(p);
-      const uint32_t nw = (hl - 16 * g) >= 16 ? 8u : (hl - 16 * g) >> 1;
-      uint32_t w[8];
-#pragma unroll
-      for (uint32_t i = 0; i < 8; ++i) w[i] = i < nw ? q[i] : 0u;
-      v = dev::u32x4{w[0] | (w[1] << 16), w[2] | (w[3] << 16), w[4] | (w[5] << 16), w[6] | (w[7] << 16)};
-    }
-    uint32_t sum = (v.x & 0xFFFFu) + (v.x >> 16) + (v.y & 0xFFFFu) + (v.y >> 16) + (v.z & 0xFFFFu) + (v.z >> 16) +
-                   (v.w & 0xFFFFu) + (v.w >> 16);
-    sum = dev::group_sum<8>(sum);  // the image's head, exact (<= 64 words)
-    if (g == 0) {
-      const uint32_t tail = static_cast<uint16_t>(~a.tail[k]);  // the tail's folded sum
-      a.ok[k] = dev::finish<MODE>(sum + tail) == 0 ? 1 : 0;
-    }
-    if (g < 2) {  // TcpHeaderN2H of header bytes 16 g .. 16 g + 15 (images >= 32 B)
-      const dev::u32x4 o{dev::n2h_dword(v.x, 0x00010203u), dev::n2h_dword(v.y, 0x00010203u),
-                         dev::n2h_dword(v.z, 0x02030100u), dev::n2h_dword(v.w, g ? 0x02030100u : 0x02030001u)};
-      if (out16) {
-        reinterpret_cast<dev::u32x4 *>(a.hdr)[2 * k + g] = o;
-      } else {
-        uint32_t *d = reinterpret_cast<uint32_t *>(a.hdr) + 8 * k + 4 * g;
-        d[0] = o.x, d[1] = o.y, d[2] = o.z, d[3] = o.w;
-      }
-    }
-  }
-}
-
-template <bool FIXED, int MODE>
-hipError_t launch_combine(const CombineArgs &a, uint32_t num_cus, hipStream_t s) {
-  static const uint32_t per_cu = dev::resident_blocks_per_cu(header_combine_kernel<FIXED, MODE>);
-  uint64_t blocks = (a.count * 8 + kBlock - 1) / kBlock;
-  const uint64_t cap = static_cast<uint64_t>(per_cu) * num_cus * 8;
-  if (blocks > cap) blocks = cap;
-  hipLaunchKernelGGL((header_combine_kernel<FIXED, MODE>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0, s, a);
-  return hipGetLastError();
-}
-
 // ---- FILL's field stores after the stream (PatchArgs) ----------------------
 //
 // One lane per image stores the 2-B checksum into bytes 28-29 as a
@@ -478,13 +416,6 @@ hipError_t launch_patch_fields(const PatchArgs &a, uint32_t num_cus, hipStream_t
   }
   if (a.stride < 30) return hipErrorInvalidValue;  // every image holds a field
   return a.update ? launch_patch<false, true>(a, num_cus, stream) : launch_patch<false, false>(a, num_cus, stream);
-}
-
-hipError_t launch_header_combine(const CombineArgs &a, uint32_t num_cus, hipStream_t stream) {
-  if (a.count == 0) return hipSuccess;
-  if (!a.tail || !a.ok || !a.hdr || (!a.offsets && a.len < 32) || (a.offsets && !a.lengths)) return hipErrorInvalidValue;
-  if (a.mode == kRef) return a.offsets ? launch_combine<false, kRef>(a, num_cus, stream) : launch_combine<true, kRef>(a, num_cus, stream);
-  return a.offsets ? launch_combine<false, kRfc1071>(a, num_cus, stream) : launch_combine<true, kRfc1071>(a, num_cus, stream);
 }
 
 hipError_t launch_header_swap(const HeaderArgs &a, uint32_t num_cus, hipStream_t stream) {

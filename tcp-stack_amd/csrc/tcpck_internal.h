@@ -62,8 +62,6 @@ struct RunArgs {
   uint32_t blocks_per_cu;    // vvstream: occupancy cap (LDS padding) and grid base, 0 = by resources
   int mode;                  // vvstream: kRef or kRfc1071
   uint8_t *hdr;              // sstream VERIFY: host-order header k also to hdr + 32 k (receive)
-  uint32_t skip;             // sstream CHECKSUM on offset lists: image k's tail from byte min(len, skip)
-                             // (tcpck_batch_receive's combined form; the header pass sums the rest)
 };
 
 // Fixed stride == len for rstream (tcpck_rstream.hip).
@@ -170,29 +168,6 @@ struct HeaderArgs {
 };
 hipError_t launch_header_swap(const HeaderArgs &a, uint32_t num_cus, hipStream_t stream);
 
-// ---- RECEIVE's combined form, second pass (tcpck_header.hip) ----
-// The slot stream has summed each image's TAIL -- bytes [min(len, kHeadBytes),
-// len) -- into tail[k] (CHECKSUM results).  This pass reads each image's head
-// (its first min(len, kHeadBytes) bytes: the line its header lives in, which
-// the tail stream never reads), and writes ok[k] = (checksum of head + tail ==
-// 0) and the host-order header k to hdr + 32 k.  Exact in both modes: the
-// tail's folded sum is ~tail[k] (mod 2^16 in REF; RFC 1071's fold keeps
-// zero-ness), and fold(head + fold(tail)) == fold(head + tail).
-constexpr uint32_t kHeadBytes = 128;
-struct CombineArgs {
-  const uint8_t *arena;
-  const uint64_t *offsets;  // null: image k at k * stride, len bytes
-  const uint32_t *lengths;
-  uint64_t stride;
-  uint32_t len;
-  uint64_t count;
-  const uint16_t *tail;     // CHECKSUM of image k's tail
-  uint8_t *ok;              // verdicts
-  uint8_t *hdr;             // 4-B aligned, 32 B per image
-  int mode;                 // kRef or kRfc1071
-};
-hipError_t launch_header_combine(const CombineArgs &a, uint32_t num_cus, hipStream_t stream);
-
 // ---- FILL's field stores as a second pass (tcpck_header.hip) ----
 // One lane per image writes bytes 28-29 with a write-through streaming 2-B
 // store (nothing else in the arena is read or written).
@@ -219,6 +194,7 @@ struct PatchArgs {
   uint32_t store_bits;      // probe forms: 1 + store cache bits (sc0 1, nt 2, sc1 4; 0 plain) | granularity << 4
 };
 hipError_t launch_patch_fields(const PatchArgs &a, uint32_t num_cus, hipStream_t stream);
+
 
 // timing-only streaming micro-kernels (tcpck_diag.hip)
 hipError_t launch_diag_stream(int variant, const uint8_t *buf, uint64_t bytes, uint32_t *out, uint32_t num_cus,

@@ -100,7 +100,6 @@ struct SSArgs {
   int mode;                 // kRef or kRfc1071
   uint8_t *hdr;             // HDR: host-order header k at hdr + 32 k
   uint32_t defer_field;     // kFill: results to out only, the fields left for launch_patch_fields
-  uint32_t skip;            // offset lists (RECEIVE's tails): image k read from byte min(len, skip) on
 };
 
 __device__ __forceinline__ u32x4 zero_word(u32x4 w, uint32_t wi) {
@@ -117,50 +116,6 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t x) {
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) x = max(x, static_cast<uint32_t>(__shfl_xor(static_cast<int>(x), m, 64)));
   return x;
-}
-
-// RECEIVE's tail stream (SSArgs::skip, tcpck_batch_receive's combined form):
-// image j becomes its bytes [min(l_j, skip), l_j), so the stream never reads
-// the first line (its header pass reads it).  An image of <= skip bytes has an
-// empty tail; it is placed where the run's next longer image's tail starts (its
-// one chunk is then loaded with that tail's, no line of its own), or at its own
-// end when no longer image follows in the run.  Offsets stay in order.
-// Descriptors of run image kPer lane + i in o[i], l[i] (past the run: l = 0).
-__device__ __forceinline__ void tails(uint64_t (&o)[kPer], uint32_t (&l)[kPer], uint32_t nimg, uint32_t skip,
-                                      uint32_t lane) {
-  static_assert(kPer == 2, "two descriptors per lane");
-  uint64_t t[kPer];
-#pragma unroll
-  for (int i = 0; i < kPer; ++i) {
-    const uint32_t j = kPer * lane + i;
-    t[i] = (j < nimg && l[i] > skip) ? o[i] + skip : ~uint64_t{0};
-  }
-  // suffix minimum over the lanes >= this one, then the first tail start after each image
-  uint64_t m = t[0] < t[1] ? t[0] : t[1];
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t lo = static_cast<uint32_t>(__shfl_down(static_cast<int>(static_cast<uint32_t>(m)), d, 64));
-    const uint32_t hi = static_cast<uint32_t>(__shfl_down(static_cast<int>(static_cast<uint32_t>(m >> 32)), d, 64));
-    const uint64_t v = lane + d < 64 ? (static_cast<uint64_t>(hi) << 32) | lo : ~uint64_t{0};
-    m = v < m ? v : m;
-  }
-  const uint32_t nlo = static_cast<uint32_t>(__shfl_down(static_cast<int>(static_cast<uint32_t>(m)), 1, 64));
-  const uint32_t nhi = static_cast<uint32_t>(__shfl_down(static_cast<int>(static_cast<uint32_t>(m >> 32)), 1, 64));
-  const uint64_t after1 = lane < 63 ? (static_cast<uint64_t>(nhi) << 32) | nlo : ~uint64_t{0};  // images >= 2 lane + 2
-  const uint64_t after0 = t[1] < after1 ? t[1] : after1;                                    // images >= 2 lane + 1
-#pragma unroll
-  for (int i = 0; i < kPer; ++i) {
-    const uint32_t j = kPer * lane + i;
-    if (j >= nimg) continue;
-    if (l[i] > skip) {
-      o[i] += skip;
-      l[i] -= skip;
-    } else {
-      const uint64_t nx = i == 0 ? after0 : after1;
-      o[i] = nx != ~uint64_t{0} ? nx : o[i] + l[i];
-      l[i] = 0;
-    }
-  }
 }
 
 // MODE kRfc1071: exact u32 prefix tables (as tcpck_vvstream.hip), the
@@ -228,7 +183,6 @@ __global__ void __launch_bounds__(kBlock) sstream_kernel(SSArgs a) {
       o[i] = j < nimg ? a.offsets[kb + j] - a.base : 0;
       l[i] = j < nimg ? a.lengths[kb + j] : 0u;
     }
-    if (a.skip) tails(o, l, nimg, a.skip, lane);
     B = dev::align16_rel(arena, dev::read_lane64(o[0], 0));
     uint32_t n[kPer], hh[kPer], r16[kPer], hi = 0;
     bool ok = true, odd = false, shrt = false, hmis = false, hsmall = false;
@@ -565,13 +519,8 @@ __global__ void __launch_bounds__(kBlock) sstream_kernel(SSArgs a) {
   }
   if (bad) {  // wave-uniform: a layout the compacted walk does not take -> exact per-image pass
     for (uint64_t k = kb; k < ke; ++k) {
-      uint64_t start = FIXED ? k * S : a.offsets[k] - a.base;
-      uint32_t len = FIXED ? L : a.lengths[k];
-      if (!FIXED && a.skip) {  // the image's tail (where its empty tail sits does not matter here)
-        const uint32_t h0 = len < a.skip ? len : a.skip;
-        start += h0;
-        len -= h0;
-      }
+      const uint64_t start = FIXED ? k * S : a.offsets[k] - a.base;
+      const uint32_t len = FIXED ? L : a.lengths[k];
       if (OP == kFill && len < 30) continue;  // precondition of kFill (the C ABI rejects these)
       const uint32_t sum = dev::wave_image_sum<2, MODE>(arena, start, len, OP == kFill);
       if (lane == 0) store(k, sum, start);
@@ -684,8 +633,6 @@ hipError_t launch_sstream(int op, int variant, bool fixed, const RunArgs &r, uin
   a.out = r.out;
   a.mode = r.mode;
   a.hdr = r.hdr;
-  a.skip = r.skip;
-  if (a.skip && (fixed || op != kChecksum || r.hdr)) return hipErrorInvalidValue;  // RECEIVE's tail stream only
   // + 128 (kFill with a results buffer): the results only, the caller runs the field pass
   a.defer_field = (variant & 128) ? 1u : 0u;
   if (a.defer_field && (op != kFill || !r.out)) return hipErrorInvalidValue;
