@@ -79,10 +79,13 @@ extern "C" {
                                    run's first step read with the default cache
                                    policy; 28 = the policy's; + 32: FILL reads
                                    every step with the default policy, AUTO's
-                                   choice for images up to 448 B; + 64: FILL
+                                   choice for packed fixed images below 320 B
+                                   and variable means up to 448 B; + 64: FILL
                                    with a results buffer writes the results
                                    only and the write-through field pass
-                                   stores the fields)
+                                   stores the fields, AUTO's for packed fixed
+                                   images of 320 B - 1 KiB and gapped ones
+                                   from 512 B)
                                    | (blocks per CU cap << 8: LDS padding)
                                    | (grid oversubscription << 16: 0 = by batch
                                    size, 1 = none, M = M x the resident grid)   */

@@ -154,6 +154,7 @@ for s in ${STEPS:-tests smoke bench prof}; do
     flines) step flines_tests 600 python -u -m pytest tests/test_gpu_fill_lines.py -x -q --timeout 300 --timeout-method thread &&
       step flines 600 python scripts/fill_line_probe.py &&
       step flines_trace 300 rocprofv3 --kernel-trace --stats -d gpurun_out/flines_trace -o run --output-format csv -- python3 scripts/fill_line_probe.py --lengths 1492 ;;
+    fsweep) step fsweep 900 python scripts/fill_policy_sweep.py ;;
     bench_receive) step bench_receive 600 python bench.py --config receive ;;
     bench_fill) step bench_fill 600 python bench.py --config fill ;;
     bench_slots) step bench_slots 600 python bench.py --config slots ;;

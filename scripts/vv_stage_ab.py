@@ -1,0 +1,84 @@
+#!/usr/bin/env python3
+"""vvstream result staging, A/B on one box (round 4).
+
+A: libtcpck.so -- results staged in a VGPR, 64 per store (as rstream).
+B: libtcpck_probe.so built with -DTCPCK_VV_NOSTAGE for this run only -- each
+   step's results stored from inside the step loop (the round-1..3 form).
+The AUTO CHECKSUM / VERIFY on C3's packed 4M mix and on packed fixed 96/256-B
+images, interleaved rounds of 20 back-to-back launches; results compared."""
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "tcp-stack_amd")]
+
+import torch  # noqa: E402
+import tcpck  # noqa: E402
+
+
+def timed(fn, s, reps=20):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(reps):
+        fn()
+    e1.record(s)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def ab(label, fa, fb, outa, outb, algo, s, rounds=9):
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < 0.3:
+        fa()
+        fb()
+        torch.cuda.synchronize()
+    ta, tb = [], []
+    for _ in range(rounds):
+        ta.append(timed(fa, s))
+        tb.append(timed(fb, s))
+    same = torch.equal(outa, outb)
+    ma, mb = float(np.median(ta)), float(np.median(tb))
+    print(f"{label:26s} staged {ma * 1e3:7.1f} us ({100 * algo / (ma * 1e-3) / 8e12:5.1f} %)   "
+          f"unstaged {mb * 1e3:7.1f} us ({100 * algo / (mb * 1e-3) / 8e12:5.1f} %)   results {'equal' if same else 'DIFFER'}",
+          flush=True)
+
+
+def main():
+    A = tcpck.Context(0)
+    B = tcpck.Context(0, probe=True)
+    s = torch.cuda.current_stream()
+    K = tcpck
+    rng = np.random.default_rng(42)
+    n = 1 << 22
+    ln = (np.asarray((64, 576, 1460), np.uint32)[rng.integers(0, 3, n)] + 32).astype(np.uint32)
+    off = np.concatenate([[0], np.cumsum(ln[:-1], dtype=np.uint64)]).astype(np.uint64)
+    total = int(ln.sum())
+    arena = torch.empty(total, dtype=torch.uint8, device="cuda")
+    d_off = torch.from_numpy(off.view(np.int64)).cuda()
+    d_len = torch.from_numpy(ln.view(np.int32)).cuda()
+    K.synth_var(arena, d_off, d_len, int(ln.max()), n, seed=42)
+    hints = dict(total_bytes=total, min_len=int(ln.min()), max_len=int(ln.max()), packed=True)
+    for op, name, dt in ((K.OP_CHECKSUM, "C3 CHECKSUM", torch.int16), (K.OP_VERIFY, "C3 VERIFY", torch.uint8)):
+        oa = torch.empty(n, dtype=dt, device="cuda")
+        ob = torch.empty(n, dtype=dt, device="cuda")
+        ab(name, lambda: A.batch_var(op, arena, d_off, d_len, n, oa, stream=s, **hints),
+           lambda: B.batch_var(op, arena, d_off, d_len, n, ob, stream=s, **hints), oa, ob, total + 2 * n, s)
+    del arena
+    torch.cuda.empty_cache()
+    for L in (96, 256, 448):
+        m = 1564475392 // L
+        arena = torch.empty(m * L, dtype=torch.uint8, device="cuda")
+        K.synth_fixed(arena, L, L, m, seed=42)
+        oa = torch.empty(m, dtype=torch.int16, device="cuda")
+        ob = torch.empty(m, dtype=torch.int16, device="cuda")
+        ab(f"fixed {L} CHECKSUM", lambda: A.batch_fixed(K.OP_CHECKSUM, arena, L, L, m, oa, stream=s),
+           lambda: B.batch_fixed(K.OP_CHECKSUM, arena, L, L, m, ob, stream=s), oa, ob, m * L + 2 * m, s)
+        del arena
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()

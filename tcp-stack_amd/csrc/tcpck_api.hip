@@ -225,6 +225,13 @@ constexpr int kVvDeferFill = 64;         // vvstream: kFill writes the results o
 // images of at least this many bytes; smaller images pay more for 1M-per-
 // 38-us scattered field stores than the in-stream stores cost them
 constexpr uint64_t kDeferFillMinLen = 512;
+// packed fixed images: vvstream's deferred form from 320 B up to 1 KiB, where
+// it beats the in-stream forms and rstream's (round-4 re-check after the
+// write-through field pass, scripts/fill_policy_sweep.py,
+// profiles/r04/fill_policy_sweep.log, us per 1.5 GB: 320 B 448 -> 430, 384 B
+// 427 -> 397, 448 B 408 -> 366, 512 B 347 (gstream) -> 328, 640 B 359
+// (rstream 25) -> 322, 768 B 318 -> 308; 1 KiB stays on rstream 25: 279 vs 284)
+constexpr uint64_t kVvDeferPackedMin = 320, kVvDeferPackedEnd = 1024;
 constexpr int kSstreamDeferFill = 128;   // sstream: kFill writes the results only, the field pass follows
 // variable layouts: vvstream's in-stream zeroing costs ~25 ns per image, so
 // its deferred form pays only for larger images (C3's mean 732 B: 718 -> 702
@@ -325,11 +332,12 @@ void pick_fixed(int op, int mode, const uint8_t *arena, uint64_t stride, uint32_
         kernel = TCPCK_KERNEL_SEG;
         param = (tcpck::kShapeSmall + 1) | kSegXcdOrder;
       }
-    } else if (op == TCPCK_OP_FILL && len <= 512 && tcpck::gstream_applies(arena, stride, len)) {
-      // send-path FILL of power-of-two images, 32 B (pure ACKs) .. 512 B, and
-      // of the other multiples of 16 B up to 240 B (1 KiB: rstream's deferred
-      // fields since round 3's write-through field pass, 277 vs 299 us for
-      // 1.5M images; 512 B stays: 345 vs 406 us, profiles/r04/fill_line_probe.log):
+    } else if (op == TCPCK_OP_FILL && len <= 256 && tcpck::gstream_applies(arena, stride, len)) {
+      // send-path FILL of power-of-two images, 32 B (pure ACKs) .. 256 B, and
+      // of the other multiples of 16 B up to 240 B (512 B and 1 KiB: the
+      // deferred-field forms since round 3's write-through field pass,
+      // vvstream 328 vs 347 us and rstream 279 vs 299 us per 1.5 GB,
+      // profiles/r04/fill_policy_sweep.log):
       // gstream; up to 256 B every line holds a checksum field, and reading
       // the lines with the default cache policy keeps them in L2 until the
       // field store lands, so they leave as whole lines rather than masked
@@ -344,7 +352,8 @@ void pick_fixed(int op, int mode, const uint8_t *arena, uint64_t stride, uint32_
       // 1-2 points ahead of vvstream FIXED)
       kernel = TCPCK_KERNEL_GSTREAM;
       param = len <= 128 ? tcpck::kGstreamWriteBack : (len <= 256 ? tcpck::kGstreamDefaultLoads : 0);
-    } else if (len < 512) {
+    } else if (len < 512 || (op == TCPCK_OP_FILL && len < kVvDeferPackedEnd)) {
+      // (FILL from 512 B: vvstream's deferred form, kVvDeferPackedMin, below)
       // packed, by image length (scripts/policy_sweep.py, profiles/r01/policy_small.log):
       // below 512 B boundaries are dense enough that resolving all of a step's
       // ends in parallel from the prefix table wins (vvstream FIXED, 80-81% at
@@ -445,7 +454,9 @@ hipError_t run_fixed_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint
   }
   if (kernel == TCPCK_KERNEL_VVSTREAM) {  // any even length: the prefix table takes any number of ends per step
     if (len == 0 || stride > (1u << 24) || (op == TCPCK_OP_FILL && len < 30)) return hipErrorInvalidValue;
-    if (auto_pick && !caller.instream && op == TCPCK_OP_FILL && out && len >= kDeferFillMinLen) param |= kVvDeferFill;
+    if (auto_pick && !caller.instream && op == TCPCK_OP_FILL && out &&
+        len >= (stride == len ? kVvDeferPackedMin : kDeferFillMinLen))
+      param = (param & ~kVvKeep) | kVvDeferFill;  // (the default-policy reads served the in-stream stores)
     if (param & kVvDeferFill) *patch = true;
     if (mode != TCPCK_MODE_REF && (len >= (1u << 17) || (param & 32))) return hipErrorInvalidValue;
     tcpck::RunArgs a{};
