@@ -20,21 +20,27 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "tcp-stack_amd"), os.path.join(ROOT, "t
 import torch  # noqa: E402
 import tcpck  # noqa: E402
 
-FIXED_L = [16, 32, 64, 96, 128, 192, 256, 384, 512, 768, 1024, 1492, 4096]
+FIXED_L = [16, 32, 64, 96, 128, 192, 256, 320, 384, 448, 512, 640, 768, 1024, 1492, 2048, 3000, 4096]
 MIXES = {"32/1492": (0, 1460), "96/608/1492": (64, 576, 1460), "32..1492": (0, 32, 64, 128, 256, 512, 1024, 1460),
          "608/1492": (576, 1460)}
 
 
-def time_runs(runs, reps, stream):
+def time_runs(runs, reps, stream, per=10):
+    """Median over `reps` rounds of `per` back-to-back launches (interleaved by round)."""
     t = {r[0]: [] for r in runs}
+    for label, fn in runs:  # settle
+        for _ in range(per):
+            fn()
+    torch.cuda.synchronize()
     for _ in range(reps):
         for label, fn in runs:
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record(stream)
-            fn()
+            for _ in range(per):
+                fn()
             b.record(stream)
             torch.cuda.synchronize()
-            t[label].append(a.elapsed_time(b))
+            t[label].append(a.elapsed_time(b) / per)
     return {k: float(np.median(v)) for k, v in t.items()}
 
 
@@ -61,13 +67,14 @@ def main():
         ln = torch.full((n,), L, dtype=torch.int32, device="cuda")
         cand = [("auto", lambda: ctx.batch_fixed(K.OP_CHECKSUM, a, L, L, n, out, stream=s)),
                 ("seg", lambda: ctx.batch_fixed_ex(K.OP_CHECKSUM, a, L, L, n, out, K.KERNEL_SEG, 0, stream=s)),
-                ("rstream", lambda: ctx.batch_fixed_ex(K.OP_CHECKSUM, a, L, L, n, out, K.KERNEL_RSTREAM, 0, stream=s)),
-                ("vvstream fix", lambda: ctx.batch_fixed_ex(K.OP_CHECKSUM, a, L, L, n, out, K.KERNEL_VVSTREAM, 4,
-                                                            stream=s)),
-                ("rstream U2", lambda: ctx.batch_fixed_ex(K.OP_CHECKSUM, a, L, L, n, out, K.KERNEL_RSTREAM, 1,
+                ("rstream 20", lambda: ctx.batch_fixed_ex(K.OP_CHECKSUM, a, L, L, n, out, K.KERNEL_RSTREAM, 20,
                                                           stream=s)),
-                ("var vvstream", lambda: ctx.batch_var_ex(K.OP_CHECKSUM, a, off, ln, n, out, K.KERNEL_VVSTREAM, 4,
-                                                          packed=True, total_bytes=n * L, stream=s))]
+                ("vvstream fix 28", lambda: ctx.batch_fixed_ex(K.OP_CHECKSUM, a, L, L, n, out, K.KERNEL_VVSTREAM, 28,
+                                                               stream=s)),
+                ("gstream 0", lambda: ctx.batch_fixed_ex(K.OP_CHECKSUM, a, L, L, n, out, K.KERNEL_GSTREAM, 0,
+                                                         stream=s)),
+                ("var vvstream 28", lambda: ctx.batch_var_ex(K.OP_CHECKSUM, a, off, ln, n, out, K.KERNEL_VVSTREAM, 28,
+                                                             packed=True, total_bytes=n * L, stream=s))]
         runs = []
         for label, fn in cand:
             try:
@@ -102,14 +109,10 @@ def main():
         lay = dict(total_bytes=total, min_len=int(ln_np.min()), max_len=int(ln_np.max()), packed=True)
         cand = [("auto", lambda: ctx.batch_var(K.OP_CHECKSUM, a, off, ln, n, out, stream=s, **lay)),
                 ("seg", lambda: ctx.batch_var_ex(K.OP_CHECKSUM, a, off, ln, n, out, K.KERNEL_SEG, 0, stream=s, **lay)),
-                ("vvstream", lambda: ctx.batch_var_ex(K.OP_CHECKSUM, a, off, ln, n, out, K.KERNEL_VVSTREAM, 0,
-                                                      stream=s, **lay)),
-                ("vvstream U8", lambda: ctx.batch_var_ex(K.OP_CHECKSUM, a, off, ln, n, out, K.KERNEL_VVSTREAM, 1,
+                ("vvstream 28", lambda: ctx.batch_var_ex(K.OP_CHECKSUM, a, off, ln, n, out, K.KERNEL_VVSTREAM, 28,
                                                          stream=s, **lay)),
-                ("vvstream pol", lambda: ctx.batch_var_ex(K.OP_CHECKSUM, a, off, ln, n, out, K.KERNEL_VVSTREAM, 4,
-                                                          stream=s, **lay)),
-                ("vvstream cnt", lambda: ctx.batch_var_ex(K.OP_CHECKSUM, a, off, ln, n, out, K.KERNEL_VVSTREAM, 2,
-                                                          stream=s, **lay))]
+                ("sstream 0", lambda: ctx.batch_var_ex(K.OP_CHECKSUM, a, off, ln, n, out, K.KERNEL_SSTREAM, 0,
+                                                       stream=s, sorted=True, **lay))]
         runs = []
         for label, fn in cand:
             out.zero_()
