@@ -1,9 +1,12 @@
 #!/usr/bin/env python3
-"""vvstream result staging, A/B on one box (round 4).
+"""vvstream A/B on one box (round 4): libtcpck.so (A) against a
+libtcpck_probe.so built for this run only with one change switched off (B).
 
-A: libtcpck.so -- results staged in a VGPR, 64 per store (as rstream).
-B: libtcpck_probe.so built with -DTCPCK_VV_NOSTAGE for this run only -- each
-   step's results stored from inside the step loop (the round-1..3 form).
+  default  A: results staged in a VGPR, 64 per store (as rstream); B:
+           -DTCPCK_VV_NOSTAGE, each step's results stored from inside the step
+           loop (the round-1..3 form)
+  --cache  A: the pending ends kept in a VGPR across steps (CACHE_E); B:
+           -DTCPCK_VV_NOCACHE, the ends re-read from LDS and balloted every step
 The AUTO CHECKSUM / VERIFY on C3's packed 4M mix and on packed fixed 96/256-B
 images, interleaved rounds of 20 back-to-back launches; results compared."""
 import os
@@ -41,8 +44,9 @@ def ab(label, fa, fb, outa, outb, algo, s, rounds=9):
         tb.append(timed(fb, s))
     same = torch.equal(outa, outb)
     ma, mb = float(np.median(ta)), float(np.median(tb))
-    print(f"{label:26s} staged {ma * 1e3:7.1f} us ({100 * algo / (ma * 1e-3) / 8e12:5.1f} %)   "
-          f"unstaged {mb * 1e3:7.1f} us ({100 * algo / (mb * 1e-3) / 8e12:5.1f} %)   results {'equal' if same else 'DIFFER'}",
+    na, nb = ("cached", "per-step") if "--cache" in sys.argv else ("staged", "unstaged")
+    print(f"{label:26s} {na} {ma * 1e3:7.1f} us ({100 * algo / (ma * 1e-3) / 8e12:5.1f} %)   "
+          f"{nb} {mb * 1e3:7.1f} us ({100 * algo / (mb * 1e-3) / 8e12:5.1f} %)   results {'equal' if same else 'DIFFER'}",
           flush=True)
 
 
@@ -68,14 +72,16 @@ def main():
            lambda: B.batch_var(op, arena, d_off, d_len, n, ob, stream=s, **hints), oa, ob, total + 2 * n, s)
     del arena
     torch.cuda.empty_cache()
-    for L in (96, 256, 448):
+    for L in (96, 256, 448, 736, 1492, 4096):
         m = 1564475392 // L
         arena = torch.empty(m * L, dtype=torch.uint8, device="cuda")
         K.synth_fixed(arena, L, L, m, seed=42)
         oa = torch.empty(m, dtype=torch.int16, device="cuda")
         ob = torch.empty(m, dtype=torch.int16, device="cuda")
-        ab(f"fixed {L} CHECKSUM", lambda: A.batch_fixed(K.OP_CHECKSUM, arena, L, L, m, oa, stream=s),
-           lambda: B.batch_fixed(K.OP_CHECKSUM, arena, L, L, m, ob, stream=s), oa, ob, m * L + 2 * m, s)
+        ab(f"fixed {L} CHECKSUM vv28", lambda: A.batch_fixed_ex(K.OP_CHECKSUM, arena, L, L, m, oa, K.KERNEL_VVSTREAM, 28,
+                                                                stream=s),
+           lambda: B.batch_fixed_ex(K.OP_CHECKSUM, arena, L, L, m, ob, K.KERNEL_VVSTREAM, 28, stream=s), oa, ob,
+           m * L + 2 * m, s)
         del arena
         torch.cuda.empty_cache()
 
