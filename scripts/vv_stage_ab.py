@@ -7,6 +7,9 @@ libtcpck_probe.so built for this run only with one change switched off (B).
            loop (the round-1..3 form)
   --cache  A: the pending ends kept in a VGPR across steps (CACHE_E); B:
            -DTCPCK_VV_NOCACHE, the ends re-read from LDS and balloted every step
+  --qsel   rstream (tcpck_rstream.hip) A: a 4-B-aligned boundary's P from one
+           readlane of the lane's exclusive prefix + its v_dot2 partial (QSEL);
+           B: -DTCPCK_RS_NOQSEL, six readlanes and a scalar word sum
 The AUTO CHECKSUM / VERIFY on C3's packed 4M mix and on packed fixed 96/256-B
 images, interleaved rounds of 20 back-to-back launches; results compared."""
 import os
@@ -44,10 +47,34 @@ def ab(label, fa, fb, outa, outb, algo, s, rounds=9):
         tb.append(timed(fb, s))
     same = torch.equal(outa, outb)
     ma, mb = float(np.median(ta)), float(np.median(tb))
-    na, nb = ("cached", "per-step") if "--cache" in sys.argv else ("staged", "unstaged")
+    na, nb = (("cached", "per-step") if "--cache" in sys.argv else
+              (("qsel", "6-read") if "--qsel" in sys.argv else ("staged", "unstaged")))
     print(f"{label:26s} {na} {ma * 1e3:7.1f} us ({100 * algo / (ma * 1e-3) / 8e12:5.1f} %)   "
           f"{nb} {mb * 1e3:7.1f} us ({100 * algo / (mb * 1e-3) / 8e12:5.1f} %)   results {'equal' if same else 'DIFFER'}",
           flush=True)
+
+
+def main_qsel(A, B, s, K):
+    for L, mode in ((1492, 0), (1492, 1), (512, 0), (1024, 0), (2048, 0), (3000, 0)):
+        m = 1564475392 // L
+        arena = torch.empty(m * L, dtype=torch.uint8, device="cuda")
+        K.synth_fixed(arena, L, L, m, seed=42)
+        for op, dt, name in ((K.OP_CHECKSUM, torch.int16, "CHECKSUM"), (K.OP_VERIFY, torch.uint8, "VERIFY")):
+            oa = torch.empty(m, dtype=dt, device="cuda")
+            ob = torch.empty(m, dtype=dt, device="cuda")
+            ab(f"rstream {L} {name} m{mode}",
+               lambda: A.batch_fixed_ex(op, arena, L, L, m, oa, K.KERNEL_RSTREAM, 20, mode=mode, stream=s),
+               lambda: B.batch_fixed_ex(op, arena, L, L, m, ob, K.KERNEL_RSTREAM, 20, mode=mode, stream=s), oa, ob,
+               m * L + 2 * m, s)
+        del arena
+        torch.cuda.empty_cache()
+    n = 8 << 20  # C5 on one GPU
+    arena = torch.empty(n * 1492, dtype=torch.uint8, device="cuda")
+    K.synth_fixed(arena, 1492, 1492, n, seed=42)
+    oa = torch.empty(n, dtype=torch.int16, device="cuda")
+    ob = torch.empty(n, dtype=torch.int16, device="cuda")
+    ab("rstream C5 8M CHECKSUM", lambda: A.batch_fixed(K.OP_CHECKSUM, arena, 1492, 1492, n, oa, stream=s),
+       lambda: B.batch_fixed(K.OP_CHECKSUM, arena, 1492, 1492, n, ob, stream=s), oa, ob, n * 1494, s, rounds=5)
 
 
 def main():
@@ -55,6 +82,9 @@ def main():
     B = tcpck.Context(0, probe=True)
     s = torch.cuda.current_stream()
     K = tcpck
+    if "--qsel" in sys.argv:
+        main_qsel(A, B, s, K)
+        return
     rng = np.random.default_rng(42)
     n = 1 << 22
     ln = (np.asarray((64, 576, 1460), np.uint32)[rng.integers(0, 3, n)] + 32).astype(np.uint32)
