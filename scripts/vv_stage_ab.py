@@ -1,6 +1,9 @@
 #!/usr/bin/env python3
 """vvstream A/B on one box (round 4): libtcpck.so (A) against a
 libtcpck_probe.so built for this run only with one change switched off (B).
+All three changes lost or tied and were removed with their build switches
+(logs profiles/r04/vv_stage_ab.log, vv_cache_ab.log,
+rs_qsel_ab.log): re-running this needs the change and its -D switch back.
 
   default  A: results staged in a VGPR, 64 per store (as rstream); B:
            -DTCPCK_VV_NOSTAGE, each step's results stored from inside the step
