@@ -7,7 +7,9 @@ deferred form (rstream 25) and CHECKSUM.  (round 4)
 it.  31: the stream skips every field's 128-B line, then a pass reads each
 field line and writes it back whole (a full-line write needs no merge read).
 Median of rounds of 20 back-to-back steps after a settle; every FILL's arena is
-compared with the 25 form's."""
+compared with the 25 form's.  The line form lost (profiles/r04/fill_line_probe.log,
+DESIGN.md section 8) and rstream variant 31 was removed with it: its cases are
+rejected by the current libraries."""
 import argparse
 import os
 import sys

@@ -151,9 +151,6 @@ for s in ${STEPS:-tests smoke bench prof}; do
     prof_fill_c3) step prof_fill_c3 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_fill_c3 -o run --output-format csv -- python3 bench.py --config fill_c3 --steps 10 --warmup 2 --no-cpu-baseline --no-e2e ;;
     new4) step new4 900 python -u -m pytest tests/test_gpu_full_paths.py -x -v --timeout 300 --timeout-method thread ;;
     tests_new) step tests_new 900 python -u -m pytest tests/test_gpu_c5.py tests/test_gpu_multi_ctx.py tests/test_drop_in.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
-    flines) step flines_tests 600 python -u -m pytest tests/test_gpu_fill_lines.py -x -q --timeout 300 --timeout-method thread &&
-      step flines 600 python scripts/fill_line_probe.py &&
-      step flines_trace 300 rocprofv3 --kernel-trace --stats -d gpurun_out/flines_trace -o run --output-format csv -- python3 scripts/fill_line_probe.py --lengths 1492 ;;
     fsweep) step fsweep 900 python scripts/fill_policy_sweep.py ;;
     bench_receive) step bench_receive 600 python bench.py --config receive ;;
     bench_fill) step bench_fill 600 python bench.py --config fill ;;
