@@ -353,7 +353,7 @@ void pick_fixed(int op, int mode, const uint8_t *arena, uint64_t stride, uint32_
       kernel = TCPCK_KERNEL_GSTREAM;
       param = len <= 128 ? tcpck::kGstreamWriteBack : (len <= 256 ? tcpck::kGstreamDefaultLoads : 0);
     } else if (len < 512 || (op == TCPCK_OP_FILL && len < kVvDeferPackedEnd)) {
-      // (FILL from 512 B: vvstream's deferred form, kVvDeferPackedMin, below)
+      // (FILL up to 1 KiB stays here: from kVvDeferPackedMin on in vvstream's deferred form, run_fixed_impl)
       // packed, by image length (scripts/policy_sweep.py, profiles/r01/policy_small.log):
       // below 512 B boundaries are dense enough that resolving all of a step's
       // ends in parallel from the prefix table wins (vvstream FIXED, 80-81% at
