@@ -116,6 +116,7 @@ IMAGE_BYTES = {"slots": "96/608/1492 in 2048-B slots", "receive": "96/608/1492 i
                "segment": "32 + 1460 in 1504-B slots"}
 MODES = {"c2_rfc": 1}  # TCPCK_MODE_RFC1071; every other config runs the reference arithmetic (0)
 NO_RESULTS = {"fill_noout"}  # steps that write no results array (only the fields in place)
+RING_COUNT = 2  # slots / receive: identical rings taken in turn (Workload)
 
 
 def log(*a):
@@ -134,19 +135,22 @@ def parse():
     p.add_argument("--no-extras", action="store_true", help="default run: skip the c3/c4/c5_strong keys")
     p.add_argument("--settle-ms", type=float, default=250.0,
                    help="untimed back-to-back launches before the warm-up steps (clock ramp)")
+    p.add_argument("--launch-check", action="store_true",
+                   help="start the ranks and print their layout only (no GPU; tests/test_bench_contract.py)")
     p.add_argument("--per-launch-events", action="store_true",
                    help="one HIP event pair per launch (adds ~10 us idle per step)")
     return p.parse_args()
 
 
-def bench_c1(args):
-    """C1: one 1460-B segment at a time over UDP loopback, CPU only (plumbing).
-
-    tcp-stack_amd/bin/loopback_c1 is the same program compiled against the
-    drop-in header (this library) and, as oracle/_ref/loopback_c1_ref, against
-    the reference's own tcp-header.h; both run here on the host."""
+def run_c1(n: int) -> dict:
+    """C1 (BASELINE configs[0]): n single 1460-B segments over UDP loopback,
+    CPU only -- send insert (socket-manager.cc:9-10), receive buffer
+    (network-service.cc:49-56), verify (socket-manager.h:182).
+    tcp-stack_amd/bin/loopback_c1 is the program compiled against the drop-in
+    header (this library); oracle/_ref/loopback_c1_ref, where present, the same
+    source compiled against the reference's own include/tcp-header.h is its
+    cpu_baseline.  Both run on the host."""
     import subprocess
-    n = max(1000, args.steps * 1000)
 
     def run(exe):
         r = subprocess.run([exe, str(n), "1460"], capture_output=True, text=True, timeout=300)
@@ -155,20 +159,31 @@ def bench_c1(args):
         return json.loads(r.stdout.strip().splitlines()[-1])
 
     ours = run(os.path.join(ROOT, "tcp-stack_amd", "bin", "loopback_c1"))
-    rec = {"metric": "C1 loopback send+fill+recv+verify latency per 1492-B segment (CPU, no GPU)",
-           "value": round(ours["us_per_segment"], 3), "unit": "us/segment", "n_gpus": 0, "steps": n,
-           "warmup": 0, "ms_per_step": round(ours["us_per_segment"] / 1e3, 6), "higher_is_better": False,
-           "scaling": "weak", "vs_baseline": None, "dtype": "u16", "data": "synthetic (fixed payload pattern)",
-           "config": {"workload": "C1: single 1460-B segments over UDP 127.0.0.1, drop-in tcp_stack/tcp-header.h",
-                      "segments": n, "verified": ours["verified"], "send_checksum_ns": ours["send_checksum_ns"],
-                      "recv_checksum_ns": ours["recv_checksum_ns"]}}
+    rec = {"value": round(ours["us_per_segment"], 3), "unit": "us/segment", "segments": n,
+           "received": ours["received"], "verified": ours["verified"],
+           "send_ck_ns": ours["send_checksum_ns"], "recv_ck_ns": ours["recv_checksum_ns"]}
     ref = os.path.join(ROOT, "oracle", "_ref", "loopback_c1_ref")
     if os.path.exists(ref):
         r = run(ref)
         rec["cpu_baseline"] = {"value": round(r["us_per_segment"], 3), "unit": "us/segment", "cores": 1,
-                               "kind": "reference", "sample": f"{n} segments, same program built on the "
-                               "reference's include/tcp-header.h (-O2)",
-                               "send_checksum_ns": r["send_checksum_ns"], "recv_checksum_ns": r["recv_checksum_ns"]}
+                               "kind": "reference", "verified": r["verified"],
+                               "send_ck_ns": r["send_checksum_ns"], "recv_ck_ns": r["recv_checksum_ns"]}
+    return rec
+
+
+def bench_c1(args):
+    """--config c1: the C1 record as a line of its own."""
+    n = max(1000, args.steps * 1000)
+    r = run_c1(n)
+    rec = {"metric": "C1 loopback send+fill+recv+verify latency per 1492-B segment (CPU, no GPU)",
+           "value": r.pop("value"), "unit": r.pop("unit"), "n_gpus": 0, "steps": n, "warmup": 0,
+           "ms_per_step": None, "higher_is_better": False, "scaling": "weak", "vs_baseline": None, "dtype": "u16",
+           "data": "synthetic (fixed payload pattern)",
+           "config": {"workload": "C1: single 1460-B segments over UDP 127.0.0.1, drop-in tcp_stack/tcp-header.h",
+                      **{k: v for k, v in r.items() if k != "cpu_baseline"}}}
+    rec["ms_per_step"] = round(rec["value"] / 1e3, 6)
+    if "cpu_baseline" in r:
+        rec["cpu_baseline"] = r["cpu_baseline"]
     print(json.dumps(rec), flush=True)
 
 
@@ -196,24 +211,39 @@ class Workload:
             rng = np.random.default_rng(42 + rank)
             ln = (np.asarray((64, 576, 1460), np.uint32)[rng.integers(0, 3, count)] + 32).astype(np.uint32)
             off = np.arange(count, dtype=np.uint64) * np.uint64(L)
-            arena = torch.empty(count * L, dtype=torch.uint8, device="cuda")
             d_off, d_ln = torch.from_numpy(off).cuda(), torch.from_numpy(ln).cuda()
-            tcpck.synth_var(arena, d_off, d_ln, 1492, count, seed=42, first_index=first, stream=stream)
+            # RING_COUNT rings with the same datagrams, taken in turn: step k+1
+            # never reads the lines step k pulled into the 256-MB Infinity Cache
+            # (RECEIVE's header pass ends a step on the first 128-B line of all
+            # 1M slots, 128 MB, which the next step's stream reads first;
+            # a real receive ring never sees the same datagrams twice)
+            rings = []
+            for _ in range(RING_COUNT):
+                a = torch.empty(count * L, dtype=torch.uint8, device="cuda")
+                tcpck.synth_var(a, d_off, d_ln, 1492, count, seed=42, first_index=first, stream=stream)
+                rings.append(a)
+            arena = rings[0]
             img_bytes = int(ln.astype(np.int64).sum())
             lmin, lmax = int(ln.min()), int(ln.max())
 
             if kind == "slots":
-                def step(out):
-                    ctx.batch_var(tcpck.OP_VERIFY, arena, d_off, d_ln, count, out, total_bytes=img_bytes,
+                def ring_step(a, out):
+                    ctx.batch_var(tcpck.OP_VERIFY, a, d_off, d_ln, count, out, total_bytes=img_bytes,
                                   min_len=lmin, max_len=lmax, sorted=True, stream=stream)
             else:
                 hdr_out = torch.empty(count * 32, dtype=torch.uint8, device="cuda")
                 self.extra_bytes = 32 * count  # the header array written
 
-                def step(out):
-                    ctx.batch_receive(arena, count, out, hdr_out, offsets=d_off, lengths=d_ln,
+                def ring_step(a, out):
+                    ctx.batch_receive(a, count, out, hdr_out, offsets=d_off, lengths=d_ln,
                                       total_bytes=img_bytes, min_len=lmin, max_len=lmax, sorted=True,
                                       stream=stream)
+            self.turn = 0
+
+            def step(out):
+                ring_step(rings[self.turn % self.n_rings], out)
+                self.turn += 1
+            self.n_rings = RING_COUNT
         elif kind == "segment":
             P, seg, stride = count, L, 1504
             payload = torch.empty(P, dtype=torch.uint8, device="cuda")
@@ -344,8 +374,7 @@ def measure(w: Workload, args, world, stream, coll_dev):
     shard_bytes = torch.tensor([w.img_bytes], dtype=torch.int64, device=coll_dev)
     if world > 1:
         dist.all_reduce(shard_bytes)  # bytes all ranks processed per step (shards may differ by one image)
-    settle = {"ms": round(settle_ms, 1), "launches": settled,
-              "why": "untimed launches before the W warm-ups: the idle GPU's clock ramp lasts 10-50 ms"}
+    settle = {"ms": round(settle_ms, 1), "launches": settled}
     return tmax, launch_ms, launch_ms_all, int(shard_bytes.item()), settle
 
 
@@ -378,25 +407,85 @@ def extra_config(name, key, ctx, stream, rank, world, args, coll_dev):
         rec["kernel_GiBs"] = round(step_bytes / (max(launch_ms_all) * 1e-3) / GIB, 2)
         rec["images_total"] = CONFIGS[name][2]
         rec["parallelism"] = f"shard{world}: one batch split by tcpck.shard.shard_range, no collective"
+    if getattr(w, "n_rings", 1) > 1:
+        # the same step on ONE ring, every step over the same datagrams: what the
+        # Infinity Cache's cross-step reuse adds (never `value`)
+        w.n_rings = 1
+        tmax1, launch1, _, step_bytes1, _ = measure(w, args, world, stream, coll_dev)
+        rec["same_ring"] = {"value": round(step_bytes1 * args.steps / tmax1 / GIB, 2),
+                            "frac": round(w.algo_bytes / (launch1 * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
     del w
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
     return key, rec
 
 
+def spawn_ranks(args) -> int | None:
+    """`--gpus N` (N > 1) run bare, without a launcher: start the N ranks as a
+    CHILD `torch.distributed.run` on this same command line (one process per
+    GPU, rendezvous on 127.0.0.1) and return its exit code; rank 0's line
+    reaches our stdout through the inherited descriptor.  Runs before anything
+    touches the GPU, and never replaces this process (no exec).  None when
+    there is nothing to spawn (N = 1, or already a rank of a launcher)."""
+    if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return None
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:  # a free rendezvous port
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    log(f"--gpus {args.gpus} without a launcher: spawning {' '.join(cmd[1:6])} ...")
+    sys.stdout.flush()
+    return subprocess.run(cmd).returncode
+
+
+def launch_check(args) -> None:
+    """--launch-check: the rank layout alone (no GPU): every rank joins the
+    process group on TCPCK_BENCH_BACKEND (gloo here), rank 0 prints the world
+    size and every rank's (rank, local rank).  Exercises spawn_ranks on CPU."""
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group(os.environ.get("TCPCK_BENCH_BACKEND", "gloo"))
+        t = torch.zeros(2 * world, dtype=torch.int64)
+        t[2 * rank], t[2 * rank + 1] = rank, local
+        dist.all_reduce(t)
+        ranks = t.view(world, 2).tolist()
+    else:
+        ranks = [[rank, local]]
+    if rank == 0:
+        print(json.dumps({"n_gpus": world, "gpus_arg": args.gpus, "ranks": ranks}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
     if args.config == "c1":
         return bench_c1(args)
+    rc = spawn_ranks(args)
+    if rc is not None:
+        sys.exit(rc)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        # one line per job: a launcher with another rank count than --gpus would
+        # print an N-GPU line for a different N
+        log(f"error: --gpus {args.gpus} but the launcher started WORLD_SIZE {world} ranks")
+        sys.exit(2)
+    if args.launch_check:
+        return launch_check(args)
     import torch
     import torch.distributed as dist
     import tcpck
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        log(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
     # rehearsal knobs (not used by the driver): several ranks on one GPU with
     # gloo collectives, to exercise the N>1 path on a one-GPU box
     backend = os.environ.get("TCPCK_BENCH_BACKEND", "nccl")
@@ -428,10 +517,10 @@ def main():
         dt_max = max_over_ranks(dt, device=coll_dev)
         ok_all = min(gather_ranks(1.0 if ok else 0.0, device=coll_dev)) > 0
         if np.isfinite(dt_max):
-            e2e = {"value": round(world * w.count * w.L / dt_max / GIB, 2), "unit": "GiB/s",
+            e2e = {"value": round(world * w.count * w.L / dt_max / GIB, 2), "unit": "GiB/s", "match": ok_all,
                    "what": "pinned host arena -> 64 MiB chunks H2D on 2 streams -> kernel -> u16 results D2H, "
-                           f"all {world} rank(s) at once, whole-job bytes / slowest rank",
-                   "results_match_device_path": ok_all}
+                           f"all {world} rank(s) at once, whole-job bytes / slowest rank; match: results == the "
+                           "device path's"}
 
     want_cpu = rank == 0 and world == 1 and not args.no_cpu_baseline and w.kind in ("fixed", "mixed")
     cpu_rec = cpu_baseline_for(w, args.cpu_seconds) if want_cpu else None  # before the extras free the arena
@@ -460,8 +549,12 @@ def main():
         rec["cpu_baseline"] = cpu_rec
     if e2e is not None:
         rec["e2e"] = e2e
+    if rank == 0 and world == 1 and args.config == "c2" and not args.no_extras:
+        rec["c1"] = run_c1(20000)  # BASELINE configs[0], host CPU only
     if rank == 0:
-        print(json.dumps(rec), flush=True)
+        line, detail = compact_line(rec)
+        print(json.dumps(line, separators=(",", ":")), flush=True)
+        write_detail(detail, args)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
@@ -482,6 +575,71 @@ def metric_for(kind, mode=0):
     if kind == "segment":
         return "GiB/s of device-resident send stream segmented into checksummed images; % HBM roofline (read + write)"
     return METRIC
+
+
+# ---- the printed line: numbers only, under LINE_LIMIT bytes ------------------
+# The driver keeps only the tail of stdout (BENCH_r04 kept 8.3 KB of an 11.9-KB
+# line, cutting four keys), so the line carries the numbers and every prose
+# field goes to the detail record (stderr + gpurun_out/bench_detail.json).
+LINE_LIMIT = 6000
+_TOP_CPU = ("value", "unit", "cores", "kind", "sample", "match", "min_GiBs", "max_GiBs", "one_thread_GiBs",
+            "reference_O0_GiBs", "cpu_model")
+_KEY_CPU = ("value", "cores", "kind", "match", "min_GiBs", "max_GiBs")
+
+
+def _split(d: dict, keep) -> tuple[dict, dict]:
+    return {k: v for k, v in d.items() if k in keep}, {k: v for k, v in d.items() if k not in keep}
+
+
+def compact_line(rec: dict) -> tuple[dict, dict]:
+    """(the printed line, the detail record) of a full bench record: prose,
+    pass lists and per-key descriptions move to the detail."""
+    line, detail = {}, {}
+    for k, v in rec.items():
+        if k == "settle":
+            detail[k] = v
+        elif k == "roofline":
+            line[k], rest = _split(v, ("bound", "achieved", "peak", "unit", "frac", "traffic",
+                                       "algorithmic_bytes_per_launch", "avg_launch_ms", "per_gpu_frac"))
+            detail[k] = rest
+        elif k == "cpu_baseline":
+            line[k], detail[k] = _split(v, _TOP_CPU)
+        elif k == "e2e":
+            line[k], detail[k] = _split(v, ("value", "unit", "match"))
+        elif k == "c1":
+            line[k] = v
+        elif isinstance(v, dict) and "roofline" in v and k != "config":  # an extra key
+            r = v["roofline"]
+            key = {"value": v["value"], "ms_per_step": v["ms_per_step"],
+                   "roofline": {"frac": r["frac"], "achieved": r["achieved"], "traffic": r["traffic"],
+                                "algo_bytes": r["algorithmic_bytes_per_launch"], "launch_ms": r["avg_launch_ms"]}}
+            if "per_gpu_frac" in r:
+                key["roofline"]["per_gpu_frac"] = r["per_gpu_frac"]
+            for extra in ("scaling", "kernel_GiBs", "images_total", "same_ring"):
+                if extra in v and (extra != "scaling" or v[extra] != "weak"):
+                    key[extra] = v[extra]
+            d = {kk: vv for kk, vv in v.items() if kk not in key and kk not in ("roofline", "cpu_baseline")}
+            d["traffic_source"] = r.get("traffic_source")
+            if "cpu_baseline" in v:
+                key["cpu_baseline"], d["cpu_baseline"] = _split(v["cpu_baseline"], _KEY_CPU)
+            line[k], detail[k] = key, d
+        else:
+            line[k] = v
+    line["detail"] = "stderr + gpurun_out/bench_detail.json: per-key workload, metric, sample, settle"
+    return line, detail
+
+
+def write_detail(detail: dict, args) -> None:
+    text = json.dumps(detail, separators=(",", ":"))
+    log("bench detail: " + text)
+    try:
+        d = os.path.join(ROOT, "gpurun_out")
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, "bench_detail.json" if args.config == "c2" else f"bench_detail_{args.config}.json"),
+                  "w") as f:
+            f.write(text + "\n")
+    except OSError as e:
+        log(f"bench detail not written: {e}")
 
 
 _LIB_SHA = None
@@ -557,10 +715,11 @@ def cpu_baseline(host_arena, gpu_res, sargs, sbytes, sdesc, budget_s, mode=0, se
         one, _ = passes(pk, 1, 1, 0.5)
         pk.close()
         out.update(summary(rates))
-        out.update({"kind": "reference", "one_thread_GiBs": round(one[0], 2),
-                    "sample": sdesc + f"; 7 passes of {reps} sweeps on {nthr} threads (median; min/max beside it); "
-                              "CalculateChecksum (tcp-header.h:252-263) built -O3 -march=x86-64-v3; results == GPU "
-                              f"results: {match}"})
+        out.update({"kind": "reference", "match": match, "one_thread_GiBs": round(one[0], 2),
+                    "sample": sdesc,
+                    "sample_detail": f"7 passes of {reps} sweeps on {nthr} threads (median; min/max beside it); "
+                                     "CalculateChecksum (tcp-header.h:252-263) built -O3 -march=x86-64-v3; "
+                                     "match: results == the GPU's"})
         if secondary_o0 and R.RefLib.available("O0"):
             # secondary: the reference as its makefile builds it (-O0 -g, makefile:2), same threads
             p0 = R.RefLib("O0").packets(host_arena, **sargs)
@@ -583,9 +742,9 @@ def cpu_baseline(host_arena, gpu_res, sargs, sbytes, sdesc, budget_s, mode=0, se
             rates.append(sbytes * reps / (time.perf_counter() - t0) / GIB)
         out.update(summary(rates))
         what = "RFC 1071 restatement (oracle/ref16.c oracle_rfc1071)" if mode else "oracle/ref16.c restatement"
-        out.update({"kind": "port", "sample": sdesc + f"; {what}, 7 passes of {reps} sweeps on {nthr} threads "
-                                                      f"(median; min/max beside it); results == GPU results: "
-                                                      f"{bool(np.array_equal(got, gpu_res[:n]))}"})
+        out.update({"kind": "port", "match": bool(np.array_equal(got, gpu_res[:n])), "sample": sdesc,
+                    "sample_detail": f"{what}, 7 passes of {reps} sweeps on {nthr} threads (median; min/max beside "
+                                     "it); match: results == the GPU's"})
     log(f"cpu baseline: {out['value']} GiB/s on {nthr} threads (min {out['min_GiBs']}, max {out['max_GiBs']})")
     try:
         out["cpu_model"] = open("/proc/cpuinfo").read().split("model name")[1].split("\n")[0].strip(": \t")
@@ -606,11 +765,11 @@ def cpu_baseline_for(w: "Workload", budget_s: float):
         host_arena = w.arena.cpu().numpy()
         sbytes = int(ln.astype(np.int64).sum())
         return cpu_baseline(host_arena, res, dict(offsets=off, lengths=ln), sbytes,
-                            f"all {w.count} images of the batch ({sbytes / 1e9:.2f} GB, host copy)", budget_s, w.mode)
+                            f"all {w.count} images ({sbytes / 1e9:.2f} GB, host copy)", budget_s, w.mode)
     n = CPU_EXTRA.get(w.name, (None,))[0] or w.count
     host_arena = w.arena[:n * w.L].cpu().numpy()
     sbytes = n * w.L
-    what = f"all {n} images of the batch" if n == w.count else f"the batch's first {n} images (a contiguous subset)"
+    what = f"all {n} images" if n == w.count else f"the first {n} images"
     return cpu_baseline(host_arena, res, dict(stride=w.L, length=w.L, count=n), sbytes,
                         f"{what} ({sbytes / 1e9:.2f} GB, host copy)", budget_s, w.mode,
                         secondary_o0=w.name == "c2")

@@ -102,12 +102,16 @@ const char *tcpck_strerror(int status);
 int tcpck_device_supported(int device);
 
 /* ---- context: one per device; owns no hidden global HIP state ------------
- * tcpck_ctx_create allocates the context's 16-MiB results scratch on `device`
- * (TCPCK_ENOMEM if it cannot): a FILL without a results buffer writes its
- * results there, 8M images per launch chunk, so the reference's call shape
- * (socket-manager.cc:9-10 stores into the packet only) runs the same two-pass
- * forms as a FILL with one.  Such FILLs are serialised per context: each
- * waits (on its stream, asynchronously) for the previous one's work. */
+ * A FILL without a results buffer (the reference's call shape,
+ * socket-manager.cc:9-10 stores into the packet only) whose AUTO form reads
+ * the results back writes them to one of the context's 4 results-scratch
+ * slots of 16 MiB (8M images per launch chunk), allocated on the first such
+ * call, so it runs the same two-pass forms as a FILL with a buffer.  FILLs
+ * on different streams take different slots and overlap; a slot's reuse waits
+ * (on the caller's stream, asynchronously) for its previous user's work.  On a
+ * stream under capture (HIP graphs), or when the slots cannot be allocated,
+ * such a FILL runs AUTO's in-stream form instead (same bytes, no slot, no
+ * event).  Context creation allocates nothing on the device. */
 int tcpck_ctx_create(int device, tcpck_ctx **out);
 int tcpck_ctx_destroy(tcpck_ctx *ctx);
 int tcpck_ctx_device(const tcpck_ctx *ctx);

@@ -58,6 +58,10 @@ int tcpck_probe_receive_ex(tcpck_ctx *ctx, int mode, void *d_arena, uint64_t str
  * stamps (3, 7; NULL = off). */
 int tcpck_ctx_set_debug(tcpck_ctx *ctx, void *d_buf);
 
+/* The context's results-scratch slots (tcpck.h, out-less FILL): how many are
+ * allocated and a bit per slot that a FILL has used (its event recorded). */
+int tcpck_probe_scratch_state(tcpck_ctx *ctx, int *allocated, int *used_mask);
+
 /* Timing-only streaming micro-kernel over d_buf (results are not checksums):
  * variant = chunks per lane per step x steps in flight x scan, see
  * tcp-stack_amd/csrc/tcpck_diag.hip.  d_out: u32 per wave. */

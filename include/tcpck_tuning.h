@@ -143,9 +143,14 @@ extern "C" {
  *                              update form nor the deferred-field forms (rstream
  *                              25, vvstream + 64, sstream + 128)
  * Under TCPCK_KERNEL_AUTO a FILL without a results buffer (d_out NULL, the
- * reference's call shape) writes its results into the context's scratch
- * (tcpck_ctx_create allocates 16 MiB: 8M images per launch chunk), so it
- * takes the same forms as a FILL with one. */
+ * reference's call shape) whose form reads the results back (the update form,
+ * the deferred-field forms) writes them into a context scratch slot (tcpck.h:
+ * 4 slots of 16 MiB, allocated on first use, 8M images per launch chunk), so
+ * it takes the same forms as a FILL with one; the other forms launch with no
+ * results at all.  A batch of more than 8M images on an offset list runs in
+ * 8M-image chunks whose layout hint keeps the flags and length bounds and
+ * scales total_bytes with the chunk's count, so AUTO sees the batch's own
+ * typical image in every chunk. */
 #define TCPCK_PARAM_FILL_UPDATE (1 << 28)
 #define TCPCK_PARAM_FILL_INSTREAM (1 << 29)
 /* RECEIVE into a header array (tcpck_batch_receive_ex): where the VERIFY kernel

@@ -149,11 +149,13 @@ int ensure_stage(tcpck_ctx *ctx, uint64_t bytes, uint64_t images) {
 }
 
 void free_stage(tcpck_ctx *ctx) {
-  if (ctx->scratch_ev) {
-    (void)hipEventSynchronize(ctx->scratch_ev);
-    (void)hipEventDestroy(ctx->scratch_ev);
+  for (auto &slot : ctx->scratch) {
+    if (slot.ev) {
+      (void)hipEventSynchronize(slot.ev);
+      (void)hipEventDestroy(slot.ev);
+    }
+    if (slot.buf) (void)hipFree(slot.buf);
   }
-  if (ctx->scratch) (void)hipFree(ctx->scratch);
   if (ctx->side) {
     (void)hipEventDestroy(ctx->fork);
     (void)hipEventDestroy(ctx->join);
@@ -267,6 +269,23 @@ struct CallerBits {
   explicit CallerBits(int param)
       : two_pass((param & TCPCK_PARAM_RECEIVE_TWO_PASS) != 0), instream((param & TCPCK_PARAM_FILL_INSTREAM) != 0) {}
 };
+
+// FILL under AUTO with a results buffer on a fixed layout: whether AUTO's
+// kernel takes its deferred form (the stream writes the results only, the
+// write-through field pass stores them from the results; see run_fixed_impl).
+bool fixed_fill_defers(int kernel, int param, uint64_t stride, uint32_t len) {
+  switch (kernel) {
+    case TCPCK_KERNEL_RSTREAM: return stride >= 30 && (param & 0xFF) == kRstreamPolicy;
+    case TCPCK_KERNEL_SSTREAM: return len >= kDeferFillMinLen;
+    case TCPCK_KERNEL_VVSTREAM: return len >= (stride == len ? kVvDeferPackedMin : kDeferFillMinLen);
+    default: return false;
+  }
+}
+
+// The same on an offset list (run_var_impl): vvstream from kDeferFillMinVar.
+bool var_fill_defers(int kernel, uint64_t typical) {
+  return kernel == TCPCK_KERNEL_VVSTREAM && typical >= kDeferFillMinVar;
+}
 
 // AUTO's kernel for a fixed layout: sets kernel (from TCPCK_KERNEL_AUTO) and
 // its param (measurements in DESIGN.md section 4).
@@ -396,8 +415,8 @@ hipError_t run_fixed_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint
   // images; written through to HBM in their own pass they cost 38 us (C2:
   // 280 -> 248 us, scripts/fill_drain_probe.py, profiles/r03/fill_*.log)
   // (TCPCK_PARAM_FILL_INSTREAM keeps the in-stream form)
-  if (auto_pick && !caller.instream && kernel == TCPCK_KERNEL_RSTREAM && op == TCPCK_OP_FILL && out && stride >= 30 &&
-      (param & 0xFF) == kRstreamPolicy)
+  const bool may_defer = auto_pick && !caller.instream && op == TCPCK_OP_FILL && out;
+  if (may_defer && kernel == TCPCK_KERNEL_RSTREAM && fixed_fill_defers(kernel, param, stride, len))
     param = (param & ~0xFF) | kRstreamDeferFill;
   if (kernel == TCPCK_KERNEL_RSTREAM) {
     if (stride != len || len < 16 || len > (1u << 24)) return hipErrorInvalidValue;
@@ -431,8 +450,7 @@ hipError_t run_fixed_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint
     return tcpck::launch_gstream(op, param & 0xFFFF, a, num_cus, s);
   }
   if (kernel == TCPCK_KERNEL_SSTREAM) {  // fixed slots: stride % 16 == 0, stride >= len
-    if (auto_pick && !caller.instream && op == TCPCK_OP_FILL && out && len >= kDeferFillMinLen)
-      param |= kSstreamDeferFill;
+    if (may_defer && fixed_fill_defers(kernel, param, stride, len)) param |= kSstreamDeferFill;
     if (param & kSstreamDeferFill) *patch = true;
     if (count == 1) stride = (static_cast<uint64_t>(len) + 15) & ~uint64_t{15};  // one image: never read
     if (!tcpck::sstream_fixed_applies(stride, len) || (op == TCPCK_OP_FILL && len < 30) ||
@@ -454,8 +472,7 @@ hipError_t run_fixed_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint
   }
   if (kernel == TCPCK_KERNEL_VVSTREAM) {  // any even length: the prefix table takes any number of ends per step
     if (len == 0 || stride > (1u << 24) || (op == TCPCK_OP_FILL && len < 30)) return hipErrorInvalidValue;
-    if (auto_pick && !caller.instream && op == TCPCK_OP_FILL && out &&
-        len >= (stride == len ? kVvDeferPackedMin : kDeferFillMinLen))
+    if (may_defer && fixed_fill_defers(kernel, param, stride, len))
       param = (param & ~kVvKeep) | kVvDeferFill;  // (the default-policy reads served the in-stream stores)
     if (param & kVvDeferFill) *patch = true;
     if (mode != TCPCK_MODE_REF && (len >= (1u << 17) || (param & 32))) return hipErrorInvalidValue;
@@ -623,7 +640,7 @@ hipError_t run_var_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const 
   if (kernel == TCPCK_KERNEL_VVSTREAM) {
     if (mode != TCPCK_MODE_REF && (param & 32)) return hipErrorInvalidValue;
     // (REF packed batches of typical >= 448 B take the update form in run_var)
-    if (auto_pick && !caller.instream && op == TCPCK_OP_FILL && out && patch && typical >= kDeferFillMinVar)
+    if (auto_pick && !caller.instream && op == TCPCK_OP_FILL && out && patch && var_fill_defers(kernel, typical))
       param |= kVvDeferFill;
     if (param & kVvDeferFill) {
       if (!patch) return hipErrorInvalidValue;
@@ -758,27 +775,101 @@ hipError_t run_var(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const uint6
 namespace {
 
 // FILL without a results buffer under AUTO (the reference's call shape,
-// socket-manager.cc:9-10): the results go to the ctx scratch so AUTO keeps
-// the forms that need them (rstream's deferred fields, vvstream's update pass:
-// C2 in-stream 69.3 % -> 76-77 %, C3 53.7 -> 62 %, profiles/r03/fill_forms.log).
-bool use_scratch(const tcpck_ctx *ctx, int op, const void *out, int kernel) {
-  return op == TCPCK_OP_FILL && !out && kernel == TCPCK_KERNEL_AUTO && ctx->scratch;
+// socket-manager.cc:9-10): when AUTO's form for the layout reads the results
+// back -- rstream's and vvstream's deferred fields, the update pass (C2
+// in-stream 69.3 % -> 76-77 %, C3 53.7 -> 62 %, profiles/r03/fill_forms.log)
+// -- the results go to a ctx scratch slot; every other form (gstream, seg,
+// the in-stream run forms) launches with out = NULL and takes no slot.
+bool fill_reads_results_fixed(int mode, const uint8_t *arena, uint64_t stride, uint32_t len, int param) {
+  if (param & TCPCK_PARAM_FILL_INSTREAM) return false;
+  const int dummy = 0;
+  if (stride >= 30 && fill_by_update(TCPCK_OP_FILL, mode, &dummy, TCPCK_KERNEL_AUTO, param, true, stride, len))
+    return true;
+  int k = TCPCK_KERNEL_AUTO, p = param;
+  pick_fixed(TCPCK_OP_FILL, mode, arena, stride, len, k, p);
+  return fixed_fill_defers(k, p, stride, len);
 }
 
-// launch(k0, n, results) for images [k0, k0 + n), n <= scratch_images.  Calls
-// are serialised per ctx, and each first waits for the previous use's event
-// (recorded after every use): always, not only when the stream differs -- a
-// destroyed stream's handle can come back for a new stream while the old one's
-// work still runs.
-template <typename Launch>
-hipError_t with_scratch(tcpck_ctx *ctx, uint64_t count, hipStream_t s, Launch launch) {
+bool fill_reads_results_var(int mode, const tcpck_layout *layout, uint64_t count, int param) {
+  if (param & TCPCK_PARAM_FILL_INSTREAM) return false;
+  const int dummy = 0;
+  if (fill_by_update(TCPCK_OP_FILL, mode, &dummy, TCPCK_KERNEL_AUTO, param, false, 0, 0, layout, count)) return true;
+  int k = TCPCK_KERNEL_AUTO, p = param;
+  bool fuse_small = false;
+  pick_var(TCPCK_OP_FILL, mode, layout, count, false, false, k, p, fuse_small);
+  const uint64_t typical = (layout && layout->total_bytes) ? layout->total_bytes / count : 1500;
+  return var_fill_defers(k, typical);
+}
+
+// A scratch slot for one out-less FILL, its mutex held (nullptr: none, the
+// caller runs the in-stream form).  None while `s` is under stream capture:
+// a captured event record would order later uncaptured FILLs against a graph
+// node, and a replayed graph would share the slot with no ordering at all.
+tcpck_ctx::ScratchSlot *take_scratch(tcpck_ctx *ctx, hipStream_t s, std::unique_lock<std::mutex> &held) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cs) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  if (cs != hipStreamCaptureStatusNone) return nullptr;
   std::lock_guard<std::mutex> lk(ctx->scratch_mu);
+  if (ctx->scratch_failed) return nullptr;
+  if (!ctx->scratch[0].buf) {  // first use: every slot, or none
+    for (auto &slot : ctx->scratch) {
+      void *p = nullptr;
+      hipEvent_t ev = nullptr;
+      if (hipMalloc(&p, tcpck::api::kScratchImages * 2) != hipSuccess ||
+          hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+        if (p) (void)hipFree(p);
+        (void)hipGetLastError();
+        for (auto &sl : ctx->scratch) {
+          if (sl.buf) (void)hipFree(sl.buf);
+          if (sl.ev) (void)hipEventDestroy(sl.ev);
+          sl.buf = nullptr;
+          sl.ev = nullptr;
+        }
+        ctx->scratch_failed = true;
+        return nullptr;
+      }
+      slot.buf = static_cast<uint16_t *>(p);
+      slot.ev = ev;
+    }
+    ctx->scratch_images = tcpck::api::kScratchImages;
+  }
+  // an idle slot (never used, or its last user's work done), else the next in turn
+  constexpr int n = tcpck_ctx::kScratchSlots;
+  int pick = -1;
+  for (int i = 0; i < n && pick < 0; ++i) {
+    auto &slot = ctx->scratch[(ctx->scratch_next + i) % n];
+    std::unique_lock<std::mutex> try_lk(slot.mu, std::try_to_lock);
+    if (!try_lk.owns_lock()) continue;
+    if (!slot.used || hipEventQuery(slot.ev) == hipSuccess) {
+      pick = static_cast<int>((ctx->scratch_next + i) % n);
+      held = std::move(try_lk);
+    }
+  }
+  (void)hipGetLastError();  // hipEventQuery's hipErrorNotReady
+  if (pick < 0) {
+    pick = static_cast<int>(ctx->scratch_next % n);
+    held = std::unique_lock<std::mutex>(ctx->scratch[pick].mu);
+  }
+  ctx->scratch_next = static_cast<unsigned>(pick + 1);
+  return &ctx->scratch[pick];
+}
+
+// launch(k0, n, results) for images [k0, k0 + n), n <= scratch_images, with
+// the slot's previous use waited for first (always, not only when the stream
+// differs -- a destroyed stream's handle can come back for a new stream while
+// the old one's work still runs) and the slot's event recorded after.
+template <typename Launch>
+hipError_t with_scratch(tcpck_ctx *ctx, tcpck_ctx::ScratchSlot *slot, uint64_t count, hipStream_t s,
+                        Launch launch) {
   hipError_t e = hipSuccess;
-  if (ctx->scratch_used) e = hipStreamWaitEvent(s, ctx->scratch_ev, 0);
+  if (slot->used) e = hipStreamWaitEvent(s, slot->ev, 0);
   for (uint64_t k0 = 0; k0 < count && e == hipSuccess; k0 += ctx->scratch_images)
-    e = launch(k0, std::min(ctx->scratch_images, count - k0), ctx->scratch);
-  const hipError_t er = hipEventRecord(ctx->scratch_ev, s);
-  if (er == hipSuccess) ctx->scratch_used = true;
+    e = launch(k0, std::min(ctx->scratch_images, count - k0), slot->buf);
+  const hipError_t er = hipEventRecord(slot->ev, s);
+  if (er == hipSuccess) slot->used = true;
   return e != hipSuccess ? e : er;
 }
 
@@ -800,11 +891,15 @@ int batch_fixed_ex(tcpck_ctx *ctx, int op, int mode, void *d_arena, uint64_t str
   DeviceGuard g(ctx->device);
   if (g.status() != hipSuccess) return hip_status(g.status());
   auto *arena = static_cast<uint8_t *>(d_arena);
-  if (use_scratch(ctx, op, d_out, kernel))
-    return hip_status(with_scratch(ctx, count, s, [&](uint64_t k0, uint64_t n, uint16_t *res) {
-      return run_fixed(ctx, op, mode, arena + k0 * stride, n == 1 ? len : stride, len, n, res, kernel, param, s,
-                       nullptr, hk);
-    }));
+  if (op == TCPCK_OP_FILL && !d_out && kernel == TCPCK_KERNEL_AUTO &&
+      fill_reads_results_fixed(mode, arena, stride, len, param)) {
+    std::unique_lock<std::mutex> held;
+    if (auto *slot = take_scratch(ctx, s, held))
+      return hip_status(with_scratch(ctx, slot, count, s, [&](uint64_t k0, uint64_t n, uint16_t *res) {
+        return run_fixed(ctx, op, mode, arena + k0 * stride, n == 1 ? len : stride, len, n, res, kernel, param, s,
+                         nullptr, hk);
+      }));
+  }
   return hip_status(run_fixed(ctx, op, mode, arena, stride, len, count, d_out, kernel, param, s, nullptr, hk));
 }
 
@@ -818,16 +913,24 @@ int batch_var_ex(tcpck_ctx *ctx, int op, int mode, void *d_arena, const uint64_t
   DeviceGuard g(ctx->device);
   if (g.status() != hipSuccess) return hip_status(g.status());
   auto *arena = static_cast<uint8_t *>(d_arena);
-  if (use_scratch(ctx, op, d_out, kernel))
-    return hip_status(with_scratch(ctx, count, s, [&](uint64_t k0, uint64_t n, uint16_t *res) {
-      tcpck_layout sub{};
-      if (layout) {
-        sub = *layout;  // a sub-range keeps the flags and the length bounds; the byte hint scales
-        sub.total_bytes = static_cast<uint64_t>(static_cast<unsigned __int128>(layout->total_bytes) * n / count);
-      }
-      return run_var(ctx, op, mode, arena, d_offsets + k0, d_lengths + k0, 0, n, res, layout ? &sub : nullptr, kernel,
-                     param, s, nullptr, hk);
-    }));
+  if (op == TCPCK_OP_FILL && !d_out && kernel == TCPCK_KERNEL_AUTO &&
+      fill_reads_results_var(mode, layout, count, param)) {
+    std::unique_lock<std::mutex> held;
+    if (auto *slot = take_scratch(ctx, s, held))
+      return hip_status(with_scratch(ctx, slot, count, s, [&](uint64_t k0, uint64_t n, uint16_t *res) {
+        tcpck_layout sub{};
+        if (layout) {
+          // a sub-range keeps the flags and the length bounds, and its byte hint
+          // scales with its image count, so its typical image -- the quantity
+          // AUTO chooses by -- is the whole batch's and every chunk runs the
+          // same form (tcpck_tuning.h)
+          sub = *layout;
+          sub.total_bytes = static_cast<uint64_t>(static_cast<unsigned __int128>(layout->total_bytes) * n / count);
+        }
+        return run_var(ctx, op, mode, arena, d_offsets + k0, d_lengths + k0, 0, n, res, layout ? &sub : nullptr,
+                       kernel, param, s, nullptr, hk);
+      }));
+  }
   return hip_status(run_var(ctx, op, mode, arena, d_offsets, d_lengths, 0, count, d_out, layout, kernel, param, s,
                             nullptr, hk));
 }
@@ -954,22 +1057,7 @@ int tcpck_ctx_create(int device, tcpck_ctx **out) {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
     ctx->num_cus = prop.multiProcessorCount;
-  {
-    // the results scratch of FILL without a results buffer (tcpck_api_internal.h)
-    DeviceGuard g(device);
-    void *p = nullptr;
-    hipEvent_t ev = nullptr;
-    if (g.status() != hipSuccess || hipMalloc(&p, tcpck::api::kScratchImages * 2) != hipSuccess ||
-        hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
-      if (p) (void)hipFree(p);
-      (void)hipGetLastError();
-      delete ctx;
-      return TCPCK_ENOMEM;
-    }
-    ctx->scratch = static_cast<uint16_t *>(p);
-    ctx->scratch_images = tcpck::api::kScratchImages;
-    ctx->scratch_ev = ev;
-  }
+  // (the results scratch of out-less FILLs is allocated on first use: take_scratch)
   *out = ctx;
   return TCPCK_OK;
 }

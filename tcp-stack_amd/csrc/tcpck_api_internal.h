@@ -32,16 +32,26 @@ struct tcpck_ctx {
   uint64_t chunk_bytes = 64ull << 20;
 
   // FILL without a results buffer (the reference's insert stores only into the
-  // packet, socket-manager.cc:9-10): the results go to this ctx-owned scratch,
-  // allocated at tcpck_ctx_create, so AUTO keeps its two-pass forms (the stream
-  // writes the results, the write-through field pass stores them).  Batches of
-  // more images run in chunks.  `scratch_ev` is recorded after every use and
-  // every later use waits for it first.
+  // packet, socket-manager.cc:9-10) where AUTO's form reads the results back
+  // (the stream writes them, the write-through field pass stores them): the
+  // results go to one of kScratchSlots ctx-owned slots, allocated on first use.
+  // A call takes an idle slot (or, all busy, the next in turn) under
+  // `scratch_mu`, then holds that slot's own mutex while it waits on the
+  // slot's event, launches and records the event again -- so FILLs from
+  // several threads on several streams overlap, and a slot's reuse still waits
+  // for its previous user's work.  Batches of more images run in chunks.
+  struct ScratchSlot {
+    std::mutex mu;
+    uint16_t *buf = nullptr;
+    hipEvent_t ev = nullptr;
+    bool used = false;  // ev recorded at least once
+  };
+  static constexpr int kScratchSlots = 4;
   std::mutex scratch_mu;
-  uint16_t *scratch = nullptr;
+  ScratchSlot scratch[kScratchSlots];
   uint64_t scratch_images = 0;
-  hipEvent_t scratch_ev = nullptr;
-  bool scratch_used = false;
+  unsigned scratch_next = 0;
+  bool scratch_failed = false;  // allocation refused once: in-stream forms from then on
 
   // probe library only (tcpck_ex_probe.hip): per-wave time stamp buffer, and the
   // side stream + events of the concurrent RECEIVE form

@@ -10,7 +10,7 @@
 //   * tcpck_batch_receive_ex: with an explicit kernel, the headers fused into
 //     any kernel that can (sstream's after-the-verdicts conversion, HDR 1);
 //   * tcpck_probe_receive_ex: the header pass forms (TCPCK_PROBE_RECEIVE_*);
-//   * tcpck_ctx_set_debug, tcpck_diag_stream.
+//   * tcpck_ctx_set_debug, tcpck_diag_stream, tcpck_probe_scratch_state.
 #include <hip/hip_runtime.h>
 
 #include <mutex>
@@ -171,6 +171,19 @@ int tcpck_diag_stream(tcpck_ctx *ctx, int variant, const void *d_buf, uint64_t b
 int tcpck_ctx_set_debug(tcpck_ctx *ctx, void *d_buf) {
   if (!ctx) return TCPCK_EINVAL;
   ctx->dbg = d_buf;
+  return TCPCK_OK;
+}
+
+int tcpck_probe_scratch_state(tcpck_ctx *ctx, int *allocated, int *used_mask) {
+  if (!ctx || !allocated || !used_mask) return TCPCK_EINVAL;
+  std::lock_guard<std::mutex> lk(ctx->scratch_mu);
+  *allocated = 0;
+  *used_mask = 0;
+  for (int i = 0; i < tcpck_ctx::kScratchSlots; ++i) {
+    std::lock_guard<std::mutex> sl(ctx->scratch[i].mu);
+    if (ctx->scratch[i].buf) ++*allocated;
+    if (ctx->scratch[i].used) *used_mask |= 1 << i;
+  }
   return TCPCK_OK;
 }
 

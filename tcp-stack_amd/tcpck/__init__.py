@@ -57,7 +57,7 @@ SEG_SHAPES = {1: "G8/U2", 2: "G16/U6", 3: "G64/U4", 4: "G64/U2", 5: "G32/U3", 6:
 # include/tcpck_tuning.h: in libtcpck.so (AUTO's kernels only) and libtcpck_probe.so
 TUNING_EXPORTS = ("tcpck_batch_fixed_ex", "tcpck_batch_var_ex", "tcpck_batch_segment_ex", "tcpck_batch_receive_ex")
 # include/tcpck_tuning.h, measurement only: libtcpck_probe.so
-PROBE_EXPORTS = ("tcpck_ctx_set_debug", "tcpck_diag_stream", "tcpck_probe_receive_ex")
+PROBE_EXPORTS = ("tcpck_ctx_set_debug", "tcpck_diag_stream", "tcpck_probe_receive_ex", "tcpck_probe_scratch_state")
 # include/tcpck_probe.h: tcpck_probe_receive_ex's flags word (the header pass forms)
 PROBE_RECEIVE_HDR_FIRST = 1    # offset lists, with PARAM_RECEIVE_TWO_PASS: header pass first
 PROBE_RECEIVE_CONCURRENT = 2   # header pass on a side stream beside VERIFY
@@ -176,6 +176,7 @@ def lib(probe: bool = False) -> ctypes.CDLL:
         "tcpck_batch_fixed_ex": (i32, [vp, i32, i32, vp, u64, u32, u64, vp, i32, i32, vp]),
         "tcpck_batch_var_ex": (i32, [vp, i32, i32, vp, vp, vp, u64, vp, ctypes.POINTER(Layout), i32, i32, vp]),
         "tcpck_ctx_set_debug": (i32, [vp, vp]),
+        "tcpck_probe_scratch_state": (i32, [vp, ctypes.POINTER(i32), ctypes.POINTER(i32)]),
         "tcpck_diag_stream": (i32, [vp, i32, vp, u64, vp, vp]),
         "tcpck_probe_receive_ex": (i32, [vp, i32, vp, u64, u32, vp, vp, u64, vp, vp, ctypes.POINTER(Layout), i32, i32,
                                          i32, vp]),
@@ -399,6 +400,14 @@ class Context:
     def set_debug(self, buf) -> None:
         """Per-wave {start, end, hw_id, xcc_id} stamp buffer for timing builds (None = off)."""
         _check(self._L.tcpck_ctx_set_debug(self._h, _ptr(buf)), "tcpck_ctx_set_debug")
+
+    def scratch_state(self) -> tuple[int, int]:
+        """(slots allocated, bit mask of slots used) of the out-less FILL results
+        scratch (libtcpck_probe.so only, tcpck_probe.h)."""
+        a, m = ctypes.c_int(), ctypes.c_int()
+        _check(self._L.tcpck_probe_scratch_state(self._h, ctypes.byref(a), ctypes.byref(m)),
+               "tcpck_probe_scratch_state")
+        return a.value, m.value
 
     def set_chunk_bytes(self, n: int) -> None:
         _check(self._L.tcpck_ctx_set_chunk_bytes(self._h, n), "tcpck_ctx_set_chunk_bytes")

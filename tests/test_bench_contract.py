@@ -55,3 +55,102 @@ def test_metric_per_kind():
     for n, _ in bench.EXTRAS:
         kind = bench.CONFIGS[n][1] if n in bench.CONFIGS else bench.EXTRA[n][1]
         assert bench.metric_for(kind).startswith("GiB/s")
+
+
+def _env_without_launcher():
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    env["TCPCK_BENCH_BACKEND"] = "gloo"
+    return env
+
+
+def test_bare_gpus_n_spawns_n_ranks():
+    """`python bench.py --gpus N` run bare (the driver's command
+    has no launcher) must start N ranks, not print a 1-GPU line.  The launch
+    check starts them through bench.py's own child torch.distributed.run and
+    gathers every rank's (rank, local rank) over gloo -- no GPU."""
+    import json
+    import subprocess
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--launch-check"],
+                       capture_output=True, text=True, timeout=240, env=_env_without_launcher(), cwd="/tmp")
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line == {"n_gpus": 2, "gpus_arg": 2, "ranks": [[0, 0], [1, 1]]}
+
+
+def test_launcher_world_mismatch_fails():
+    """A launcher that started another rank count than --gpus is an error (rc 2), not a silent N-line."""
+    import subprocess
+    env = _env_without_launcher()
+    env.update(WORLD_SIZE="3", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--launch-check"],
+                       capture_output=True, text=True, timeout=120, env=env, cwd="/tmp")
+    assert r.returncode == 2 and "WORLD_SIZE 3" in r.stderr
+
+
+def _full_record(world=1):
+    """A bench record as main() assembles it before compact_line, every prose
+    field at its real length and every number at full width."""
+    long = "x" * 240
+    roof = {"bound": "hbm", "achieved": 7454.1234, "peak": 8000.0, "unit": "GB/s", "frac": 0.93181,
+            "traffic": 1566653440, "traffic_source": long, "algorithmic_bytes_per_launch": 17180393472,
+            "avg_launch_ms": 2.310341}
+    if world > 1:
+        roof["per_gpu_frac"] = [0.9318] * world
+    cpu = {"unit": "GiB/s", "cores": 16, "affinity_cpus": 256, "nproc": 256, "omp_num_threads": 16,
+           "value": 123.45, "min_GiBs": 120.01, "max_GiBs": 125.99, "passes_GiBs": [123.4] * 7, "kind": "reference",
+           "match": True, "one_thread_GiBs": 9.87, "sample": "all 1048576 images (1.56 GB, host copy)",
+           "sample_detail": long, "reference_O0_GiBs": 1.23, "reference_O0_note": long, "cpu_model": "A" * 48}
+    rec = {"metric": bench.METRIC, "value": 6946.12, "unit": "GiB/s", "n_gpus": world, "steps": 20, "warmup": 5,
+           "ms_per_step": 0.21199, "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u16",
+           "data": "synthetic (device-generated: send-path headers + splitmix64 payloads, seed 42)",
+           "config": {"workload": bench.CONFIGS["c2"][0], "images_per_gpu": 1 << 20, "image_bytes": 1492,
+                      "bytes_per_gpu": 1564475392, "parallelism": "shard1 (independent per-GPU batches, no collective)"},
+           "roofline": dict(roof), "settle": {"ms": 250.3, "launches": 1184}}
+    for name, key in bench.EXTRAS:
+        desc = bench.CONFIGS[name][0] if name in bench.CONFIGS else bench.EXTRA[name][0]
+        kind = bench.CONFIGS[name][1] if name in bench.CONFIGS else bench.EXTRA[name][1]
+        r = {"workload": desc, "metric": bench.metric_for(kind), "value": 6946.12, "unit": "GiB/s",
+             "ms_per_step": 0.212345, "scaling": "strong" if name in bench.STRONG else "weak",
+             "images_per_gpu": 4194304, "bytes_per_gpu": 3070000000, "roofline": dict(roof),
+             "settle": {"ms": 250.3, "launches": 1184}}
+        if name in bench.CPU_EXTRA:
+            r["cpu_baseline"] = dict(cpu)
+        if name in bench.STRONG:
+            r.update(kernel_GiBs=6946.12, images_total=8 << 20, parallelism="shard8: " + long)
+        if kind in ("slots", "receive"):
+            r["same_ring"] = {"value": 5123.45, "frac": 0.7512}
+        rec[key] = r
+    rec["cpu_baseline"] = dict(cpu)
+    rec["e2e"] = {"value": 49.19, "unit": "GiB/s", "match": True, "what": long}
+    rec["c1"] = {"value": 2.812, "unit": "us/segment", "segments": 20000, "received": 20000, "verified": 20000,
+                 "send_ck_ns": 123.4, "recv_ck_ns": 120.1,
+                 "cpu_baseline": {"value": 2.9, "unit": "us/segment", "cores": 1, "kind": "reference",
+                                  "verified": 20000, "send_ck_ns": 400.1, "recv_ck_ns": 390.2}}
+    return rec
+
+
+def test_line_fits_the_driver_tail():
+    """the driver keeps ~8.3 KB of stdout; the line stays under
+    bench.LINE_LIMIT (6 KB) with every key's numbers in it, at N=1 and N=8."""
+    import json
+    for world in (1, 8):
+        line, detail = bench.compact_line(_full_record(world))
+        text = json.dumps(line, separators=(",", ":"))
+        assert len(text) < bench.LINE_LIMIT, len(text)
+        for _, key in bench.EXTRAS:
+            k = line[key]
+            assert {"value", "ms_per_step", "roofline"} <= set(k), key
+            assert {"frac", "achieved", "traffic", "algo_bytes", "launch_ms"} <= set(k["roofline"]), key
+            assert "workload" in detail[key] and "metric" in detail[key]
+        for key in ("c3", "c4", "c2_rfc"):
+            assert {"value", "min_GiBs", "max_GiBs", "match", "kind", "cores"} <= set(line[key]["cpu_baseline"])
+        # the contract's top-level fields
+        for f in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+                  "scaling", "vs_baseline", "dtype", "data", "config"):
+            assert f in line, f
+        assert {"bound", "achieved", "peak", "unit", "frac", "traffic"} <= set(line["roofline"])
+        assert {"value", "unit", "cores", "kind", "sample"} <= set(line["cpu_baseline"])
+        assert line["c1"]["verified"] == line["c1"]["segments"]
+        assert line["receive"]["same_ring"]["frac"] > 0
