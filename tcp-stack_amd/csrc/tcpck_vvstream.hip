@@ -33,6 +33,14 @@
 //     lane whose image start + 28 falls in the step posts the word to the
 //     chunk's lane through LDS (images >= 30 B: one field per chunk at most)
 //     -- and the result is stored to out[k] and into the field;
+//   * kFill + BLK (flag 128, images >= 64 B, reference mode, no gaps): each
+//     field leaves as its whole 64-B block, written through from the step's
+//     own registers (unmasked) with the checksum in place -- a whole-block
+//     store needs no merge read at the memory side, a 2-B store does.  The
+//     field lane's chunk gets the word; the block's 4 lanes store.  The one
+//     image that can cross a step boundary with its field before the
+//     boundary has its block staged in LDS (64 B per wave) until its end is
+//     resolved.  Blocks reaching outside the batch's bytes take the 2-B store;
 //   * a wave whose lengths disagree with the offsets (layout hint wrong)
 //     recomputes its images one by one.  kFill checks this before it writes
 //     anything into the arena.
@@ -79,15 +87,35 @@ __device__ __forceinline__ u32x4 zero_word(u32x4 w, uint32_t wi) {
   return w;
 }
 
+// Word wi (0..7) of a 16-byte chunk set to v.
+__device__ __forceinline__ u32x4 put_word(u32x4 w, uint32_t wi, uint32_t v) {
+  const uint32_t sh = (wi & 1u) << 4;
+  const uint32_t m = ~(0xFFFFu << sh), x = (v & 0xFFFFu) << sh;
+  const uint32_t di = wi >> 1;
+  w.x = di == 0 ? (w.x & m) | x : w.x;
+  w.y = di == 1 ? (w.y & m) | x : w.y;
+  w.z = di == 2 ? (w.z & m) | x : w.z;
+  w.w = di == 3 ? (w.w & m) | x : w.w;
+  return w;
+}
+
+__device__ __forceinline__ void store16_chunk_wt(__amdgpu_buffer_rsrc_t r, uint32_t voff, u32x4 v) {
+  typedef unsigned v4u __attribute__((ext_vector_type(4)));
+  __builtin_amdgcn_raw_buffer_store_b128(v4u{v.x, v.y, v.z, v.w}, r, static_cast<int>(voff), 0, 19);  // sc0 sc1 nt
+}
+
 // LAYOUT: 0 packed variable, 1 fixed packed (stride == len), 2 fixed gapped
 // MODE kRfc1071: the prefix table holds exact u32 sums -- u32 P at the dword
 // positions when every end is 4-B aligned (as in REF), else u32 P at every
 // word position (twice the LDS of REF's packed u16 table) -- so P(end) -
 // P(start) is an image's exact word sum and folds
-template <int U, int OP, int SPLIT, int LAYOUT, bool KEEP = false, int MODE = kRef>
+template <int U, int OP, int SPLIT, int LAYOUT, bool KEEP = false, int MODE = kRef, bool BLK = false>
 __global__ void __launch_bounds__(kBlock) vvstream_kernel(VVArgs a) {
   constexpr bool FIXED = LAYOUT != 0;
   constexpr bool GAP = LAYOUT == 2;
+  static_assert(!BLK || (OP == kFill && !GAP && MODE == kRef && !KEEP), "BLK: reference-mode FILL, no gaps");
+  constexpr uint32_t kMinFill = BLK ? 64u : 30u;  // BLK: one field per 64-B block
+  __shared__ u32x4 s_blk[kWavesPerBlock][BLK ? 4 : 1];  // BLK: the staged block of the image crossing the step
   __shared__ uint32_t s_end[kWavesPerBlock][FIXED ? 1 : kRing + kMirror];
   __shared__ __attribute__((aligned(16))) uint32_t s_pre[kWavesPerBlock][MODE == kRef ? 256 : 512];  // the step's prefixes
   __shared__ uint32_t s_fld[kWavesPerBlock][OP == kFill ? 64 : 1];              // kFill: field word + 1 per chunk
@@ -153,7 +181,23 @@ __global__ void __launch_bounds__(kBlock) vvstream_kernel(VVArgs a) {
     const uint32_t span = static_cast<uint32_t>(s1 - A0);
     const uint32_t nsteps = (span + 1023) >> 10;
     const uint32_t last_chunk = span > 0 ? (span - 1) >> 4 : 0;
-    const auto rsrc = dev::make_rsrc(arena + A0, (last_chunk + 1) << 4);
+    // BLK: the batch's bytes, run-relative: a block is stored whole only inside
+    // them, and the buffer covers the blocks of the run's fields that reach
+    // past its span (their bytes belong to the next run's images, read here)
+    int64_t blo = 0, bhi = 0;
+    uint32_t extent = (last_chunk + 1) << 4;
+    if constexpr (BLK) {
+      const uint64_t b0 = FIXED ? 0 : a.offsets[0] - a.base;
+      const uint64_t b1 = FIXED ? (N - 1) * S + L : a.offsets[N - 1] - a.base + a.lengths[N - 1];
+      blo = static_cast<int64_t>(b0) - static_cast<int64_t>(A0);
+      bhi = static_cast<int64_t>(b1) - static_cast<int64_t>(A0);
+      const int64_t want = min(static_cast<int64_t>((span + 63u) & ~63u), bhi & ~int64_t{15});
+      if (want > static_cast<int64_t>(extent)) extent = static_cast<uint32_t>(want);
+    }
+    const auto rsrc = dev::make_rsrc(arena + A0, extent);
+    // BLK: the 64-B block at run-relative b lies inside the batch
+    auto whole = [&](uint32_t b) { return static_cast<int64_t>(b) >= blo && static_cast<int64_t>(b) + 64 <= bhi; };
+    uint32_t stage_f = 0;  // BLK: the staged field (run-relative), 0 = none
     // KEEP (kFill, small images): every line holds a checksum field, so read
     // it with the default policy -- still in L2 when the field store lands, it
     // leaves as a whole line instead of a masked partial write (gstream's
@@ -230,7 +274,7 @@ __global__ void __launch_bounds__(kBlock) vvstream_kernel(VVArgs a) {
         const uint32_t jb = r * kRound + 4 * lane;
         bool sh = false;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) sh |= (jb + i < nimg) && d[i] < 30;
+        for (int i = 0; i < 4; ++i) sh |= (jb + i < nimg) && d[i] < kMinFill;
         short_fill |= __ballot(sh) != 0;
       }
       // ends past the batch read as ~0 (never inside a step)
@@ -270,7 +314,7 @@ __global__ void __launch_bounds__(kBlock) vvstream_kernel(VVArgs a) {
           for (uint32_t j = lane; j < nimg; j += 64) {
             const uint32_t l = lens[j];
             sum += l;
-            sh |= l < 30 || (MODE == kRfc1071 && l >= (1u << 17));  // (RFC 1071: as fill_round)
+            sh |= l < kMinFill || (MODE == kRfc1071 && l >= (1u << 17));  // (RFC 1071: as fill_round)
           }
           short_fill = short_fill || __ballot(sh) != 0;
           bad = bad || short_fill || lead + dev::group_sum<64>(sum) != span;
@@ -279,7 +323,7 @@ __global__ void __launch_bounds__(kBlock) vvstream_kernel(VVArgs a) {
         }
       }
     } else {
-      if constexpr (OP == kFill) bad = L < 30;
+      if constexpr (OP == kFill) bad = L < kMinFill;
     }
     auto end_of = [&](uint32_t j) -> uint32_t {  // run-relative end of run image j (j < nimg)
       if constexpr (GAP) {
@@ -311,6 +355,7 @@ __global__ void __launch_bounds__(kBlock) vvstream_kernel(VVArgs a) {
           const uint32_t sb = st << 10;
           const uint32_t c = sb + (lane << 4);
           u32x4 w = ring[u];
+          const u32x4 raw = w;  // BLK: the block stores write the unmasked bytes
           if (sb == 0 || sb + 1024 > span) {
             const int32_t lo = min(max(static_cast<int32_t>(lead) - static_cast<int32_t>(c), 0), 16);
             const int32_t hi = min(max(static_cast<int32_t>(span) - static_cast<int32_t>(c), 0), 16);
@@ -381,7 +426,22 @@ __global__ void __launch_bounds__(kBlock) vvstream_kernel(VVArgs a) {
               const uint32_t el = static_cast<uint32_t>(
                   __builtin_amdgcn_update_dpp(static_cast<int>(e_last), static_cast<int>(e), 0x138, 0xF, 0xF, false));
               const uint32_t start = lane == 0 ? e_last : el;  // image jn + lane starts where jn + lane - 1 ends
-              if (inb && (!GAP || (j & 1u))) store_rel(kb + (GAP ? j >> 1 : j), P - pprev, start, rsrc);
+              if constexpr (BLK) {
+                if (inb) {
+                  const uint16_t c = dev::finish<MODE>(P - pprev);  // tcp-header.h:262
+                  if (a.out) static_cast<uint16_t *>(a.out)[kb + j] = c;
+                  const uint32_t f = start + 28;  // tcp-header.h:177
+                  if (f >= sb) {                  // the field's block is in this step's registers
+                    fld[(f - sb) >> 4] = 0x80000000u | (((f & 15u) >> 1) << 16) | c;
+                  } else if (whole(f & ~63u)) {   // the staged block (the image crossed the step start)
+                    reinterpret_cast<uint16_t *>(s_blk[wv])[(f & 63u) >> 1] = c;
+                  } else {
+                    dev::store16_field(rsrc, f, c);
+                  }
+                }
+              } else if (inb && (!GAP || (j & 1u))) {
+                store_rel(kb + (GAP ? j >> 1 : j), P - pprev, start, rsrc);
+              }
             } else {
               if (inb && (!GAP || (j & 1u))) store(kb + (GAP ? j >> 1 : j), P - pprev, 0);
             }
@@ -392,6 +452,36 @@ __global__ void __launch_bounds__(kBlock) vvstream_kernel(VVArgs a) {
             if (!FIXED && jn + 66 > loaded && loaded < nimg) fill_round();  // never with AL4
             j = jn + lane;
             e = ends_at(jn);
+          }
+          if constexpr (BLK) {
+            __builtin_amdgcn_wave_barrier();  // fld / s_blk written by other lanes
+            // the staged block, its field resolved in this step: lanes 0-3 store it
+            if (stage_f != 0 && stage_f < e_last) {
+              if (lane < 4 && whole(stage_f & ~63u)) store16_chunk_wt(rsrc, (stage_f & ~63u) + 16 * lane, s_blk[wv][lane]);
+              stage_f = 0;
+            }
+            // the fields resolved in this step: every lane of a field's 64-B block stores its chunk
+            const uint32_t v = fld[lane];
+            const uint64_t bv = __ballot(v != 0);
+            if (bv) {
+              const uint32_t cb = sb + ((lane & ~3u) << 4);  // the lane's block
+              if ((bv >> (lane & ~3u)) & 0xFull) {
+                if (whole(cb))
+                  store16_chunk_wt(rsrc, sb + (lane << 4), v ? put_word(raw, (v >> 16) & 7u, v) : raw);
+                else if (v)
+                  dev::store16_field(rsrc, sb + (lane << 4) + (((v >> 16) & 7u) << 1), static_cast<uint16_t>(v));
+              }
+              if (v) fld[lane] = 0u;
+            }
+            // the image crossing this step's end, its field in this step: stage its block
+            if (jn < nv) {
+              const uint32_t f = e_last + 28;
+              if (f >= sb && f < sb + 1024) {
+                const uint32_t cb = f & ~63u;
+                if (((sb + (lane << 4)) & ~63u) == cb) s_blk[wv][lane & 3u] = raw;
+                stage_f = f;
+              }
+            }
           }
           __builtin_amdgcn_wave_barrier();  // the next step rewrites the table
           carry += dev::read_lane(incl, 63);
@@ -404,6 +494,19 @@ __global__ void __launch_bounds__(kBlock) vvstream_kernel(VVArgs a) {
     else
       stream_run(std::false_type{});
     if constexpr (!FIXED) bad = bad || pos != span || loaded < nimg;
+    if (BLK && !bad && jn < nv) {  // the image ending at the span: its block is staged
+      const uint16_t c = dev::finish<MODE>(carry - p_last);
+      if (lane == 0 && a.out) static_cast<uint16_t *>(a.out)[kb + jn] = c;
+      const uint32_t f = e_last + 28;
+      if (whole(f & ~63u)) {
+        if (lane == 0) reinterpret_cast<uint16_t *>(s_blk[wv])[(f & 63u) >> 1] = c;
+        __builtin_amdgcn_wave_barrier();
+        if (lane < 4) store16_chunk_wt(rsrc, (f & ~63u) + 16 * lane, s_blk[wv][lane]);
+      } else if (lane == 0) {
+        dev::store16_field(rsrc, f, c);
+      }
+      jn = nv - 1 == jn ? nv : jn;  // (images >= 64 B: the last one only)
+    }
     if (!bad && jn < nv) {  // ends exactly at the last step's end (= span): the first gets the rest
       const uint32_t rem = nv - jn;
       for (uint32_t i = lane; i < rem; i += 64) {
@@ -425,9 +528,9 @@ __global__ void __launch_bounds__(kBlock) vvstream_kernel(VVArgs a) {
   }
 }
 
-template <int U, int OP, int SPLIT, int LAYOUT, bool KEEP = false, int MODE = kRef>
+template <int U, int OP, int SPLIT, int LAYOUT, bool KEEP = false, int MODE = kRef, bool BLK = false>
 hipError_t launch_one(const RunArgs &s, uint32_t oversub, int flags, uint32_t num_cus, hipStream_t stream) {
-  static const uint32_t per_cu = dev::resident_blocks_per_cu(vvstream_kernel<U, OP, SPLIT, LAYOUT, KEEP, MODE>);
+  static const uint32_t per_cu = dev::resident_blocks_per_cu(vvstream_kernel<U, OP, SPLIT, LAYOUT, KEEP, MODE, BLK>);
   const uint64_t resident = static_cast<uint64_t>(per_cu) * num_cus;
   uint64_t blocks = resident * (oversub ? oversub : 1);
   const uint64_t need = (s.count + kWavesPerBlock - 1) / kWavesPerBlock;
@@ -447,8 +550,8 @@ hipError_t launch_one(const RunArgs &s, uint32_t oversub, int flags, uint32_t nu
   a.order = (flags & 8) ? 4u : dev::kOrderDefault;  // groups of 16 blocks per XCD
   a.keep_first = (flags & 16) ? 1u : 0u;
   a.defer_field = (flags & 64) ? 1u : 0u;
-  hipLaunchKernelGGL((vvstream_kernel<U, OP, SPLIT, LAYOUT, KEEP, MODE>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0,
-                     stream, a);
+  hipLaunchKernelGGL((vvstream_kernel<U, OP, SPLIT, LAYOUT, KEEP, MODE, BLK>), dim3(static_cast<uint32_t>(blocks)),
+                     dim3(kBlock), 0, stream, a);
   return hipGetLastError();
 }
 
@@ -466,6 +569,8 @@ hipError_t dispatch(int op, const RunArgs &a, uint32_t oversub, int flags, uint3
     case kChecksum: return launch_one<U, kChecksum, SPLIT, LAYOUT>(a, oversub, flags, num_cus, s);
     case kVerify: return launch_one<U, kVerify, SPLIT, LAYOUT>(a, oversub, flags, num_cus, s);
     case kFill:
+      if constexpr (LAYOUT != 2)
+        if (flags & 128) return launch_one<U, kFill, SPLIT, LAYOUT, false, kRef, true>(a, oversub, flags, num_cus, s);
       return (flags & 32) ? launch_one<U, kFill, SPLIT, LAYOUT, true>(a, oversub, flags, num_cus, s)
                           : launch_one<U, kFill, SPLIT, LAYOUT>(a, oversub, flags, num_cus, s);
     default: return hipErrorInvalidValue;
@@ -483,9 +588,11 @@ hipError_t launch_vvstream(int op, int variant, bool fixed, const RunArgs &a, ui
   uint32_t m = a.oversub ? a.oversub : 1;
   // 8: XCD-chunked run order; 16: L2-kept first step; 32: kFill reads every
   // step with the default cache policy (small images); 64: kFill writes the
-  // results only (the caller runs launch_patch_fields for the fields)
-  const int flags = variant & 120;
+  // results only (the caller runs launch_patch_fields for the fields); 128:
+  // kFill stores each field's whole 64-B block (BLK; reference mode, no gaps)
+  const int flags = variant & 248;
   if ((flags & 64) && (op != kFill || !a.out)) return hipErrorInvalidValue;
+  if ((flags & 128) && (op != kFill || a.mode != kRef || gap || (flags & 96))) return hipErrorInvalidValue;
   variant &= 7;
   int u8 = (variant & 1);
   int split = variant >= 2 ? 1 : 0;
@@ -498,7 +605,7 @@ hipError_t launch_vvstream(int op, int variant, bool fixed, const RunArgs &a, ui
     // runs short with larger M, as rstream does (C5: profiles/r01/split_probe.log).
     m = dev::oversub_for(a.oversub, bytes, static_cast<uint64_t>(num_cus) * 32, 1024, 8u << 10);
     u8 = m >= 32;
-    if (op == kFill && !fixed && !(flags & 96)) {  // (deferred fields, + 64: the stream is CHECKSUM's)
+    if (op == kFill && !fixed && !(flags & 224)) {  // (deferred fields, + 64: the stream is CHECKSUM's; BLK too)
       // FILL of packed variable batches: runs of >= 4 KiB and U4 (C3: M = 64,
       // 53.7 % of the roof against 48.6 % at the checksum policy's U8 x 32;
       // M = 96-255 fall off fast, profiles/r01/c3_fill_sweep.log)
