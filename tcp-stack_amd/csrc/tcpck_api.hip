@@ -485,6 +485,7 @@ hipError_t run_fixed_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint
     a.out = out;
     a.oversub = static_cast<uint32_t>(param >> 16) & 0xFFu;
     a.blocks_per_cu = static_cast<uint32_t>(param >> 8) & 0xFFu;
+    a.dbg = static_cast<uint64_t *>(ctx->dbg);  // set by the probe library only
     return tcpck::launch_vvstream(op, param & 0xFF, true, a, num_cus, s);
   }
   if (kernel != TCPCK_KERNEL_SEG) return hipErrorInvalidValue;
@@ -657,6 +658,7 @@ hipError_t run_var_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const 
     a.oversub = static_cast<uint32_t>(param >> 16) & 0xFFu;
     a.total_bytes = layout ? layout->total_bytes : 0;
     a.blocks_per_cu = static_cast<uint32_t>(param >> 8) & 0xFFu;
+    a.dbg = static_cast<uint64_t *>(ctx->dbg);  // set by the probe library only
     return tcpck::launch_vvstream(op, param & 0xFF, false, a, static_cast<uint32_t>(ctx->num_cus), s);
   }
   if (kernel == TCPCK_KERNEL_SSTREAM) {  // any offset list (runs of <= 128 images)

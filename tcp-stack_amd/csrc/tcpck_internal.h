@@ -62,6 +62,7 @@ struct RunArgs {
   uint32_t blocks_per_cu;    // vvstream: occupancy cap (LDS padding) and grid base, 0 = by resources
   int mode;                  // vvstream: kRef or kRfc1071
   uint8_t *hdr;              // sstream VERIFY: host-order header k also to hdr + 32 k (receive)
+  uint64_t *dbg;             // vvstream, probe library only: 8 x u64 of time stamps per wave (tcpck_probe.h)
 };
 
 // Fixed stride == len for rstream (tcpck_rstream.hip).

@@ -74,7 +74,17 @@ struct VVArgs {
   uint32_t order;           // block order (dev::ordered_block)
   uint32_t keep_first;      // 1: the run's first step read with the default cache policy (L2-kept edge line)
   uint32_t defer_field;     // kFill: results to out only, the fields left for launch_patch_fields
+  uint64_t *dbg;            // probe library: 8 x u64 per wave {start, descriptors, first data, end, hw/xcc, images, span, 0}
 };
+
+#ifdef TCPCK_PROBE
+// s_memrealtime (100 MHz) once `dep` exists: a stamp ordered after the value it names
+__device__ __forceinline__ uint64_t stamp_after(uint32_t dep) {
+  uint64_t t;
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : "v"(dep));
+  return t;
+}
+#endif
 
 // Word wi (0..7) of a 16-byte chunk set to zero.
 __device__ __forceinline__ u32x4 zero_word(u32x4 w, uint32_t wi) {
@@ -125,6 +135,10 @@ __global__ void __launch_bounds__(kBlock) vvstream_kernel(VVArgs a) {
   const uint32_t bid = dev::ordered_block(blockIdx.x, gridDim.x, a.order);
   const uint64_t wid = static_cast<uint64_t>(bid) * kWavesPerBlock + wv;
   const uint64_t N = a.count;
+#ifdef TCPCK_PROBE
+  const uint64_t t_start = a.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
+  uint64_t t_desc = 0, t_first = 0;
+#endif
   const uint32_t S = a.stride;
   const uint32_t L = FIXED ? a.len : 0u;
   uint64_t kb, ke;
@@ -154,6 +168,9 @@ __global__ void __launch_bounds__(kBlock) vvstream_kernel(VVArgs a) {
   const uint32_t nimg = static_cast<uint32_t>(ke - kb);
   const uint32_t nv = GAP ? 2 * nimg : nimg;  // (virtual) images whose ends the stream resolves
   bool bad = !(s1 >= s0 && s1 - A0 < (uint64_t{1} << 31));
+#ifdef TCPCK_PROBE
+  if (a.dbg) t_desc = stamp_after(static_cast<uint32_t>(s1 - A0));
+#endif
 
   // k = batch image index, start = its offset in the arena
   auto store = [&](uint64_t k, uint32_t sum, uint64_t start) {
@@ -390,6 +407,9 @@ __global__ void __launch_bounds__(kBlock) vvstream_kernel(VVArgs a) {
           const uint32_t q2 = dev::dot2_u16(w.y, q1);
           const uint32_t q3 = dev::dot2_u16(w.z, q2);
           const uint32_t tot = dev::dot2_u16(w.w, q3);
+#ifdef TCPCK_PROBE
+          if (a.dbg && st == 0) t_first = stamp_after(tot);
+#endif
           const uint32_t incl = dev::wave_inclusive_scan(tot);
           bool table = false;
           for (;;) {  // once per step unless it holds more than 64 ends
@@ -517,6 +537,22 @@ __global__ void __launch_bounds__(kBlock) vvstream_kernel(VVArgs a) {
     }
     bad = bad || jn != nv;
   }
+#ifdef TCPCK_PROBE
+  if (a.dbg && lane == 0) {
+    uint32_t hw_id, xcc_id;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw_id));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc_id));
+    uint64_t *d = a.dbg + 8 * wid;
+    d[0] = t_start;
+    d[1] = t_desc;
+    d[2] = t_first;
+    d[3] = __builtin_amdgcn_s_memrealtime();
+    d[4] = hw_id | (static_cast<uint64_t>(xcc_id) << 32);
+    d[5] = ke - kb;
+    d[6] = s1 - s0;
+    d[7] = 0;
+  }
+#endif
   if (bad) {  // wave-uniform: the layout is not what the walk assumed -> exact per-image pass
     for (uint64_t k = kb; k < ke; ++k) {
       const uint64_t start = FIXED ? k * S : a.offsets[k] - a.base;
@@ -550,6 +586,7 @@ hipError_t launch_one(const RunArgs &s, uint32_t oversub, int flags, uint32_t nu
   a.order = (flags & 8) ? 4u : dev::kOrderDefault;  // groups of 16 blocks per XCD
   a.keep_first = (flags & 16) ? 1u : 0u;
   a.defer_field = (flags & 64) ? 1u : 0u;
+  a.dbg = s.dbg;
   hipLaunchKernelGGL((vvstream_kernel<U, OP, SPLIT, LAYOUT, KEEP, MODE, BLK>), dim3(static_cast<uint32_t>(blocks)),
                      dim3(kBlock), 0, stream, a);
   return hipGetLastError();
