@@ -24,6 +24,7 @@ import synth_np  # noqa: E402
 
 VV_POLICY = 4 | 8 | 16  # tcpck_api.hip kVvPolicy
 BLK = 128
+MS = []
 
 
 def b2b(fn, s, reps=10, rounds=5):
@@ -64,7 +65,7 @@ def case(ctx, s, name, off, ln, total, only, fixed=None):
              ("FILL_AUTO_noout", lambda: auto(None)),
              ("FILL_BLK", lambda: run(tcpck.OP_FILL, VV_POLICY | BLK)),
              ("FILL_BLK_noout", lambda: run(tcpck.OP_FILL, VV_POLICY | BLK, None))]
-    for m in (16, 64):
+    for m in MS:
         forms.append((f"FILL_BLK_M{m}", lambda m=m: run(tcpck.OP_FILL, VV_POLICY | BLK | (m << 16))))
     ref = None
     for label, fn in forms:
@@ -96,7 +97,9 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("--only", default="")
     p.add_argument("--cases", default="c3,c2var,c2fixed,mix608")
+    p.add_argument("--ms", default="16,64", help="grid multipliers M of the extra FILL_BLK_M<M> forms")
     args = p.parse_args()
+    MS[:] = [int(x) for x in args.ms.split(",") if x]
     only = set(x for x in args.only.split(",") if x)
     cases = args.cases.split(",")
     ctx = tcpck.Context(0, probe=True)

@@ -606,8 +606,12 @@ hipError_t dispatch(int op, const RunArgs &a, uint32_t oversub, int flags, uint3
     case kChecksum: return launch_one<U, kChecksum, SPLIT, LAYOUT>(a, oversub, flags, num_cus, s);
     case kVerify: return launch_one<U, kVerify, SPLIT, LAYOUT>(a, oversub, flags, num_cus, s);
     case kFill:
+#ifdef TCPCK_PROBE
+      // BLK: measured against AUTO's FILL forms and slower at every grid
+      // (scripts/fill_block_probe.py, profiles/r05/): the probe library only
       if constexpr (LAYOUT != 2)
         if (flags & 128) return launch_one<U, kFill, SPLIT, LAYOUT, false, kRef, true>(a, oversub, flags, num_cus, s);
+#endif
       return (flags & 32) ? launch_one<U, kFill, SPLIT, LAYOUT, true>(a, oversub, flags, num_cus, s)
                           : launch_one<U, kFill, SPLIT, LAYOUT>(a, oversub, flags, num_cus, s);
     default: return hipErrorInvalidValue;
@@ -629,7 +633,11 @@ hipError_t launch_vvstream(int op, int variant, bool fixed, const RunArgs &a, ui
   // kFill stores each field's whole 64-B block (BLK; reference mode, no gaps)
   const int flags = variant & 248;
   if ((flags & 64) && (op != kFill || !a.out)) return hipErrorInvalidValue;
+#ifdef TCPCK_PROBE
   if ((flags & 128) && (op != kFill || a.mode != kRef || gap || (flags & 96))) return hipErrorInvalidValue;
+#else
+  if (flags & 128) return hipErrorInvalidValue;  // BLK: the probe library only
+#endif
   variant &= 7;
   int u8 = (variant & 1);
   int split = variant >= 2 ? 1 : 0;
