@@ -98,7 +98,7 @@ __device__ __forceinline__ u32x4 zero_word(u32x4 w, uint32_t wi) {
 }
 
 // Word wi (0..7) of a 16-byte chunk set to v.
-__device__ __forceinline__ u32x4 put_word(u32x4 w, uint32_t wi, uint32_t v) {
+[[maybe_unused]] __device__ __forceinline__ u32x4 put_word(u32x4 w, uint32_t wi, uint32_t v) {
   const uint32_t sh = (wi & 1u) << 4;
   const uint32_t m = ~(0xFFFFu << sh), x = (v & 0xFFFFu) << sh;
   const uint32_t di = wi >> 1;
@@ -109,7 +109,7 @@ __device__ __forceinline__ u32x4 put_word(u32x4 w, uint32_t wi, uint32_t v) {
   return w;
 }
 
-__device__ __forceinline__ void store16_chunk_wt(__amdgpu_buffer_rsrc_t r, uint32_t voff, u32x4 v) {
+[[maybe_unused]] __device__ __forceinline__ void store16_chunk_wt(__amdgpu_buffer_rsrc_t r, uint32_t voff, u32x4 v) {
   typedef unsigned v4u __attribute__((ext_vector_type(4)));
   __builtin_amdgcn_raw_buffer_store_b128(v4u{v.x, v.y, v.z, v.w}, r, static_cast<int>(voff), 0, 19);  // sc0 sc1 nt
 }
