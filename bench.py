@@ -580,7 +580,7 @@ def metric_for(kind, mode=0):
 # ---- the printed line: numbers only, under LINE_LIMIT bytes ------------------
 # The driver keeps only the tail of stdout (BENCH_r04 kept 8.3 KB of an 11.9-KB
 # line, cutting four keys), so the line carries the numbers and every prose
-# field goes to the detail record (stderr + gpurun_out/bench_detail.json).
+# field goes to the detail record (stderr + gpurun_out/bench_detail_<config>_n<N>.json).
 LINE_LIMIT = 6000
 _TOP_CPU = ("value", "unit", "cores", "kind", "sample", "match", "min_GiBs", "max_GiBs", "one_thread_GiBs",
             "reference_O0_GiBs", "cpu_model")
@@ -625,7 +625,7 @@ def compact_line(rec: dict) -> tuple[dict, dict]:
             line[k], detail[k] = key, d
         else:
             line[k] = v
-    line["detail"] = "stderr + gpurun_out/bench_detail.json: per-key workload, metric, sample, settle"
+    line["detail"] = "stderr + gpurun_out/bench_detail_<config>_n<N>.json: per-key workload, metric, sample, settle"
     return line, detail
 
 
@@ -635,8 +635,7 @@ def write_detail(detail: dict, args) -> None:
     try:
         d = os.path.join(ROOT, "gpurun_out")
         os.makedirs(d, exist_ok=True)
-        with open(os.path.join(d, "bench_detail.json" if args.config == "c2" else f"bench_detail_{args.config}.json"),
-                  "w") as f:
+        with open(os.path.join(d, f"bench_detail_{args.config}_n{args.gpus}.json"), "w") as f:
             f.write(text + "\n")
     except OSError as e:
         log(f"bench detail not written: {e}")

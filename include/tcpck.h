@@ -193,7 +193,7 @@ int tcpck_batch_header_swap(tcpck_ctx *ctx, void *d_arena, const uint64_t *d_off
  *   d_hdr != NULL: 4-B aligned, 32 * count bytes: header k in host order at
  *                  d_hdr + 32 k, the arena left as received.  One dense array
  *                  of whole lines instead of one partial-line write per image
- *                  (the cheaper form on this part, DESIGN.md "Receive path").
+ *                  (the cheaper form on this part, profiles/DESIGN_history_r01-r04.md "Receive path").
  * Asynchronous on `stream`. */
 int tcpck_batch_receive(tcpck_ctx *ctx, int mode, void *d_arena, uint64_t stride, uint32_t len,
                         const uint64_t *d_offsets, const uint32_t *d_lengths, uint64_t count,

@@ -40,7 +40,7 @@ extern "C" {
                                | (grid oversubscription << 16)
                                | (1 << 24: each XCD takes groups of 16 blocks)  */
 /* 2, 3, 4, 6, 7: span, stream, fstream, rvstream and vstream, measured in
-   round 1 and removed; 11: bstream (byte runs across
+   round 1 and removed (profiles/DESIGN_history_r01-r04.md section 4); 11: bstream (byte runs across
    image edges, round 2, removed); the numbers are not reused. */
 #define TCPCK_KERNEL_RSTREAM 5 /* fixed stride == len only, MODE_REF: one run per
                                   wave, scalar boundary walk; param = variant
@@ -85,7 +85,12 @@ extern "C" {
                                    only and the write-through field pass
                                    stores the fields, AUTO's for packed fixed
                                    images of 320 B - 1 KiB and gapped ones
-                                   from 512 B)
+                                   from 512 B; + 128, libtcpck_probe.so only:
+                                   FILL stores each field's whole 64-B block
+                                   from the stream's registers, written
+                                   through -- images >= 64 B, MODE_REF, no
+                                   gaps, not with + 32 / + 64; measured slower
+                                   than AUTO)
                                    | (blocks per CU cap << 8: LDS padding)
                                    | (grid oversubscription << 16: 0 = by batch
                                    size, 1 = none, M = M x the resident grid)   */

@@ -26,7 +26,7 @@ OPS = {"checksum": tcpck.OP_CHECKSUM, "verify": tcpck.OP_VERIFY, "fill": tcpck.O
 def timed(fn, s, reps=20, rounds=5, settle_ms=60.0):
     import time
     t0 = time.perf_counter()
-    while (time.perf_counter() - t0) * 1e3 < settle_ms:  # the idle GPU's clock ramp
+    while (time.perf_counter() - t0) * 1e3 < settle_ms:  # the idle GPU's clock ramp (profiles/DESIGN_history_r01-r04.md section 4)
         for _ in range(5):
             fn()
         torch.cuda.synchronize()

@@ -170,7 +170,7 @@ void free_stage(tcpck_ctx *ctx) {
   }
 }
 
-// ---- kernel selection (AUTO; measurements in DESIGN.md section 4) ------------
+// ---- kernel selection (AUTO; measurements in profiles/DESIGN_history_r01-r04.md section 4) ------------
 // reference mode:
 //   fixed, stride == len   < 512 B vvstream (prefix table), 512 B..4 KiB
 //                          rstream (scalar boundary walk), larger seg with
@@ -288,7 +288,7 @@ bool var_fill_defers(int kernel, uint64_t typical) {
 }
 
 // AUTO's kernel for a fixed layout: sets kernel (from TCPCK_KERNEL_AUTO) and
-// its param (measurements in DESIGN.md section 4).
+// its param (measurements in profiles/DESIGN_history_r01-r04.md section 4).
 void pick_fixed(int op, int mode, const uint8_t *arena, uint64_t stride, uint32_t len, int &kernel, int &param) {
   if (mode == TCPCK_MODE_RFC1071 && stride == len && len >= 512 && len <= kFixedRunMaxLen) {
     // RFC 1071 on packed fixed images: rstream's prefix is an exact u32 word
@@ -399,7 +399,7 @@ hipError_t run_fixed_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint
   // host-order header from the stream's registers (one launch, the header
   // bytes read once); elsewhere the header pass follows the VERIFY pass, which
   // measured faster than any fused form for MSS-sized images (header stores
-  // inside the read stream cost more than a separate pass: DESIGN.md "Receive
+  // inside the read stream cost more than a separate pass: profiles/DESIGN_history_r01-r04.md "Receive
   // path", profiles/r03/receive_fused_probe.log)
   // (TCPCK_PARAM_RECEIVE_TWO_PASS keeps the separate pass, AUTO included)
   if (auto_pick && op == TCPCK_OP_RECEIVE && hdr && kernel == TCPCK_KERNEL_SSTREAM && len <= kHdrStreamMaxLen &&
@@ -503,7 +503,7 @@ hipError_t run_fixed_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint
 }
 
 // RECEIVE = the VERIFY pass, then the header pass on the same stream (fusing
-// the header work into rstream's stream measured no faster: DESIGN.md "Receive
+// the header work into rstream's stream measured no faster: profiles/DESIGN_history_r01-r04.md "Receive
 // path").  hdr: host-order headers to hdr[32k, 32k + 32) instead of in place.
 // FILL as CHECKSUM + field update (reference mode, a results buffer): the
 // layout's CHECKSUM kernel at its full streaming rate, then the field pass

@@ -299,7 +299,7 @@ hipError_t launch_one(const uint8_t *buf, uint64_t bytes, uint32_t *out, uint32_
 // 16 B at 1024 t + 16 l), U steps in flight, nt loads; else a grid-stride float4
 // copy, U loads issued before their U stores.  SPOL: store aux bits (0
 // default, 2 nt, 16 sc1).  The measure segmentation's read + write rate is
-// judged against.
+// judged against (profiles/DESIGN_history_r01-r04.md section 6).
 template <int U, int SPOL, bool RUN>
 __global__ void __launch_bounds__(kBlock) diag_copy_kernel(uint8_t *buf, uint64_t bytes) {
   const uint64_t half = (bytes >> 1) & ~uint64_t{127};

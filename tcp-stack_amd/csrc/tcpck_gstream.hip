@@ -193,7 +193,7 @@ template <int U, int G, int SPOL, int LPOL, bool FLINE, int WB>
 hipError_t by_op(int op, const GroupStreamArgs &a, uint32_t num_cus, hipStream_t s) {
 #ifndef TCPCK_PROBE
   // AUTO sends only FILL here: vvstream / rstream CHECKSUM and VERIFY these
-  // layouts equally fast or faster (gstream)
+  // layouts equally fast or faster (profiles/DESIGN_history_r01-r04.md section 4, gstream)
   if (op != kFill) return hipErrorInvalidValue;
 #endif
   switch (op) {

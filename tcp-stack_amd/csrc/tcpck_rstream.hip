@@ -61,7 +61,7 @@ using dev::u32x4;
 // lines: 128 MB) and can write it back whole without reading HBM;
 // a.order (runtime): the block order, dev::ordered_block -- with the XCD
 // orders each XCD streams compact regions instead of every eighth run
-// (measured +4% at C2; the HBM bytes do not change), and
+// (measured +4% at C2, profiles/DESIGN_history_r01-r04.md section 4; the HBM bytes do not change), and
 // neighbouring runs share an XCD's L2 for the run-edge line (FLAV bit 2).
 // MODE: kRef, or kRfc1071 -- the run's prefix P is an exact u32 running sum
 // of its words, so P(end) - P(start) is an image's exact word sum (< 2^32 for

@@ -218,7 +218,7 @@ __global__ void __launch_bounds__(kBlock) vvstream_kernel(VVArgs a) {
     // KEEP (kFill, small images): every line holds a checksum field, so read
     // it with the default policy -- still in L2 when the field store lands, it
     // leaves as a whole line instead of a masked partial write (gstream's
-    // measurement)
+    // measurement, profiles/DESIGN_history_r01-r04.md section 4)
     auto load_step = [&](uint32_t st) -> u32x4 {
       if constexpr (KEEP) {
         typedef unsigned v4u __attribute__((ext_vector_type(4)));
