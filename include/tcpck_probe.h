@@ -31,8 +31,10 @@ extern "C" {
 /* tcpck_probe_receive_ex: tcpck_batch_receive_ex with the header pass in a
  * measured form, chosen by a flags word of its own (param keeps
  * tcpck_tuning.h's meaning):
- *   HDR_FIRST   offset lists, with TCPCK_PARAM_RECEIVE_TWO_PASS: the header
- *               pass before the VERIFY pass
+ *   HDR_FIRST   (accepted, no effect: since round 5 the product runs a separate
+ *               header pass into a header array before the VERIFY pass)
+ *   HDR_AFTER   the separate header pass after the VERIFY pass (the order
+ *               before round 5)
  *   CONCURRENT  the header pass on the context's side stream, beside VERIFY
  *   HDR_WT      the header array stores written through (sc0 sc1 nt)
  *   HDR_WIDE    two lanes per 16-B aligned image, one 16-B buffer load each,
@@ -43,6 +45,7 @@ extern "C" {
  *               over the batch, 3 each block's images 1/128 of the batch
  *               apart (0: in order) */
 #define TCPCK_PROBE_RECEIVE_HDR_FIRST 1
+#define TCPCK_PROBE_RECEIVE_HDR_AFTER 16
 #define TCPCK_PROBE_RECEIVE_CONCURRENT 2
 #define TCPCK_PROBE_RECEIVE_HDR_WT 4
 #define TCPCK_PROBE_RECEIVE_HDR_WIDE 8

@@ -4,10 +4,11 @@ datagrams, SORTED offset list, verdicts + host-order header array) timed the
 honest way -- on rings taken in turn, so no step finds the previous step's
 lines in the 256-MB Infinity Cache -- and, for comparison, on one ring.
 
-Forms: AUTO (the VERIFY stream, then the header pass), the header pass FIRST
-(tcpck_probe.h PROBE_RECEIVE_HDR_FIRST with PARAM_RECEIVE_TWO_PASS: its 128 MB
-of first lines are then in the Infinity Cache when the stream reads them),
-VERIFY alone.  Back-to-back launches, median of 5 rounds; verdicts and header
+Forms: AUTO (since round 5 the header pass FIRST: its 128 MB of first lines
+are then in the Infinity Cache when the VERIFY stream reads them), the header
+pass after VERIFY (tcpck_probe.h PROBE_RECEIVE_HDR_AFTER, the order before
+round 5), VERIFY alone.  --layout: the bench ring (offset list), 1492-B
+images in 2048-B fixed slots, or C2's packed fixed 1492-B images.  Back-to-back launches, median of 5 rounds; verdicts and header
 arrays compared with AUTO's."""
 import argparse
 import os
@@ -44,12 +45,16 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("--rings", type=int, default=3)
     p.add_argument("--slot", type=int, default=2048)
+    p.add_argument("--layout", default="ring", choices=["ring", "slots1492", "c2"])
     args = p.parse_args()
     ctx = tcpck.Context(0, probe=True)
     s = torch.cuda.current_stream()
     count, L = 1 << 20, args.slot
     rng = np.random.default_rng(42)
     ln = (np.asarray((64, 576, 1460), np.uint32)[rng.integers(0, 3, count)] + 32).astype(np.uint32)
+    if args.layout != "ring":
+        ln[:] = 1492
+        L = 1492 if args.layout == "c2" else L
     off = np.arange(count, dtype=np.uint64) * np.uint64(L)
     d_off, d_ln = torch.from_numpy(off).cuda(), torch.from_numpy(ln).cuda()
     rings = []
@@ -61,16 +66,19 @@ def main():
     algo = img + 32 * count + count
     ok = torch.empty(count, dtype=torch.uint8, device="cuda")
     hdr = torch.empty(count * 32, dtype=torch.uint8, device="cuda")
-    kw = dict(offsets=d_off, lengths=d_ln, total_bytes=img, min_len=int(ln.min()), max_len=int(ln.max()),
-              sorted=True, stream=s)
+    if args.layout == "ring":
+        kw = dict(offsets=d_off, lengths=d_ln, total_bytes=img, min_len=int(ln.min()), max_len=int(ln.max()),
+                  sorted=True, stream=s)
+        verify = lambda a: ctx.batch_var(tcpck.OP_VERIFY, a, d_off, d_ln, count, ok, total_bytes=img,
+                                         min_len=int(ln.min()), max_len=int(ln.max()), sorted=True, stream=s)
+    else:
+        kw = dict(stride=L, length=1492, stream=s)
+        verify = lambda a: ctx.batch_fixed(tcpck.OP_VERIFY, a, L, 1492, count, ok, stream=s)
     forms = {
-        "AUTO (VERIFY, then headers)": lambda a: ctx.batch_receive(a, count, ok, hdr, **kw),
-        "headers FIRST, then VERIFY": lambda a: ctx.batch_receive(a, count, ok, hdr, kernel=tcpck.KERNEL_AUTO,
-                                                                  param=tcpck.PARAM_RECEIVE_TWO_PASS,
-                                                                  probe_flags=tcpck.PROBE_RECEIVE_HDR_FIRST, **kw),
-        "VERIFY alone (slots)": lambda a: ctx.batch_var(tcpck.OP_VERIFY, a, d_off, d_ln, count, ok,
-                                                        total_bytes=img, min_len=int(ln.min()),
-                                                        max_len=int(ln.max()), sorted=True, stream=s),
+        "AUTO (headers first)": lambda a: ctx.batch_receive(a, count, ok, hdr, **kw),
+        "headers after VERIFY": lambda a: ctx.batch_receive(a, count, ok, hdr, kernel=tcpck.KERNEL_AUTO,
+                                                            probe_flags=tcpck.PROBE_RECEIVE_HDR_AFTER, **kw),
+        "VERIFY alone": verify,
     }
     ref = None
     for name, fn in forms.items():

@@ -529,9 +529,53 @@ bool fill_by_update(int op, int mode, const void *out, int kernel, int param, bo
   return layout && (layout->flags & TCPCK_LAYOUT_PACKED) && typical >= kFillUpdateMinVar && typical <= kRunMaxLen;
 }
 
+// RECEIVE into a header array: whether the VERIFY kernel writes the headers
+// itself (sstream's stream-register form) -- the same choice run_fixed_impl
+// makes.  Otherwise the separate header pass runs FIRST: its one 128-B line
+// per image (128 MB for 1M datagrams) is then still in the 256-MB Infinity
+// Cache when the VERIFY stream reads the images, where after VERIFY it read
+// every line from HBM again.  On a receive ring taken in turn with others (no
+// step sees the previous step's lines) 158.1 -> 152.5 us per 1M datagrams of
+// 96/608/1492 B in 2048-B slots (scripts/receive_ring_probe.py,
+// profiles/r05/receive_ring_probe.log); the verdicts and headers are the same
+// either way (the header array is not the arena).
+bool fixed_receive_fuses(int mode, const uint8_t *arena, uint64_t stride, uint32_t len, int kernel, int param,
+                         const Hooks &hk) {
+  const bool auto_pick = kernel == TCPCK_KERNEL_AUTO;
+  const CallerBits caller(param);
+  int k = kernel, p = param;
+  if (auto_pick) pick_fixed(TCPCK_OP_RECEIVE, mode, arena, stride, len, k, p);
+  if (auto_pick && k == TCPCK_KERNEL_SSTREAM && len <= kHdrStreamMaxLen && !caller.two_pass) p |= kSstreamHdrStream;
+  return k == TCPCK_KERNEL_SSTREAM && !caller.two_pass && ((hk.fuse_any_hdr && !auto_pick) || (p & kSstreamHdrStream));
+}
+
+void pick_var(int op, int mode, const tcpck_layout *layout, uint64_t count, bool hdr, bool two_pass, int &kernel,
+              int &param, bool &fuse_small);
+
+bool var_receive_fuses(int mode, const tcpck_layout *layout, uint64_t count, int kernel, int param, const Hooks &hk) {
+  const bool auto_pick = kernel == TCPCK_KERNEL_AUTO;
+  const CallerBits caller(param);
+  int k = kernel, p = param;
+  bool fuse_small = false;
+  if (auto_pick) pick_var(TCPCK_OP_RECEIVE, mode, layout, count, true, caller.two_pass, k, p, fuse_small);
+  return k == TCPCK_KERNEL_SSTREAM && !caller.two_pass &&
+         ((hk.fuse_any_hdr && !auto_pick) || fuse_small || (p & kSstreamHdrStream));
+}
+
 hipError_t run_fixed_r(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t stride, uint32_t len,
                        uint64_t count, void *out, int kernel, int param, hipStream_t s, uint8_t *hdr, const Hooks &hk) {
   bool patch = false;
+  if (op == TCPCK_OP_RECEIVE && hdr && !hk.hdr_after && !fixed_receive_fuses(mode, arena, stride, len, kernel, param, hk)) {
+    tcpck::HeaderArgs h{};  // the header pass first (fixed_receive_fuses), then VERIFY
+    h.arena = arena;
+    h.stride = stride;
+    h.count = count;
+    h.out = hdr;
+    h.store_bits = hk.hdr_store_bits;
+    const hipError_t eh = tcpck::launch_header_swap(h, static_cast<uint32_t>(ctx->num_cus), s);
+    if (eh != hipSuccess) return eh;
+    return run_fixed_impl(ctx, TCPCK_OP_VERIFY, mode, arena, stride, len, count, out, kernel, param, s, &patch, hk);
+  }
   if (stride >= 30 && fill_by_update(op, mode, out, kernel, param, true, stride, len)) {
     const int p = param & ~(TCPCK_PARAM_FILL_UPDATE | TCPCK_PARAM_FILL_INSTREAM);
     const hipError_t e = run_fixed_impl(ctx, TCPCK_OP_CHECKSUM, mode, arena, stride, len, count, out, kernel, p, s,
@@ -722,7 +766,8 @@ hipError_t run_var_r(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const uin
   h.count = count;
   h.out = hdr;
   h.store_bits = hk.hdr_store_bits;
-  if (op == TCPCK_OP_RECEIVE && hdr && hk.hdr_first && (param & TCPCK_PARAM_RECEIVE_TWO_PASS)) {
+  if (op == TCPCK_OP_RECEIVE && hdr && !hk.hdr_after && !var_receive_fuses(mode, layout, count, kernel, param, hk)) {
+    // the header pass first, then VERIFY (fixed_receive_fuses)
     const hipError_t eh = tcpck::launch_header_swap(h, static_cast<uint32_t>(ctx->num_cus), s);
     if (eh != hipSuccess) return eh;
     return run_var_impl(ctx, TCPCK_OP_VERIFY, mode, arena, off, len, base, count, out, layout, kernel,

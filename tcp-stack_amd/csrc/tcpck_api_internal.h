@@ -70,7 +70,8 @@ constexpr uint64_t kScratchImages = 8ull << 20;  // 16 MiB of u16 results: C5's 
 struct Hooks {
   bool fuse_any_hdr = false;     // RECEIVE, explicit kernel: fuse the headers into any kernel that can
                                  // (sstream's after-the-verdicts conversion, HDR 1)
-  bool hdr_first = false;        // offset lists, RECEIVE + TCPCK_PARAM_RECEIVE_TWO_PASS: header pass first
+  bool hdr_after = false;        // RECEIVE into a header array: the separate header pass after VERIFY (the
+                                 // product runs it first, tcpck_api.hip receive_hdr_first)
   uint32_t hdr_store_bits = 0;   // HeaderArgs::store_bits of the header pass
 };
 

@@ -30,7 +30,7 @@ namespace {
 Hooks probe_hooks(int flags) {
   Hooks h;
   h.fuse_any_hdr = true;
-  h.hdr_first = (flags & TCPCK_PROBE_RECEIVE_HDR_FIRST) != 0;
+  h.hdr_after = (flags & TCPCK_PROBE_RECEIVE_HDR_AFTER) != 0;
   h.hdr_store_bits = ((flags & TCPCK_PROBE_RECEIVE_HDR_WT) ? 1u : 0u) |
                      ((flags & TCPCK_PROBE_RECEIVE_HDR_WIDE)
                           ? 2u | ((static_cast<uint32_t>(flags) >> TCPCK_PROBE_RECEIVE_CACHE_SHIFT & 3u) << 4)
