@@ -56,6 +56,11 @@ int tcpck_probe_receive_ex(tcpck_ctx *ctx, int mode, void *d_arena, uint64_t str
                            void *d_hdr, const tcpck_layout *layout, int kernel, int param, int probe_flags,
                            tcpck_stream stream);
 
+/* tcpck_batch_fixed_ex / tcpck_batch_var_ex param bit: FILL's field pass
+ * (deferred or update form) walks the images in reverse index order, so it
+ * starts on the lines the stream read last (probe library only). */
+#define TCPCK_PROBE_PARAM_PATCH_REVERSE (1 << 27)
+
 /* Device buffer of 4 x u64 per wave receiving {start, end} s_memrealtime
  * (100 MHz) stamps, HW_ID and XCC_ID from the rstream variants built with
  * stamps (3, 7; NULL = off). */

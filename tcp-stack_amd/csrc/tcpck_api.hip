@@ -589,6 +589,7 @@ hipError_t run_fixed_r(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_
     pa.lo = 0;
     pa.hi = (count - 1) * stride + len;
     pa.update = 1;
+    pa.reverse = hk.patch_reverse ? 1u : 0u;
     return tcpck::launch_patch_fields(pa, static_cast<uint32_t>(ctx->num_cus), s);
   }
   bool hdr_done = false;
@@ -603,6 +604,7 @@ hipError_t run_fixed_r(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_
     p.sums = static_cast<uint16_t *>(out);
     p.lo = 0;
     p.hi = (count - 1) * stride + len;
+    p.reverse = hk.patch_reverse ? 1u : 0u;
     return tcpck::launch_patch_fields(p, static_cast<uint32_t>(ctx->num_cus), s);
   }
   if (op != TCPCK_OP_RECEIVE || hdr_done) return e;
@@ -757,6 +759,7 @@ hipError_t run_var_r(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const uin
     pa.count = count;
     pa.sums = static_cast<uint16_t *>(out);
     pa.update = 1;
+    pa.reverse = hk.patch_reverse ? 1u : 0u;
     pa.packed = (layout && (layout->flags & TCPCK_LAYOUT_PACKED)) ? 1u : 0u;
     return tcpck::launch_patch_fields(pa, static_cast<uint32_t>(ctx->num_cus), s);
   }
@@ -785,6 +788,7 @@ hipError_t run_var_r(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const uin
     pa.base = base;
     pa.count = count;
     pa.sums = static_cast<uint16_t *>(out);
+    pa.reverse = hk.patch_reverse ? 1u : 0u;
     return tcpck::launch_patch_fields(pa, static_cast<uint32_t>(ctx->num_cus), s);
   }
   if (op != TCPCK_OP_RECEIVE || hdr_done) return e;

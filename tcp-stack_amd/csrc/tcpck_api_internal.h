@@ -73,7 +73,11 @@ struct Hooks {
   bool hdr_after = false;        // RECEIVE into a header array: the separate header pass after VERIFY (the
                                  // product runs it first, tcpck_api.hip receive_hdr_first)
   uint32_t hdr_store_bits = 0;   // HeaderArgs::store_bits of the header pass
+  bool patch_reverse = false;    // FILL's field pass in reverse image order (PatchArgs::reverse)
 };
+
+// probe library: tcpck_batch_*_ex param bit selecting Hooks::patch_reverse
+constexpr int kProbeParamPatchReverse = 1 << 27;
 
 int hip_status(hipError_t e);
 

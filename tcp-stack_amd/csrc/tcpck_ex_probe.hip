@@ -102,15 +102,19 @@ int tcpck_batch_fixed_ex(tcpck_ctx *ctx, int op, int mode, void *d_arena, uint64
     return hip_status(tcpck::launch_rstream(tcpck::kFill, param & 0xFF, a, static_cast<uint32_t>(ctx->num_cus),
                                             static_cast<hipStream_t>(stream)));
   }
-  return tcpck::api::batch_fixed_ex(ctx, op, mode, d_arena, stride, len, count, d_out, kernel, param,
-                                    static_cast<hipStream_t>(stream), probe_hooks(0));
+  Hooks hk = probe_hooks(0);
+  hk.patch_reverse = (param & tcpck::api::kProbeParamPatchReverse) != 0;
+  return tcpck::api::batch_fixed_ex(ctx, op, mode, d_arena, stride, len, count, d_out, kernel,
+                                    param & ~tcpck::api::kProbeParamPatchReverse, static_cast<hipStream_t>(stream), hk);
 }
 
 int tcpck_batch_var_ex(tcpck_ctx *ctx, int op, int mode, void *d_arena, const uint64_t *d_offsets,
                        const uint32_t *d_lengths, uint64_t count, void *d_out, const tcpck_layout *layout,
                        int kernel, int param, tcpck_stream stream) {
-  return tcpck::api::batch_var_ex(ctx, op, mode, d_arena, d_offsets, d_lengths, count, d_out, layout, kernel, param,
-                                  static_cast<hipStream_t>(stream), probe_hooks(0));
+  Hooks hk = probe_hooks(0);
+  hk.patch_reverse = (param & tcpck::api::kProbeParamPatchReverse) != 0;
+  return tcpck::api::batch_var_ex(ctx, op, mode, d_arena, d_offsets, d_lengths, count, d_out, layout, kernel,
+                                  param & ~tcpck::api::kProbeParamPatchReverse, static_cast<hipStream_t>(stream), hk);
 }
 
 int tcpck_batch_receive_ex(tcpck_ctx *ctx, int mode, void *d_arena, uint64_t stride, uint32_t len,

@@ -209,7 +209,8 @@ __device__ __forceinline__ void store16_through(uint8_t *p, uint16_t c) {
 template <bool VAR, bool UPDATE>
 __global__ void __launch_bounds__(kBlock) patch_fields_kernel(PatchArgs a) {
   const uint64_t step = static_cast<uint64_t>(gridDim.x) * kBlock;
-  for (uint64_t k = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x; k < a.count; k += step) {
+  for (uint64_t kf = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x; kf < a.count; kf += step) {
+    const uint64_t k = a.reverse ? a.count - 1 - kf : kf;
     uint64_t f;  // the field, relative to arena
     if constexpr (VAR) {
       if (a.lengths[k] < 30) continue;  // no field

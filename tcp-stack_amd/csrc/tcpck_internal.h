@@ -193,6 +193,7 @@ struct PatchArgs {
   uint32_t packed;          // offset lists: the PACKED contract holds (unused by the 2-B pass)
   uint32_t probe_form;      // probe builds (TCPCK_KERNEL_PATCH): a timing form chosen by store_bits
   uint32_t store_bits;      // probe forms: 1 + store cache bits (sc0 1, nt 2, sc1 4; 0 plain) | granularity << 4
+  uint32_t reverse;         // the fields in reverse index order (the stream's last lines first)
 };
 hipError_t launch_patch_fields(const PatchArgs &a, uint32_t num_cus, hipStream_t stream);
 

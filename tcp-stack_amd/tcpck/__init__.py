@@ -60,6 +60,7 @@ TUNING_EXPORTS = ("tcpck_batch_fixed_ex", "tcpck_batch_var_ex", "tcpck_batch_seg
 PROBE_EXPORTS = ("tcpck_ctx_set_debug", "tcpck_diag_stream", "tcpck_probe_receive_ex", "tcpck_probe_scratch_state")
 # include/tcpck_probe.h: tcpck_probe_receive_ex's flags word (the header pass forms)
 PROBE_RECEIVE_HDR_FIRST = 1    # accepted, no effect (the product's separate header pass runs first since round 5)
+PROBE_PARAM_PATCH_REVERSE = 1 << 27  # tcpck_batch_*_ex param (probe library): FILL's field pass in reverse order
 PROBE_RECEIVE_HDR_AFTER = 16   # the separate header pass after VERIFY (the order before round 5)
 PROBE_RECEIVE_CONCURRENT = 2   # header pass on a side stream beside VERIFY
 PROBE_RECEIVE_HDR_WT = 4       # header array stores written through
