@@ -4,7 +4,9 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5|...]
 
 A step = one pass of the hot path (one tcpck_batch_* CHECKSUM launch) over one
-batch of synthetic segments already resident in HBM.  Default workload (N=1)
+batch of synthetic segments already resident in HBM; consecutive steps take
+--arenas (2) identical batches in turn, so no step reads lines the previous
+step left in the 256-MB Infinity Cache.  Default workload (N=1)
 is BASELINE.json configs[1] (C2): 1,048,576 segments with a 1460-B Ethernet-MSS
 payload = 1492-B checksummed images (32-B pseudo+TCP header + payload,
 SURVEY.md fact 3), fixed stride.  With N>1 GPUs (one process per GPU via
@@ -116,7 +118,7 @@ IMAGE_BYTES = {"slots": "96/608/1492 in 2048-B slots", "receive": "96/608/1492 i
                "segment": "32 + 1460 in 1504-B slots"}
 MODES = {"c2_rfc": 1}  # TCPCK_MODE_RFC1071; every other config runs the reference arithmetic (0)
 NO_RESULTS = {"fill_noout"}  # steps that write no results array (only the fields in place)
-RING_COUNT = 2  # slots / receive: identical rings taken in turn (Workload)
+ARENAS = 2  # identical batches taken in turn by every step (Workload; --arenas)
 
 
 def log(*a):
@@ -135,6 +137,8 @@ def parse():
     p.add_argument("--no-extras", action="store_true", help="default run: skip the c3/c4/c5_strong keys")
     p.add_argument("--settle-ms", type=float, default=250.0,
                    help="untimed back-to-back launches before the warm-up steps (clock ramp)")
+    p.add_argument("--arenas", type=int, default=ARENAS,
+                   help="identical batches per config, taken in turn by the steps (no cross-step cache reuse)")
     p.add_argument("--launch-check", action="store_true",
                    help="start the ranks and print their layout only (no GPU; tests/test_bench_contract.py)")
     p.add_argument("--per-launch-events", action="store_true",
@@ -190,7 +194,7 @@ def bench_c1(args):
 class Workload:
     """One config's device-resident batch on this rank and its step function."""
 
-    def __init__(self, name, ctx, stream, rank, world):
+    def __init__(self, name, ctx, stream, rank, world, n_arenas=1):
         import torch
         import tcpck
         from tcpck.shard import shard_range
@@ -207,94 +211,97 @@ class Workload:
         self.extra_bytes = 0  # algorithmic bytes per launch beyond the image bytes read (+2 per result)
         self.layout = None
         self.arena = None
+        # Every step reads one of n_arenas identical batches, taken in turn
+        # (--arenas, default ARENAS): step k+1 never finds the lines step k left
+        # in the 256-MB Infinity Cache -- a sender or receiver never sees the
+        # same segments twice.  make() builds one batch, run(batch, out) is
+        # one pass of the hot path over it.
         if kind in ("slots", "receive"):
             rng = np.random.default_rng(42 + rank)
             ln = (np.asarray((64, 576, 1460), np.uint32)[rng.integers(0, 3, count)] + 32).astype(np.uint32)
             off = np.arange(count, dtype=np.uint64) * np.uint64(L)
             d_off, d_ln = torch.from_numpy(off).cuda(), torch.from_numpy(ln).cuda()
-            # RING_COUNT rings with the same datagrams, taken in turn: step k+1
-            # never reads the lines step k pulled into the 256-MB Infinity Cache
-            # (RECEIVE's header pass ends a step on the first 128-B line of all
-            # 1M slots, 128 MB, which the next step's stream reads first;
-            # a real receive ring never sees the same datagrams twice)
-            rings = []
-            for _ in range(RING_COUNT):
-                a = torch.empty(count * L, dtype=torch.uint8, device="cuda")
-                tcpck.synth_var(a, d_off, d_ln, 1492, count, seed=42, first_index=first, stream=stream)
-                rings.append(a)
-            arena = rings[0]
             img_bytes = int(ln.astype(np.int64).sum())
             lmin, lmax = int(ln.min()), int(ln.max())
 
+            def make():
+                a = torch.empty(count * L, dtype=torch.uint8, device="cuda")
+                tcpck.synth_var(a, d_off, d_ln, 1492, count, seed=42, first_index=first, stream=stream)
+                return a
+
             if kind == "slots":
-                def ring_step(a, out):
+                def run(a, out):
                     ctx.batch_var(tcpck.OP_VERIFY, a, d_off, d_ln, count, out, total_bytes=img_bytes,
                                   min_len=lmin, max_len=lmax, sorted=True, stream=stream)
             else:
                 hdr_out = torch.empty(count * 32, dtype=torch.uint8, device="cuda")
                 self.extra_bytes = 32 * count  # the header array written
 
-                def ring_step(a, out):
+                def run(a, out):
                     ctx.batch_receive(a, count, out, hdr_out, offsets=d_off, lengths=d_ln,
                                       total_bytes=img_bytes, min_len=lmin, max_len=lmax, sorted=True,
                                       stream=stream)
-            self.turn = 0
-
-            def step(out):
-                ring_step(rings[self.turn % self.n_rings], out)
-                self.turn += 1
-            self.n_rings = RING_COUNT
         elif kind == "segment":
             P, seg, stride = count, L, 1504
-            payload = torch.empty(P, dtype=torch.uint8, device="cuda")
-            tcpck.synth_fixed(payload, 1492, 1492, P // 1492, seed=42, first_index=first, stream=stream)
             count = (P + seg - 1) // seg
-            images = torch.empty(count * stride, dtype=torch.uint8, device="cuda")
             hdr = np.zeros(32, np.uint8)
             hdr[0:4], hdr[4:8], hdr[12:14], hdr[14:16] = [127, 0, 0, 1], [127, 0, 0, 1], [0x3C, 0x8C], [0x3C, 0x8D]
             hdr[20:24], hdr[25] = [0, 0, 0x1E, 0x61], 0x08  # ack 7777, ACK (state.cc:178-180)
             img_bytes = P  # the stream read
             self.extra_bytes = P + 32 * count  # the images written (header + payload; slot padding excluded)
 
-            def step(out):
-                ctx.batch_segment(payload, P, seg, hdr, 1001, images, stride, out, stream=stream)
-        elif kind == "fill":
-            arena = torch.empty(count * L, dtype=torch.uint8, device="cuda")
-            tcpck.synth_fixed(arena, L, L, count, seed=42, first_index=first, stream=stream)
-            img_bytes = count * L
-            self.extra_bytes = 2 * count  # the fields written in place (+2 per result below)
-            with_out = name not in NO_RESULTS
+            def make():
+                payload = torch.empty(P, dtype=torch.uint8, device="cuda")
+                tcpck.synth_fixed(payload, 1492, 1492, P // 1492, seed=42, first_index=first, stream=stream)
+                return payload, torch.empty(count * stride, dtype=torch.uint8, device="cuda")
 
-            def step(out):
-                ctx.batch_fixed(tcpck.OP_FILL, arena, L, L, count, out if with_out else None, stream=stream)
-        elif kind == "fixed":
-            arena = torch.empty(count * L, dtype=torch.uint8, device="cuda")
-            tcpck.synth_fixed(arena, L, L, count, seed=42, first_index=first, stream=stream)
+            def run(b, out):
+                ctx.batch_segment(b[0], P, seg, hdr, 1001, b[1], stride, out, stream=stream)
+        elif kind in ("fill", "fixed"):
             img_bytes = count * L
 
-            def step(out):
-                ctx.batch_fixed(tcpck.OP_CHECKSUM, arena, L, L, count, out, mode=mode, stream=stream)
+            def make():
+                a = torch.empty(count * L, dtype=torch.uint8, device="cuda")
+                tcpck.synth_fixed(a, L, L, count, seed=42, first_index=first, stream=stream)
+                return a
+
+            if kind == "fill":
+                self.extra_bytes = 2 * count  # the fields written in place (+2 per result below)
+                with_out = name not in NO_RESULTS
+
+                def run(a, out):
+                    ctx.batch_fixed(tcpck.OP_FILL, a, L, L, count, out if with_out else None, stream=stream)
+            else:
+                def run(a, out):
+                    ctx.batch_fixed(tcpck.OP_CHECKSUM, a, L, L, count, out, mode=mode, stream=stream)
         else:
             from synth_np import mixed_layout
             off, ln, total = mixed_layout(count, seed=42 + rank)
-            arena = torch.empty(total, dtype=torch.uint8, device="cuda")
             d_off = torch.from_numpy(off).cuda()
             d_ln = torch.from_numpy(ln).cuda()
-            tcpck.synth_var(arena, d_off, d_ln, 1492, count, seed=42, first_index=first, stream=stream)
             img_bytes = int(ln.astype(np.int64).sum())
             lmin, lmax = int(ln.min()), int(ln.max())  # host-side layout hint, computed once
             self.layout = (off, ln)
 
+            def make():
+                a = torch.empty(total, dtype=torch.uint8, device="cuda")
+                tcpck.synth_var(a, d_off, d_ln, 1492, count, seed=42, first_index=first, stream=stream)
+                return a
+
+            op = tcpck.OP_FILL if kind == "fill_var" else tcpck.OP_CHECKSUM
             if kind == "fill_var":
                 self.extra_bytes = 2 * count  # the fields written in place (+2 per result below)
 
-                def step(out):
-                    ctx.batch_var(tcpck.OP_FILL, arena, d_off, d_ln, count, out, total_bytes=img_bytes,
-                                  min_len=lmin, max_len=lmax, packed=True, stream=stream)
-            else:
-                def step(out):
-                    ctx.batch_var(tcpck.OP_CHECKSUM, arena, d_off, d_ln, count, out, total_bytes=img_bytes,
-                                  min_len=lmin, max_len=lmax, packed=True, stream=stream)
+            def run(a, out):
+                ctx.batch_var(op, a, d_off, d_ln, count, out, total_bytes=img_bytes, min_len=lmin, max_len=lmax,
+                              packed=True, stream=stream)
+        self.bufs = [make() for _ in range(max(1, n_arenas))]
+        self.n_arenas, self.turn = len(self.bufs), 0
+
+        def step(out):
+            run(self.bufs[self.turn % self.n_arenas], out)
+            self.turn += 1
+        arena = self.bufs[0]
         self.arena = arena if kind in ("fixed", "mixed", "fill", "fill_var", "slots", "receive") else None
         self.count, self.first, self.img_bytes = count, first, img_bytes
         self.verdicts = kind in ("slots", "receive")  # u8 results
@@ -393,17 +400,17 @@ def roofline(w: Workload, launch_ms, launch_ms_all, traffic_key, world):
 def extra_config(name, key, ctx, stream, rank, world, args, coll_dev):
     """Another BASELINE config timed in the default run; its record for rank 0's line."""
     import torch
-    w = Workload(name, ctx, stream, rank, world)
+    w = Workload(name, ctx, stream, rank, world, args.arenas)
     same_ring = None
-    if getattr(w, "n_rings", 1) > 1:
+    if w.n_arenas > 1 and w.kind in ("slots", "receive"):
         # first the same step on ONE ring, every step over the same datagrams:
         # what the Infinity Cache's cross-step reuse adds (never `value`; timed
         # first so that the key's own K launches are the last ones in a trace)
-        rings, w.n_rings = w.n_rings, 1
+        rings, w.n_arenas = w.n_arenas, 1
         tmax1, launch1, _, step_bytes1, _ = measure(w, args, world, stream, coll_dev)
         same_ring = {"value": round(step_bytes1 * args.steps / tmax1 / GIB, 2),
                      "frac": round(w.algo_bytes / (launch1 * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
-        w.n_rings = rings
+        w.n_arenas = rings
     tmax, launch_ms, launch_ms_all, step_bytes, settle = measure(w, args, world, stream, coll_dev)
     rec = {"workload": w.desc, "metric": metric_for(w.kind, w.mode), "value": round(step_bytes * args.steps / tmax / GIB, 2),
            "unit": "GiB/s",
@@ -507,7 +514,7 @@ def main():
     from tcpck.shard import gather_ranks, max_over_ranks
     ctx = tcpck.Context(local)
     stream = torch.cuda.current_stream()
-    w = Workload(args.config, ctx, stream, rank, world)
+    w = Workload(args.config, ctx, stream, rank, world, args.arenas)
     tmax, launch_ms, launch_ms_all, step_bytes, settle = measure(w, args, world, stream, coll_dev)
     value = step_bytes * args.steps / tmax / GIB
     res = w.results()  # checksum results of this rank (the CPU baseline compares them)
