@@ -78,7 +78,7 @@ def main():
                 run(arenas[turn[0] % len(arenas)])
                 turn[0] += 1
                 if variant.endswith("flush"):
-                    torch.sum(flush, dtype=torch.int64, out=sink)
+                    flush.view(torch.int64).sum()
             ms = timed(step, s)
             print(f"{case} {variant:28s} {ms * 1e3:7.1f} us per step (HIP events{', flush included' if 'flush' in variant else ''})"
                   f"  {(img + 2 * n) / ms / 1e6 / 80:5.1f} %", flush=True)
