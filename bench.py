@@ -515,6 +515,16 @@ def main():
     ctx = tcpck.Context(local)
     stream = torch.cuda.current_stream()
     w = Workload(args.config, ctx, stream, rank, world, args.arenas)
+    one_arena = None
+    if w.n_arenas > 1:
+        # the same K steps on ONE batch re-read step after step, for reference:
+        # the Infinity Cache then serves part of each step (never `value`; timed
+        # first so that a kernel trace's last K launches are `value`'s)
+        k, w.n_arenas = w.n_arenas, 1
+        tmax1, launch1, _, step_bytes1, _ = measure(w, args, world, stream, coll_dev)
+        one_arena = {"value": round(step_bytes1 * args.steps / tmax1 / GIB, 2),
+                     "frac": round(w.algo_bytes / (launch1 * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+        w.n_arenas = k
     tmax, launch_ms, launch_ms_all, step_bytes, settle = measure(w, args, world, stream, coll_dev)
     value = step_bytes * args.steps / tmax / GIB
     res = w.results()  # checksum results of this rank (the CPU baseline compares them)
@@ -549,6 +559,8 @@ def main():
         "roofline": roofline(w, launch_ms, launch_ms_all, args.config, world),
         "settle": settle,
     }
+    if one_arena is not None:
+        rec["one_arena"] = one_arena
     del w
     torch.cuda.empty_cache()
 

@@ -107,7 +107,8 @@ def _full_record(world=1):
            "data": "synthetic (device-generated: send-path headers + splitmix64 payloads, seed 42)",
            "config": {"workload": bench.CONFIGS["c2"][0], "images_per_gpu": 1 << 20, "image_bytes": 1492,
                       "bytes_per_gpu": 1564475392, "parallelism": "shard1 (independent per-GPU batches, no collective)"},
-           "roofline": dict(roof), "settle": {"ms": 250.3, "launches": 1184}}
+           "roofline": dict(roof), "settle": {"ms": 250.3, "launches": 1184},
+           "one_arena": {"value": 6999.99, "frac": 0.9399}}
     for name, key in bench.EXTRAS:
         desc = bench.CONFIGS[name][0] if name in bench.CONFIGS else bench.EXTRA[name][0]
         kind = bench.CONFIGS[name][1] if name in bench.CONFIGS else bench.EXTRA[name][1]
@@ -154,3 +155,4 @@ def test_line_fits_the_driver_tail():
         assert {"value", "unit", "cores", "kind", "sample"} <= set(line["cpu_baseline"])
         assert line["c1"]["verified"] == line["c1"]["segments"]
         assert line["receive"]["same_ring"]["frac"] > 0
+        assert line["one_arena"]["frac"] > 0
