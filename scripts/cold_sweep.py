@@ -60,7 +60,7 @@ def sweep(name, arenas, run, params, algo, s):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--cases", default="c2,c3")
+    ap.add_argument("--cases", default="c2,c3", help="c2, c3, diag (the bare C2-size stream)")
     args = ap.parse_args()
     ctx = tcpck.Context(0, probe=True)
     s = torch.cuda.current_stream()
@@ -74,7 +74,12 @@ def main():
         out = torch.empty(n, dtype=torch.int16, device="cuda")
         run = lambda a, p: (ctx.batch_fixed(tcpck.OP_CHECKSUM, a, L, L, n, out, stream=s) if p is None else
                             ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, a, L, L, n, out, tcpck.KERNEL_RSTREAM, p, stream=s))
-        params = [("AUTO", None)]
+        if "diag" in args.cases:  # the bare stream (no checksum, XCD regions, 32x): the ceiling, cold and warm
+            dout = torch.empty(1 << 22, dtype=torch.int32, device="cuda")
+            sweep("c2", arenas, lambda a, p: ctx.diag_stream(p, a, n * L, dout, stream=s),
+                  [("AUTO warm-up", 0x3801), ("bare stream 0x3801 (xcd)", 0x3801), ("bare stream 0x3800", 0x3800)],
+                  n * L + 2 * n, s)
+        params = [("AUTO warm-up", None), ("AUTO", None)]
         for v in (20, 18, 22, 23, 24):
             for m in (16, 32, 64):
                 params.append((f"rstream {v} M{m}", v | (m << 16)))
@@ -95,7 +100,7 @@ def main():
         kw = dict(total_bytes=img, min_len=int(ln.min()), max_len=int(ln.max()), packed=True, stream=s)
         run = lambda a, p: (ctx.batch_var(tcpck.OP_CHECKSUM, a, d_off, d_ln, n, out, **kw) if p is None else
                             ctx.batch_var_ex(tcpck.OP_CHECKSUM, a, d_off, d_ln, n, out, tcpck.KERNEL_VVSTREAM, p, **kw))
-        params = [("AUTO", None)]
+        params = [("AUTO warm-up", None), ("AUTO", None)]
         for base, lab in ((3 | 8 | 16, "U8 xcd keep"), (3 | 8, "U8 xcd"), (2 | 8 | 16, "U4 xcd keep"), (3 | 16, "U8 keep")):
             for m in (16, 32, 64):
                 params.append((f"vvstream {lab} M{m}", base | (m << 16)))
