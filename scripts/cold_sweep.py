@@ -9,7 +9,9 @@ order) were measured on one arena; here each is re-timed both ways.
 
 rstream params: variant | M << 16 (18: v_dot2 + buffer loads + XCD-chunked
 order; 20: 18 + the run's first step with the default cache policy = AUTO;
-22: every step default policy; 23 / 24: 20 with 8 / 2 steps in flight).
+22: every step default policy; 23 / 24: 20 with 8 / 2 steps in flight; 14 /
+15: each XCD one contiguous region of runs, 4 / 8 steps in flight; 21: 14 +
+the first step default policy).
 vvstream params: 2 / 3 = equal-count runs U4 / U8, + 8 XCD-chunked order, +
 16 first step default policy (AUTO: 4 | 8 | 16 = 28, U8 at M 32)."""
 import argparse
@@ -25,6 +27,8 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "tcp-stack_amd"), os.path.join(ROOT, "t
 import torch  # noqa: E402
 import tcpck  # noqa: E402
 import synth_np  # noqa: E402
+
+VARIANTS, MS = [], []
 
 
 def b2b(fn, s, reps=20, rounds=5):
@@ -61,7 +65,11 @@ def sweep(name, arenas, run, params, algo, s):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--cases", default="c2,c3", help="c2, c3, diag (the bare C2-size stream)")
+    ap.add_argument("--rs", default="20,18,22,23,24", help="rstream variants (C2)")
+    ap.add_argument("--ms", default="16,32,64", help="grid multipliers (C2)")
     args = ap.parse_args()
+    VARIANTS[:] = [int(x) for x in args.rs.split(",")]
+    MS[:] = [int(x) for x in args.ms.split(",")]
     ctx = tcpck.Context(0, probe=True)
     s = torch.cuda.current_stream()
     if "c2" in args.cases:
@@ -80,8 +88,8 @@ def main():
                   [("AUTO warm-up", 0x3801), ("bare stream 0x3801 (xcd)", 0x3801), ("bare stream 0x3800", 0x3800)],
                   n * L + 2 * n, s)
         params = [("AUTO warm-up", None), ("AUTO", None)]
-        for v in (20, 18, 22, 23, 24):
-            for m in (16, 32, 64):
+        for v in VARIANTS:
+            for m in MS:
                 params.append((f"rstream {v} M{m}", v | (m << 16)))
         sweep("c2", arenas, run, params, n * L + 2 * n, s)
         del arenas, out
