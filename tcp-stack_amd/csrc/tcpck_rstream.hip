@@ -55,6 +55,8 @@ using dev::u32x4;
 // from the stream's own registers with the checksum in place, write-through
 // (sc0 sc1 nt) -- a whole-block store needs no read-modify-write of the line,
 // a 2-B store does (scripts/fill_drain_probe.py, profiles/r03/fill_blind.log);
+// bit 8 (probe, with bit 2): only the run's first LINE with the default
+// policy, the rest of step 0 nt;
 // bit 7 (kFill, probe): the chunks of each field's 64-B block read with the
 // default cache policy (the rest nt), so a field pass after the stream finds
 // the block in the caches (the memory-side Infinity Cache holds C2's 1M field
@@ -234,8 +236,19 @@ __global__ void __launch_bounds__(kBlock) rstream_kernel(FixedStreamArgs a) {
       // last line; kept in L2 (nt lines go first), the neighbour's last step
       // can find it there instead of reading it from HBM a second time
       typedef unsigned v4u __attribute__((ext_vector_type(4)));
-      const v4u v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, static_cast<int>(lane << 4), 0, 0);
-      ring[0] = u32x4{v.x, v.y, v.z, v.w};
+      if constexpr ((FLAV & 256) != 0) {
+        // (probe) only that shared line (lanes 0-7) with the default policy, the
+        // step's other 7 lines nt
+        if (lane < 8) {
+          const v4u v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, static_cast<int>(lane << 4), 0, 0);
+          ring[0] = u32x4{v.x, v.y, v.z, v.w};
+        } else {
+          ring[0] = dev::load16_buf_nt(rsrc, lane << 4, 0);
+        }
+      } else {
+        const v4u v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, static_cast<int>(lane << 4), 0, 0);
+        ring[0] = u32x4{v.x, v.y, v.z, v.w};
+      }
     } else {
       ring[u] = load_step(static_cast<uint32_t>(u));
     }
@@ -419,6 +432,11 @@ hipError_t launch_rstream(int op, int variant, const FixedStreamArgs &a, uint32_
       FixedStreamArgs b = a;
       b.order = 4u;
       return dispatch<4, false, 0, 23>(op, b, num_cus, stream);
+    }
+    case 31: {  // 20 with only the run's first line read with the default policy (FLAV bit 8)
+      FixedStreamArgs b = a;
+      b.order = 4u;
+      return dispatch<4, false, 0, 263>(op, b, num_cus, stream);
     }
     case 23: case 24: {  // 20 with 8 (23) or 2 (24) steps in flight
       FixedStreamArgs b = a;
