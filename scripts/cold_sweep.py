@@ -9,7 +9,9 @@ order) were measured on one arena; here each is re-timed both ways.
 
 rstream params: variant | M << 16 (18: v_dot2 + buffer loads + XCD-chunked
 order; 20: 18 + the run's first step with the default cache policy = AUTO;
-22: every step default policy; 23 / 24: 20 with 8 / 2 steps in flight; 14 /
+22: every step default policy; 23 / 24: 20 with 8 / 2 steps in flight; 31 =
+20 (since round 5 only the run's first line kept), 32: 20 before round 5
+(the whole first step kept); 14 /
 15: each XCD one contiguous region of runs, 4 / 8 steps in flight; 21: 14 +
 the first step default policy).
 vvstream params: 2 / 3 = equal-count runs U4 / U8, + 8 XCD-chunked order, +
@@ -28,7 +30,7 @@ import torch  # noqa: E402
 import tcpck  # noqa: E402
 import synth_np  # noqa: E402
 
-VARIANTS, MS = [], []
+VARIANTS, MS, VMS = [], [], []
 
 
 def b2b(fn, s, reps=20, rounds=5):
@@ -67,9 +69,11 @@ def main():
     ap.add_argument("--cases", default="c2,c3", help="c2, c3, diag (the bare C2-size stream)")
     ap.add_argument("--rs", default="20,18,22,23,24", help="rstream variants (C2)")
     ap.add_argument("--ms", default="16,32,64", help="grid multipliers (C2)")
+    ap.add_argument("--vms", default="16,32,64", help="grid multipliers (C3)")
     args = ap.parse_args()
     VARIANTS[:] = [int(x) for x in args.rs.split(",")]
     MS[:] = [int(x) for x in args.ms.split(",")]
+    VMS[:] = [int(x) for x in args.vms.split(",") if x]
     ctx = tcpck.Context(0, probe=True)
     s = torch.cuda.current_stream()
     if "c2" in args.cases:
@@ -109,8 +113,10 @@ def main():
         run = lambda a, p: (ctx.batch_var(tcpck.OP_CHECKSUM, a, d_off, d_ln, n, out, **kw) if p is None else
                             ctx.batch_var_ex(tcpck.OP_CHECKSUM, a, d_off, d_ln, n, out, tcpck.KERNEL_VVSTREAM, p, **kw))
         params = [("AUTO warm-up", None), ("AUTO", None)]
-        for base, lab in ((3 | 8 | 16, "U8 xcd keep"), (3 | 8, "U8 xcd"), (2 | 8 | 16, "U4 xcd keep"), (3 | 16, "U8 keep")):
-            for m in (16, 32, 64):
+        params += [("vvstream policy, whole first step kept (5)", 5 | 8 | 16), ("vvstream policy (AUTO)", 4 | 8 | 16),
+                   ("vvstream policy, no kept line", 4 | 8)]
+        for base, lab in ((3 | 8 | 16, "U8 xcd keep"), (3 | 8, "U8 xcd"), (2 | 8 | 16, "U4 xcd keep")):
+            for m in VMS:
                 params.append((f"vvstream {lab} M{m}", base | (m << 16)))
         sweep("c3", arenas, run, params, img + 2 * n, s)
     ctx.close()

@@ -373,12 +373,19 @@ hipError_t launch_rstream(int op, int variant, const FixedStreamArgs &a, uint32_
     if (variant != 20 || a.stride >= (1u << 17)) return hipErrorInvalidValue;
     FixedStreamArgs b = a;
     b.order = 4u;
-    return dispatch<4, false, 0, 7, kRfc1071>(op, b, num_cus, stream);
+    return dispatch<4, false, 0, 263, kRfc1071>(op, b, num_cus, stream);
   }
-  if (variant == 20) {  // the policy (AUTO): U4, v_dot2 sums, buffer loads, XCD-chunked order, L2-kept first step
+  if (variant == 20) {
+    // the policy (AUTO): U4, v_dot2 sums, buffer loads, XCD-chunked order, the
+    // run's first line L2-kept.  Only that line: round 1-4 read the whole first
+    // step with the default policy, and those 256 MB per C2 launch (1 KiB x
+    // 256K runs) were found in the Infinity Cache by the next launch over the
+    // same arena -- 93 % re-reading one arena, 91 % cold (two arenas in turn);
+    // the shared line alone: 92.3 % either way (scripts/cold_sweep.py,
+    // profiles/r05/cold_sweep_31.log; variant 32 keeps the whole step)
     FixedStreamArgs b = a;
     b.order = 4u;
-    return dispatch<4, false, 0, 7>(op, b, num_cus, stream);
+    return dispatch<4, false, 0, 263>(op, b, num_cus, stream);
   }
 #ifdef TCPCK_PROBE
   // measurement-only variants (libtcpck_probe.so): steps in flight, time
@@ -433,10 +440,12 @@ hipError_t launch_rstream(int op, int variant, const FixedStreamArgs &a, uint32_
       b.order = 4u;
       return dispatch<4, false, 0, 23>(op, b, num_cus, stream);
     }
-    case 31: {  // 20 with only the run's first line read with the default policy (FLAV bit 8)
+    case 31: case 32: {  // 31: 20 (FLAV bit 8: only the run's first line with the default policy);
+                         // 32: the policy before round 5, the whole first step with the default policy
       FixedStreamArgs b = a;
       b.order = 4u;
-      return dispatch<4, false, 0, 263>(op, b, num_cus, stream);
+      return variant == 31 ? dispatch<4, false, 0, 263>(op, b, num_cus, stream)
+                           : dispatch<4, false, 0, 7>(op, b, num_cus, stream);
     }
     case 23: case 24: {  // 20 with 8 (23) or 2 (24) steps in flight
       FixedStreamArgs b = a;

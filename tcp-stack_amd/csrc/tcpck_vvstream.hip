@@ -72,7 +72,8 @@ struct VVArgs {
   uint32_t stride;          // fixed layouts: image k at k * stride
   uint32_t len;             // fixed layouts: image length (<= stride)
   uint32_t order;           // block order (dev::ordered_block)
-  uint32_t keep_first;      // 1: the run's first step read with the default cache policy (L2-kept edge line)
+  uint32_t keep_first;      // 1: the run's first line read with the default cache policy (L2-kept edge
+                            // line); 2 (probe): its whole first step, the policy before round 5
   uint32_t defer_field;     // kFill: results to out only, the fields left for launch_patch_fields
   uint64_t *dbg;            // probe library: 8 x u64 per wave {start, descriptors, first data, end, hw/xcc, images, span, 0}
 };
@@ -243,8 +244,11 @@ __global__ void __launch_bounds__(kBlock) vvstream_kernel(VVArgs a) {
     u32x4 ring[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      if (u == 0 && a.keep_first) {
-        // the first line is the previous run's last: kept in L2 for its last step
+      if (u == 0 && a.keep_first && (lane < 8 || a.keep_first == 2)) {
+        // the first line is the previous run's last: kept in L2 for its last
+        // step (only that line: a whole first step with the default policy is
+        // found in the Infinity Cache by the next launch over the same arena,
+        // which cold batches never see; rstream's launcher has the numbers)
         typedef unsigned v4u __attribute__((ext_vector_type(4)));
         const v4u v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, static_cast<int>(lane << 4), 0, 0);
         ring[0] = u32x4{v.x, v.y, v.z, v.w};
@@ -584,7 +588,7 @@ hipError_t launch_one(const RunArgs &s, uint32_t oversub, int flags, uint32_t nu
   a.stride = static_cast<uint32_t>(s.stride);
   a.len = s.len;
   a.order = (flags & 8) ? 4u : dev::kOrderDefault;  // groups of 16 blocks per XCD
-  a.keep_first = (flags & 16) ? 1u : 0u;
+  a.keep_first = (flags & 16) ? ((flags & 256) ? 2u : 1u) : 0u;
   a.defer_field = (flags & 64) ? 1u : 0u;
   a.dbg = s.dbg;
   hipLaunchKernelGGL((vvstream_kernel<U, OP, SPLIT, LAYOUT, KEEP, MODE, BLK>), dim3(static_cast<uint32_t>(blocks)),
@@ -631,7 +635,7 @@ hipError_t launch_vvstream(int op, int variant, bool fixed, const RunArgs &a, ui
   // step with the default cache policy (small images); 64: kFill writes the
   // results only (the caller runs launch_patch_fields for the fields); 128:
   // kFill stores each field's whole 64-B block (BLK; reference mode, no gaps)
-  const int flags = variant & 248;
+  int flags = variant & 248;
   if ((flags & 64) && (op != kFill || !a.out)) return hipErrorInvalidValue;
 #ifdef TCPCK_PROBE
   if ((flags & 128) && (op != kFill || a.mode != kRef || gap || (flags & 96))) return hipErrorInvalidValue;
@@ -639,6 +643,12 @@ hipError_t launch_vvstream(int op, int variant, bool fixed, const RunArgs &a, ui
   if (flags & 128) return hipErrorInvalidValue;  // BLK: the probe library only
 #endif
   variant &= 7;
+#ifdef TCPCK_PROBE
+  if (variant == 5) {  // (probe) the policy with its whole first step L2-kept, as before round 5
+    variant = 4;
+    flags |= 256;
+  }
+#endif
   int u8 = (variant & 1);
   int split = variant >= 2 ? 1 : 0;
   if (variant == 4) {
