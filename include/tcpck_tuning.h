@@ -55,7 +55,10 @@ extern "C" {
                                   with each XCD taking groups of 2/4/16/64
                                   consecutive runs; 20/21: 18/14 with the run's
                                   first step read with the default cache policy,
-                                  20 = the policy's; 22: 18 with every step read
+                                  20 = the policy's (since round 5 only the
+                                  run's first line, = 31; 32: the whole first
+                                  step, the policy before round 5); 22: 18 with
+                                  every step read
                                   with the default policy; 23/24: 20 with 8/2
                                   steps in flight; 25: 20's FILL with the fields
                                   stored by the write-through 2-B field pass,
@@ -76,8 +79,10 @@ extern "C" {
                                    with equal-count runs -- fixed layouts are
                                    always equal-count; 4: policy; + 8: each XCD
                                    takes groups of 16 consecutive runs; + 16: the
-                                   run's first step read with the default cache
-                                   policy; 28 = the policy's; + 32: FILL reads
+                                   run's first line read with the default cache
+                                   policy (5 instead of 4, probe library: its
+                                   whole first step, as before round 5); 28 =
+                                   the policy's; + 32: FILL reads
                                    every step with the default policy, AUTO's
                                    choice for packed fixed images below 320 B
                                    and variable means up to 448 B; + 64: FILL
