@@ -76,7 +76,7 @@ def main():
     VMS[:] = [int(x) for x in args.vms.split(",") if x]
     ctx = tcpck.Context(0, probe=True)
     s = torch.cuda.current_stream()
-    if "c2" in args.cases:
+    if "c2" in args.cases.split(","):
         n, L = 1 << 20, 1492
         arenas = []
         for _ in range(2):
@@ -98,7 +98,7 @@ def main():
         sweep("c2", arenas, run, params, n * L + 2 * n, s)
         del arenas, out
         torch.cuda.empty_cache()
-    if "c3" in args.cases:
+    if "c3" in args.cases.split(",") or "c3fixed" in args.cases:
         n = 4 << 20
         off, ln, total = synth_np.mixed_layout(n, seed=42)
         d_off, d_ln = torch.from_numpy(off).cuda(), torch.from_numpy(ln).cuda()
@@ -112,13 +112,20 @@ def main():
         kw = dict(total_bytes=img, min_len=int(ln.min()), max_len=int(ln.max()), packed=True, stream=s)
         run = lambda a, p: (ctx.batch_var(tcpck.OP_CHECKSUM, a, d_off, d_ln, n, out, **kw) if p is None else
                             ctx.batch_var_ex(tcpck.OP_CHECKSUM, a, d_off, d_ln, n, out, tcpck.KERNEL_VVSTREAM, p, **kw))
-        params = [("AUTO warm-up", None), ("AUTO", None)]
-        params += [("vvstream policy, whole first step kept (5)", 5 | 8 | 16), ("vvstream policy (AUTO)", 4 | 8 | 16),
+        params = [("AUTO warm-up", None), ("AUTO", None)] if "c3" in args.cases.split(",") else [("AUTO", None)]
+        params += [] if "c3" not in args.cases.split(",") else [("vvstream policy, whole first step kept (5)", 5 | 8 | 16), ("vvstream policy (AUTO)", 4 | 8 | 16),
                    ("vvstream policy, no kept line", 4 | 8)]
         for base, lab in ((3 | 8 | 16, "U8 xcd keep"), (3 | 8, "U8 xcd"), (2 | 8 | 16, "U4 xcd keep")):
             for m in VMS:
                 params.append((f"vvstream {lab} M{m}", base | (m << 16)))
         sweep("c3", arenas, run, params, img + 2 * n, s)
+        if "c3fixed" in args.cases:  # C3's bytes as a 736-B fixed stride: no descriptors, the same boundary density
+            L = 736
+            n2 = img // L
+            run2 = lambda a, p: (ctx.batch_fixed(tcpck.OP_CHECKSUM, a, L, L, n2, out, stream=s) if p is None else
+                                 ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, a, L, L, n2, out, p[0], p[1], stream=s))
+            sweep("736", arenas, run2, [("AUTO (rstream)", None), ("vvstream FIXED policy", (tcpck.KERNEL_VVSTREAM, 28))],
+                  n2 * L + 2 * n2, s)
     ctx.close()
 
 
