@@ -126,6 +126,28 @@ def main():
                                  ctx.batch_fixed_ex(tcpck.OP_CHECKSUM, a, L, L, n2, out, p[0], p[1], stream=s))
             sweep("736", arenas, run2, [("AUTO (rstream)", None), ("vvstream FIXED policy", (tcpck.KERNEL_VVSTREAM, 28))],
                   n2 * L + 2 * n2, s)
+    if "slots" in args.cases.split(","):
+        # the bench's receive ring, VERIFY (the `slots` key): sstream's block order and grid, cold
+        n, SL = 1 << 20, 2048
+        rng = np.random.default_rng(42)
+        ln = (np.asarray((64, 576, 1460), np.uint32)[rng.integers(0, 3, n)] + 32).astype(np.uint32)
+        off = np.arange(n, dtype=np.uint64) * np.uint64(SL)
+        d_off, d_ln = torch.from_numpy(off).cuda(), torch.from_numpy(ln).cuda()
+        arenas = []
+        for _ in range(2):
+            a = torch.empty(n * SL, dtype=torch.uint8, device="cuda")
+            tcpck.synth_var(a, d_off, d_ln, 1492, n, seed=42)
+            arenas.append(a)
+        img = int(ln.astype(np.int64).sum())
+        ok = torch.empty(n, dtype=torch.uint8, device="cuda")
+        kw = dict(total_bytes=img, min_len=int(ln.min()), max_len=int(ln.max()), sorted=True, stream=s)
+        run = lambda a, p: (ctx.batch_var(tcpck.OP_VERIFY, a, d_off, d_ln, n, ok, **kw) if p is None else
+                            ctx.batch_var_ex(tcpck.OP_VERIFY, a, d_off, d_ln, n, ok, tcpck.KERNEL_SSTREAM, p, **kw))
+        params = [("AUTO warm-up", None), ("AUTO", None)]
+        for order, lab in ((8, "scatter"), (0 | 1, "xcd-chunked"), (4, "default order")):
+            for m in (2, 4, 8, 16):
+                params.append((f"sstream {lab} M{m}", order | 1 | (m << 16)))
+        sweep("slots", arenas, run, params, img + n, s)
     ctx.close()
 
 
