@@ -139,6 +139,16 @@ extern "C" {
                                    policy)
                                    | (grid oversubscription << 16: 0 = by batch
                                    size, M = M x the resident grid)             */
+#define TCPCK_KERNEL_RVSTREAM 13 /* offset lists of packed images (PACKED: the
+                                   lengths of a run must add up to its span,
+                                   else the run takes an exact per-image pass),
+                                   MODE_REF, CHECKSUM / VERIFY: rstream's scalar
+                                   boundary walk over the lengths, one run per
+                                   wave; param = variant (0: policy = 4 steps in
+                                   flight, XCD-chunked order, the run's first
+                                   line L2-kept; probe library: 1: 8 in flight,
+                                   2: 2) | (grid oversubscription << 16: 0 = by
+                                   batch size, runs >= 4 KiB)                   */
 /* FILL in TCPCK_MODE_REF with a results buffer, any kernel (param bits, OR'ed
  * with the kernel's own param):
  *   TCPCK_PARAM_FILL_UPDATE    the kernel's CHECKSUM pass, then a field pass that

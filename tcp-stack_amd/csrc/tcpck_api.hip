@@ -707,6 +707,20 @@ hipError_t run_var_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const 
     a.dbg = static_cast<uint64_t *>(ctx->dbg);  // set by the probe library only
     return tcpck::launch_vvstream(op, param & 0xFF, false, a, static_cast<uint32_t>(ctx->num_cus), s);
   }
+  if (kernel == TCPCK_KERNEL_RVSTREAM) {  // packed offset lists, REF, CHECKSUM / VERIFY
+    if (mode != TCPCK_MODE_REF || op == TCPCK_OP_FILL || !out) return hipErrorInvalidValue;
+    tcpck::RunArgs a{};
+    a.mode = tcpck::kRef;
+    a.arena = arena;
+    a.offsets = off;
+    a.lengths = len;
+    a.base = base;
+    a.count = count;
+    a.out = out;
+    a.oversub = static_cast<uint32_t>(param >> 16) & 0xFFu;
+    a.total_bytes = layout ? layout->total_bytes : 0;
+    return tcpck::launch_rvstream(op, param & 0xFF, a, static_cast<uint32_t>(ctx->num_cus), s);
+  }
   if (kernel == TCPCK_KERNEL_SSTREAM) {  // any offset list (runs of <= 128 images)
     if (param & kSstreamDeferFill) {
       if (!patch) return hipErrorInvalidValue;

@@ -116,6 +116,9 @@ hipError_t launch_rstream(int op, int variant, const FixedStreamArgs &a, uint32_
 // variant 0 U4 byte split, 1 U8, 2 U4 count split, 3 U8 (fixed: 0/2 U4, 1/3 U8),
 // 4 = policy (oversubscription, split and loads in flight by size)
 hipError_t launch_vvstream(int op, int variant, bool fixed, const RunArgs &a, uint32_t num_cus, hipStream_t stream);
+// Packed offset lists with rstream's scalar boundary walk (tcpck_rvstream.hip):
+// CHECKSUM / VERIFY, reference mode; variant 0 = the policy.
+hipError_t launch_rvstream(int op, int variant, const RunArgs &a, uint32_t num_cus, hipStream_t stream);
 // ---- sstream (compacted slot stream), MODE_REF, all ops: images anywhere in
 // the arena -- fixed slots (fixed = true: stride % 16 == 0, stride >= len) or
 // offsets + lengths (fixed = false; runs of <= 128 images).  variant: 0 policy

@@ -53,6 +53,7 @@ KERNEL_VVSTREAM = 8  # packed variable or fixed (stride >= len): param = 0/1 U4/
 KERNEL_GSTREAM = 9  # fixed stride == len, len a power of two in [32, 1024], 16-B aligned arena: param = 0/1/2 U4/U8/U2 (+4 default block order) | oversub << 16
 KERNEL_PATCH = 12  # libtcpck_probe.so only (tcpck_probe.h): FILL's deferred field pass alone
 KERNEL_SSTREAM = 10  # slotted layouts (fixed slots, stride % 16 == 0, or any offset list): param = 0 policy (U4, scattered order), 1 U4, 2 U8 (+4 default block order, +8 scattered) | oversub << 16
+KERNEL_RVSTREAM = 13  # packed offset lists, REF, CHECKSUM / VERIFY: rstream's scalar walk over the lengths
 SEG_SHAPES = {1: "G8/U2", 2: "G16/U6", 3: "G64/U4", 4: "G64/U2", 5: "G32/U3", 6: "G4/U8", 7: "W4/U4", 8: "W8/U4", 9: "W16/U2", 10: "W16/U4", 11: "W2/U4"}
 # include/tcpck_tuning.h: in libtcpck.so (AUTO's kernels only) and libtcpck_probe.so
 TUNING_EXPORTS = ("tcpck_batch_fixed_ex", "tcpck_batch_var_ex", "tcpck_batch_segment_ex", "tcpck_batch_receive_ex")
