@@ -177,10 +177,12 @@ __global__ void __launch_bounds__(kBlock) rvstream_kernel(RVArgs a) {
 }
 
 template <int U, int OP>
-hipError_t launch_one(const RunArgs &s, uint32_t m, uint32_t num_cus, hipStream_t stream) {
+hipError_t launch_one(const RunArgs &s, uint32_t num_cus, hipStream_t stream) {
   static const uint32_t per_cu = dev::resident_blocks_per_cu(rvstream_kernel<U, OP>);
   const uint64_t resident = static_cast<uint64_t>(per_cu) * num_cus;
-  uint64_t blocks = resident * m;
+  // M x the resident grid as rstream: the largest power of two keeping runs >= 4 KiB
+  const uint64_t bytes = s.total_bytes ? s.total_bytes : s.count * 1024;
+  uint64_t blocks = resident * dev::oversub_for(s.oversub, bytes, resident * kWavesPerBlock, 1024);
   const uint64_t need = (s.count + kWavesPerBlock - 1) / kWavesPerBlock;  // >= 1 image per wave
   if (blocks > need) blocks = need;
   if (blocks == 0) return hipSuccess;
@@ -205,15 +207,13 @@ hipError_t launch_one(const RunArgs &s, uint32_t m, uint32_t num_cus, hipStream_
 hipError_t launch_rvstream(int op, int variant, const RunArgs &a, uint32_t num_cus, hipStream_t stream) {
   if (a.count == 0) return hipSuccess;
   if (a.mode != kRef || !a.out || (op != kChecksum && op != kVerify)) return hipErrorInvalidValue;
-  const uint64_t bytes = a.total_bytes ? a.total_bytes : a.count * 1024;
-  const uint32_t m = dev::oversub_for(a.oversub, bytes, static_cast<uint64_t>(num_cus) * 32, 1024);
   if (variant == 0)
-    return op == kVerify ? launch_one<4, kVerify>(a, m, num_cus, stream) : launch_one<4, kChecksum>(a, m, num_cus, stream);
+    return op == kVerify ? launch_one<4, kVerify>(a, num_cus, stream) : launch_one<4, kChecksum>(a, num_cus, stream);
 #ifdef TCPCK_PROBE
   if (variant == 1)
-    return op == kVerify ? launch_one<8, kVerify>(a, m, num_cus, stream) : launch_one<8, kChecksum>(a, m, num_cus, stream);
+    return op == kVerify ? launch_one<8, kVerify>(a, num_cus, stream) : launch_one<8, kChecksum>(a, num_cus, stream);
   if (variant == 2)
-    return op == kVerify ? launch_one<2, kVerify>(a, m, num_cus, stream) : launch_one<2, kChecksum>(a, m, num_cus, stream);
+    return op == kVerify ? launch_one<2, kVerify>(a, num_cus, stream) : launch_one<2, kChecksum>(a, num_cus, stream);
 #endif
   return hipErrorInvalidValue;
 }
