@@ -26,7 +26,8 @@
 //     before the byte (v_readlane), the image's sum P - P_prev staged in lane
 //     k mod 64 of a VGPR, 64 results per store;
 //   * a run whose lengths do not add up to its span (the PACKED hint wrong)
-//     takes the exact per-image pass.
+//     rewrites its results by the exact per-image pass (CHECKSUM / VERIFY
+//     write only out[], so the check can wait for the walk's end).
 // CHECKSUM and VERIFY, reference mode.  (AUTO's C3 FILL is CHECKSUM's stream
 // followed by the field-update pass, so it runs on this stream too.)
 #include "tcpck_device.h"
@@ -97,15 +98,7 @@ __global__ void __launch_bounds__(kBlock) rvstream_kernel(RVArgs a) {
     const uint32_t *lens = a.lengths + kb;
     uint32_t vlen = lane < nimg ? lens[lane] : 0u;
     uint32_t vnext = lane + 64 < nimg ? lens[lane + 64] : 0u;
-    // the lengths must add up to the span (the PACKED contract): checked before any result
-    if (nimg <= 128) {
-      bad = lead + dev::group_sum<64>(vlen + vnext) != span;
-    } else {
-      uint32_t sum = 0;
-      for (uint32_t j = lane; j < nimg; j += 64) sum += lens[j];
-      bad = lead + dev::group_sum<64>(sum) != span;
-    }
-    if (!bad) {
+    {
       uint32_t nb = lead + dev::read_lane(vlen, 0);  // end of run image jn - 1
       uint32_t jn = 1;
       uint32_t carry = 0, p_last = 0;
@@ -162,9 +155,19 @@ __global__ void __launch_bounds__(kBlock) rvstream_kernel(RVArgs a) {
       for (; jn < nimg; ++jn) {
         emit(jn - 1, carry - p_last);
         p_last = carry;
+        if ((jn & 63u) == 0) {
+          vlen = vnext;
+          const uint32_t j2 = jn + 64 + lane;
+          vnext = j2 < nimg ? lens[j2] : 0u;
+        }
+        nb += dev::read_lane(vlen, jn & 63u);
       }
       emit(nimg - 1, carry - p_last);  // the last image ends at the run end
       if (nimg > out_rel) flush(nimg - out_rel);
+      // the lengths must add up to the span (the PACKED contract): nb is now the
+      // end of the run's last image by its lengths.  If they do not, the results
+      // above are rewritten by the exact pass below (only out[] was written).
+      bad = nb != span;
     }
   }
   if (bad) {  // wave-uniform: the layout is not the packed run the walk assumed -> exact per-image pass
