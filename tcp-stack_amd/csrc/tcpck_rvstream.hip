@@ -60,11 +60,16 @@ __global__ void __launch_bounds__(kBlock) rvstream_kernel(RVArgs a) {
   uint64_t kb, ke;
   dev::count_split(wid, a.per_wave, a.rem, kb, ke);
   if (kb >= ke) return;
+  const uint32_t nimg = static_cast<uint32_t>(ke - kb);
+  // lengths of run images [64 i, 64 i + 64): lane l holds image 64 i + l's.  The
+  // first batch depends only on kb: its load goes out with the offsets', before
+  // the data loads (which wait for the run's start), so it is in when the walk begins
+  const uint32_t *lens = a.lengths + kb;
+  uint32_t vlen = lane < nimg ? lens[lane] : 0u;
   const uint64_t s0 = a.offsets[kb] - a.base;
   const uint64_t s1 = a.offsets[ke - 1] - a.base + a.lengths[ke - 1];
   uint8_t *const arena = a.arena;
   const uint64_t A0 = dev::align128_rel(arena, s0);
-  const uint32_t nimg = static_cast<uint32_t>(ke - kb);
   bool bad = !(s1 >= s0 && s1 - A0 < (uint64_t{1} << 31));
 
   auto store = [&](uint64_t k, uint16_t c) {
@@ -94,9 +99,6 @@ __global__ void __launch_bounds__(kBlock) rvstream_kernel(RVArgs a) {
         ring[u] = dev::load16_buf_nt(rsrc, lane << 4, static_cast<uint32_t>(u) << 10);
       }
     }
-    // lengths of run images [64 i, 64 i + 64): lane l holds image 64 i + l's
-    const uint32_t *lens = a.lengths + kb;
-    uint32_t vlen = lane < nimg ? lens[lane] : 0u;
     uint32_t vnext = lane + 64 < nimg ? lens[lane + 64] : 0u;
     {
       uint32_t nb = lead + dev::read_lane(vlen, 0);  // end of run image jn - 1
