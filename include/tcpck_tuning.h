@@ -139,7 +139,9 @@ extern "C" {
                                    policy)
                                    | (grid oversubscription << 16: 0 = by batch
                                    size, M = M x the resident grid)             */
-#define TCPCK_KERNEL_RVSTREAM 13 /* offset lists of packed images (PACKED: the
+#define TCPCK_KERNEL_RVSTREAM 13 /* libtcpck_probe.so only (measured below
+                                   vvstream on C3):
+                                   offset lists of packed images (PACKED: the
                                    lengths of a run must add up to its span,
                                    else the run takes an exact per-image pass),
                                    MODE_REF, CHECKSUM / VERIFY: rstream's scalar

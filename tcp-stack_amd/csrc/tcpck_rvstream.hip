@@ -28,12 +28,20 @@
 //   * a run whose lengths do not add up to its span (the PACKED hint wrong)
 //     rewrites its results by the exact per-image pass (CHECKSUM / VERIFY
 //     write only out[], so the check can wait for the walk's end).
-// CHECKSUM and VERIFY, reference mode.  (AUTO's C3 FILL is CHECKSUM's stream
-// followed by the field-update pass, so it runs on this stream too.)
+// CHECKSUM and VERIFY, reference mode.
+//
+// Measured against vvstream (scripts/rvstream_probe.py, cold, profiles/r05/
+// rvstream_probe*.log): C3 85.2 % at its best grid (U2, M 32) against 86.6 %,
+// 1492-B images as an offset list 86.6 against 85.1 %, 639-B mean 75.7 vs
+// 82.9 %, 159-B mean 28 vs 75 %.  Either kernel pays one descriptor round trip
+// per run before its first data load, which the fixed-stride walk never does
+// (rstream C2 92.3 %); the walk itself is not what costs.  Not AUTO's: the
+// probe library only.
 #include "tcpck_device.h"
 
 namespace tcpck {
 
+#ifdef TCPCK_PROBE
 namespace {
 
 using dev::kBlock;
@@ -206,19 +214,26 @@ hipError_t launch_one(const RunArgs &s, uint32_t num_cus, hipStream_t stream) {
 }
 
 }  // namespace
+#endif
 
-// variant: 0 = the policy (U4; M by size, runs >= 4 KiB as rstream); probe
-// library: 1 = U8, 2 = U2 (param >> 16 = M for either).
+// variant: 0 = U4, 1 = U8, 2 = U2 (M by size, runs >= 4 KiB as rstream;
+// param >> 16 = M).  The product library refuses it.
 hipError_t launch_rvstream(int op, int variant, const RunArgs &a, uint32_t num_cus, hipStream_t stream) {
+#ifdef TCPCK_PROBE
   if (a.count == 0) return hipSuccess;
   if (a.mode != kRef || !a.out || (op != kChecksum && op != kVerify)) return hipErrorInvalidValue;
   if (variant == 0)
     return op == kVerify ? launch_one<4, kVerify>(a, num_cus, stream) : launch_one<4, kChecksum>(a, num_cus, stream);
-#ifdef TCPCK_PROBE
   if (variant == 1)
     return op == kVerify ? launch_one<8, kVerify>(a, num_cus, stream) : launch_one<8, kChecksum>(a, num_cus, stream);
   if (variant == 2)
     return op == kVerify ? launch_one<2, kVerify>(a, num_cus, stream) : launch_one<2, kChecksum>(a, num_cus, stream);
+#else
+  (void)op;
+  (void)variant;
+  (void)a;
+  (void)num_cus;
+  (void)stream;
 #endif
   return hipErrorInvalidValue;
 }

@@ -59,16 +59,17 @@ def test_product_library_holds_only_auto_kernels(built_lib):
     """libtcpck.so carries the kernels the AUTO policy can pick and nothing
     else (measurement-only code out of the product): rstream only
     as the policy's instantiation <U4, op, no stamps, no priority, flavour
-    263 (7 + the first line only L2-kept, round 5), REF / RFC 1071>; rvstream
-    as <U4, CHECKSUM / VERIFY>; no diag kernels; fewer instantiations than the
-    probe build for every kernel that has measurement-only variants."""
+    263 (7 + the first line only L2-kept, round 5), REF / RFC 1071>; no
+    rvstream (a measured alternative, not AUTO's); no diag kernels; fewer
+    instantiations than the probe build for every kernel that has
+    measurement-only variants."""
     import tcpck
     prod, probe = _kernels(tcpck.LIB_PATH), _kernels(tcpck.PROBE_PATH)
     assert set(prod["rstream_kernel"]) == {f"Li4ELi{op}ELb0ELi0ELi263ELi{m}E" for op in range(3) for m in range(2)}
-    assert set(prod["rvstream_kernel"]) == {"Li4ELi0E", "Li4ELi2E"}
+    assert "rvstream_kernel" not in prod and "rvstream_kernel" in probe
     blobs = [open(p, "rb").read() for p in (tcpck.LIB_PATH, tcpck.PROBE_PATH)]
     assert b"diag_stream_kernel" not in blobs[0] and b"diag_stream_kernel" in blobs[1]
-    for k in ("rstream_kernel", "rvstream_kernel", "seg_kernel", "gstream_kernel", "sstream_kernel", "segment_kernel"):
+    for k in ("rstream_kernel", "seg_kernel", "gstream_kernel", "sstream_kernel", "segment_kernel"):
         assert len(prod[k]) < len(probe[k]), k
 
 

@@ -1,5 +1,5 @@
 """GPU parity: rvstream, rstream's scalar boundary walk over packed offset
-lists (TCPCK_KERNEL_RVSTREAM, round 5).
+lists (TCPCK_KERNEL_RVSTREAM, round 5; libtcpck_probe.so only).
 
 Every result against the oracle (oracle/ref16.c restating
 include/tcp-header.h:252-263, pinned by tests/golden): CHECKSUM u16 and VERIFY
@@ -24,14 +24,6 @@ def pctx(built_lib):
     import tcpck
     assert torch.cuda.is_available(), "gpu tests need a GPU"
     c = tcpck.Context(0, probe=True)
-    yield c
-    c.close()
-
-
-@pytest.fixture(scope="module")
-def ctx(built_lib):
-    import tcpck
-    c = tcpck.Context(0)
     yield c
     c.close()
 
@@ -107,7 +99,7 @@ def test_rvstream_variants_grids(pctx, oracle_c, variant, m, op):
     _run(pctx, oracle_c, _lens("c3", 60000, rng), 6, o, variant | (m << 16), seed)
 
 
-def test_rvstream_verify_filled(ctx, oracle_c):
+def test_rvstream_verify_filled(pctx, oracle_c):
     """VERIFY on images after the reference's insert: all 1, then one bit flipped per 7th image."""
     import tcpck
     import synth_np
@@ -116,17 +108,17 @@ def test_rvstream_verify_filled(ctx, oracle_c):
     a = torch.empty(total, dtype=torch.uint8, device="cuda")
     d_off, d_ln = dev(off), dev(ln)
     tcpck.synth_var(a, d_off, d_ln, 1492, n, seed=5)
-    ctx.batch_var(tcpck.OP_FILL, a, d_off, d_ln, n, None)
+    pctx.batch_var(tcpck.OP_FILL, a, d_off, d_ln, n, None)
     ok = torch.empty(n, dtype=torch.uint8, device="cuda")
     hints = dict(total_bytes=int(ln.astype(np.int64).sum()), min_len=int(ln.min()), max_len=int(ln.max()), packed=True)
-    ctx.batch_var_ex(tcpck.OP_VERIFY, a, d_off, d_ln, n, ok, tcpck.KERNEL_RVSTREAM, 0, **hints)
+    pctx.batch_var_ex(tcpck.OP_VERIFY, a, d_off, d_ln, n, ok, tcpck.KERNEL_RVSTREAM, 0, **hints)
     assert int(ok.sum(dtype=torch.int64).item()) == n
     bad = np.arange(0, n, 7)
     h = a.cpu().numpy()
     pos = off[bad].astype(np.int64) + 40
     h[pos] ^= 0x10
     a.copy_(torch.from_numpy(h))
-    ctx.batch_var_ex(tcpck.OP_VERIFY, a, d_off, d_ln, n, ok, tcpck.KERNEL_RVSTREAM, 0, **hints)
+    pctx.batch_var_ex(tcpck.OP_VERIFY, a, d_off, d_ln, n, ok, tcpck.KERNEL_RVSTREAM, 0, **hints)
     want = np.ones(n, np.uint8)
     want[bad] = 0
     np.testing.assert_array_equal(ok.cpu().numpy(), want)
@@ -151,8 +143,8 @@ def test_rvstream_not_packed_recomputes(pctx, oracle_c, layout):
     _run(pctx, oracle_c, ln, 0, tcpck.OP_CHECKSUM, 0, 11, offsets=off)
 
 
-def test_rvstream_c3_full(ctx, oracle_c):
-    """C3's whole batch (4M images, the bench's seeds) through the product library's rvstream."""
+def test_rvstream_c3_full(pctx, oracle_c):
+    """C3's whole batch (4M images, the bench's seeds)."""
     import tcpck
     import synth_np
     count = 4 << 20
@@ -161,7 +153,7 @@ def test_rvstream_c3_full(ctx, oracle_c):
     d_off, d_ln = dev(off), dev(ln)
     tcpck.synth_var(a, d_off, d_ln, 1492, count, seed=42)
     out = torch.empty(count, dtype=torch.int16, device="cuda")
-    ctx.batch_var_ex(tcpck.OP_CHECKSUM, a, d_off, d_ln, count, out, tcpck.KERNEL_RVSTREAM, 0,
+    pctx.batch_var_ex(tcpck.OP_CHECKSUM, a, d_off, d_ln, count, out, tcpck.KERNEL_RVSTREAM, 0,
                      total_bytes=int(ln.astype(np.int64).sum()), min_len=int(ln.min()), max_len=int(ln.max()),
                      packed=True)
     exp = oracle_c.batch(a.cpu().numpy(), off, ln, threads=16)
@@ -177,3 +169,18 @@ def test_rvstream_rejects(pctx):
     for op, mode, o in ((tcpck.OP_FILL, 0, out), (tcpck.OP_CHECKSUM, 1, out), (tcpck.OP_CHECKSUM, 0, None)):
         with pytest.raises(tcpck.TcpckError):
             pctx.batch_var_ex(op, a, off, ln, 4, o, tcpck.KERNEL_RVSTREAM, 0, mode=mode)
+
+
+def test_rvstream_refused_by_the_product(built_lib):
+    """Not AUTO's kernel: the product library refuses it (hipErrorInvalidValue)."""
+    import tcpck
+    c = tcpck.Context(0)
+    try:
+        a = torch.zeros(4096, dtype=torch.uint8, device="cuda")
+        off = dev(np.arange(4, dtype=np.uint64) * 1024)
+        ln = dev(np.full(4, 1024, np.uint32))
+        out = torch.empty(4, dtype=torch.int16, device="cuda")
+        with pytest.raises(tcpck.TcpckError):
+            c.batch_var_ex(tcpck.OP_CHECKSUM, a, off, ln, 4, out, tcpck.KERNEL_RVSTREAM, 0, packed=True)
+    finally:
+        c.close()
