@@ -45,7 +45,7 @@ def b2b(fn, s, reps=20, rounds=5):
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--mixes", default=",".join(MIXES))
-    p.add_argument("--forms", default="0,1,2", help="rvstream variants (0 policy U4, 1 U8, 2 U2)")
+    p.add_argument("--forms", default="0,1,2", help="rvstream variants (0 policy U4, 1 U8, 2 U2, 3 U4 + run table, 4 U2 + run table)")
     p.add_argument("--ms", default="0", help="rvstream grid multipliers (0 = by size)")
     args = p.parse_args()
     ctx = tcpck.Context(0, probe=True)

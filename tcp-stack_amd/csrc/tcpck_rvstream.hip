@@ -57,7 +57,20 @@ struct RVArgs {
   void *out;               // u16 (CHECKSUM) or u8 (VERIFY)
   uint64_t per_wave, rem;  // equal-count split: count = per_wave * waves + rem
   uint32_t order;          // block order (dev::ordered_block)
+  const uint64_t *table;   // variant 3: run r's byte span [table[r], table[r + 1]) (run_table_kernel)
 };
+
+// Variant 3 (probe): every run's start in one dense table, built by a pass
+// before the stream, so a run's span comes from a line 16 runs share (in L2
+// for most of them) instead of its own line of the offsets array.
+__global__ void run_table_kernel(const uint64_t *offsets, const uint32_t *lengths, uint64_t base, uint64_t count,
+                                 uint64_t per_wave, uint64_t rem, uint64_t runs, uint64_t *table) {
+  const uint64_t r = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (r > runs) return;
+  const uint64_t end = offsets[count - 1] - base + lengths[count - 1];
+  const uint64_t kb = r * per_wave + (r < rem ? r : rem);
+  table[r] = kb < count ? offsets[kb] - base : end;
+}
 
 template <int U, int OP>
 __global__ void __launch_bounds__(kBlock) rvstream_kernel(RVArgs a) {
@@ -74,8 +87,8 @@ __global__ void __launch_bounds__(kBlock) rvstream_kernel(RVArgs a) {
   // the data loads (which wait for the run's start), so it is in when the walk begins
   const uint32_t *lens = a.lengths + kb;
   uint32_t vlen = lane < nimg ? lens[lane] : 0u;
-  const uint64_t s0 = a.offsets[kb] - a.base;
-  const uint64_t s1 = a.offsets[ke - 1] - a.base + a.lengths[ke - 1];
+  const uint64_t s0 = a.table ? a.table[wid] : a.offsets[kb] - a.base;
+  const uint64_t s1 = a.table ? a.table[wid + 1] : a.offsets[ke - 1] - a.base + a.lengths[ke - 1];
   uint8_t *const arena = a.arena;
   const uint64_t A0 = dev::align128_rel(arena, s0);
   bool bad = !(s1 >= s0 && s1 - A0 < (uint64_t{1} << 31));
@@ -190,7 +203,7 @@ __global__ void __launch_bounds__(kBlock) rvstream_kernel(RVArgs a) {
 }
 
 template <int U, int OP>
-hipError_t launch_one(const RunArgs &s, uint32_t num_cus, hipStream_t stream) {
+hipError_t launch_one(const RunArgs &s, uint32_t num_cus, hipStream_t stream, bool table = false) {
   static const uint32_t per_cu = dev::resident_blocks_per_cu(rvstream_kernel<U, OP>);
   const uint64_t resident = static_cast<uint64_t>(per_cu) * num_cus;
   // M x the resident grid as rstream: the largest power of two keeping runs >= 4 KiB
@@ -209,6 +222,21 @@ hipError_t launch_one(const RunArgs &s, uint32_t num_cus, hipStream_t stream) {
   a.per_wave = s.count / (blocks * kWavesPerBlock);
   a.rem = s.count % (blocks * kWavesPerBlock);
   a.order = 4u;  // XCD-chunked: groups of 16 blocks per XCD
+  if (table) {  // (probe) a process-wide table buffer, grown as needed: measurement only
+    static uint64_t *g_table = nullptr;
+    static uint64_t g_cap = 0;
+    const uint64_t runs = blocks * kWavesPerBlock;
+    if (runs + 1 > g_cap) {
+      if (g_table) (void)hipFree(g_table);
+      g_table = nullptr;
+      g_cap = 0;
+      if (hipMalloc(&g_table, (runs + 1) * 8) != hipSuccess) return hipErrorOutOfMemory;
+      g_cap = runs + 1;
+    }
+    hipLaunchKernelGGL(run_table_kernel, dim3(static_cast<uint32_t>((runs + 256) / 256)), dim3(256), 0, stream,
+                       s.offsets, s.lengths, s.base, s.count, a.per_wave, a.rem, runs, g_table);
+    a.table = g_table;
+  }
   hipLaunchKernelGGL((rvstream_kernel<U, OP>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0, stream, a);
   return hipGetLastError();
 }
@@ -228,6 +256,11 @@ hipError_t launch_rvstream(int op, int variant, const RunArgs &a, uint32_t num_c
     return op == kVerify ? launch_one<8, kVerify>(a, num_cus, stream) : launch_one<8, kChecksum>(a, num_cus, stream);
   if (variant == 2)
     return op == kVerify ? launch_one<2, kVerify>(a, num_cus, stream) : launch_one<2, kChecksum>(a, num_cus, stream);
+  if (variant == 3 || variant == 4)  // 0 / 2 with the run table (packed batches only: a run's end is the next's start)
+    return variant == 3 ? (op == kVerify ? launch_one<4, kVerify>(a, num_cus, stream, true)
+                                         : launch_one<4, kChecksum>(a, num_cus, stream, true))
+                        : (op == kVerify ? launch_one<2, kVerify>(a, num_cus, stream, true)
+                                         : launch_one<2, kChecksum>(a, num_cus, stream, true));
 #else
   (void)op;
   (void)variant;

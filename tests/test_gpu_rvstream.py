@@ -87,7 +87,7 @@ def test_rvstream_checksum(pctx, oracle_c, kind, n, m):
     _run(pctx, oracle_c, _lens(kind, n, rng), 2 * (seed % 64), tcpck.OP_CHECKSUM, m << 16, seed)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
 @pytest.mark.parametrize("m", [0, 2, 16, 256])
 @pytest.mark.parametrize("op", ["checksum", "verify"])
 def test_rvstream_variants_grids(pctx, oracle_c, variant, m, op):
