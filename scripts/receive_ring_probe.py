@@ -7,7 +7,9 @@ lines in the 256-MB Infinity Cache -- and, for comparison, on one ring.
 Forms: AUTO (since round 5 the header pass FIRST: its 128 MB of first lines
 are then in the Infinity Cache when the VERIFY stream reads them), the header
 pass after VERIFY (tcpck_probe.h PROBE_RECEIVE_HDR_AFTER, the order before
-round 5), VERIFY alone.  --layout: the bench ring (offset list), 1492-B
+round 5), sstream emitting each header from the stream's registers (one
+launch; AUTO's form for rings of small datagrams, kernel SSTREAM param 32),
+VERIFY alone.  --layout: the bench ring (offset list), 1492-B
 images in 2048-B fixed slots, or C2's packed fixed 1492-B images.  Back-to-back launches, median of 5 rounds; verdicts and header
 arrays compared with AUTO's."""
 import argparse
@@ -78,6 +80,8 @@ def main():
         "AUTO (headers first)": lambda a: ctx.batch_receive(a, count, ok, hdr, **kw),
         "headers after VERIFY": lambda a: ctx.batch_receive(a, count, ok, hdr, kernel=tcpck.KERNEL_AUTO,
                                                             probe_flags=tcpck.PROBE_RECEIVE_HDR_AFTER, **kw),
+        "sstream, headers in-stream": lambda a: ctx.batch_receive(a, count, ok, hdr, kernel=tcpck.KERNEL_SSTREAM,
+                                                                  param=32, **kw),
         "VERIFY alone": verify,
     }
     ref = None
