@@ -73,6 +73,8 @@ def main():
         out = torch.empty(n, dtype=torch.int16, device="cuda")
         kw = dict(total_bytes=img, min_len=int(ln.min()), max_len=int(ln.max()), packed=True, stream=s)
         forms = [("AUTO warm-up", None), ("AUTO", None)]
+        if name == "c1492":  # the same bytes as a fixed stride: AUTO's fixed kernel (rstream)
+            forms.append(("fixed stride AUTO", -1))
         for v in (int(x) for x in args.forms.split(",")):
             for m in (int(x) for x in args.ms.split(",")):
                 forms.append((f"rvstream {v} M{m or 'policy'}", v | (m << 16)))
@@ -83,7 +85,9 @@ def main():
             def step():
                 a = arenas[turn[0] % 2]
                 turn[0] += 1
-                if prm is None:
+                if prm == -1:
+                    ctx.batch_fixed(tcpck.OP_CHECKSUM, a, 1492, 1492, n, out, stream=s)
+                elif prm is None:
                     ctx.batch_var(tcpck.OP_CHECKSUM, a, d_off, d_ln, n, out, **kw)
                 else:
                     ctx.batch_var_ex(tcpck.OP_CHECKSUM, a, d_off, d_ln, n, out, tcpck.KERNEL_RVSTREAM, prm, **kw)
