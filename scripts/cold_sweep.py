@@ -70,6 +70,8 @@ def main():
     ap.add_argument("--rs", default="20,18,22,23,24", help="rstream variants (C2)")
     ap.add_argument("--ms", default="16,32,64", help="grid multipliers (C2)")
     ap.add_argument("--vms", default="16,32,64", help="grid multipliers (C3)")
+    ap.add_argument("--sms", default="2,4,8,16", help="grid multipliers (slots)")
+    ap.add_argument("--sorders", default="scatter,xcd-chunked,default order", help="block orders (slots)")
     args = ap.parse_args()
     VARIANTS[:] = [int(x) for x in args.rs.split(",")]
     MS[:] = [int(x) for x in args.ms.split(",")]
@@ -145,7 +147,9 @@ def main():
                             ctx.batch_var_ex(tcpck.OP_VERIFY, a, d_off, d_ln, n, ok, tcpck.KERNEL_SSTREAM, p, **kw))
         params = [("AUTO warm-up", None), ("AUTO", None)]
         for order, lab in ((8, "scatter"), (0 | 1, "xcd-chunked"), (4, "default order")):
-            for m in (2, 4, 8, 16):
+            if lab not in args.sorders.split(","):
+                continue
+            for m in (int(x) for x in args.sms.split(",")):
                 params.append((f"sstream {lab} M{m}", order | 1 | (m << 16)))
         sweep("slots", arenas, run, params, img + n, s)
     ctx.close()

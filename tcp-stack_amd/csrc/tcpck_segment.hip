@@ -295,11 +295,20 @@ hipError_t launch_one(SegmentArgs a, uint32_t oversub, uint32_t num_cus, hipStre
   static const uint32_t per_cu = dev::resident_blocks_per_cu(segment_kernel<U, MODE, SPOL, LPOL>);
   const uint64_t resident = static_cast<uint64_t>(per_cu) * num_cus;
   const uint64_t out_bytes = a.count * static_cast<uint64_t>(a.stride);
-  // runs of >= 3 KiB of output (two 1.5-KB images), M a power of two up to
-  // 1024: at 1.6 GB of images M = 64, 71-72 % of the roof in read + write
-  // traffic against 60-67 % at M = 16-32 and a plain device copy's 61 %
-  // (scripts/segment_probe.py, profiles/r02/segment_probe2.log)
-  uint64_t blocks = resident * dev::oversub_for(oversub, out_bytes, resident * kWavesPerBlock, 1024, 3u << 10);
+  // runs of ~3 KiB of output (two 1.5-KB images): M = the power of two
+  // nearest (in ratio) to out_bytes / (resident waves x 3 KiB), up to 1024.
+  // Measured cold at 0.40 / 1.58 / 6.6 GB of images, the best M is the power
+  // of two giving 3.0-3.2-KiB runs (69.3 % at M 16, 71.0 % at M 64, 68.9 % at
+  // M 256 of the roof in read + write traffic; M 56 / 72 at 1.58 GB 69.7 /
+  // 69.8 %); rounding DOWN to a power of two put the bench's 1.58 GB at M 32
+  // (6-KiB runs, 66.7 %) (scripts/segment_probe.py, profiles/r05/segment_m_*.log)
+  uint64_t m = oversub;
+  if (!m) {
+    const double q = static_cast<double>(out_bytes) / static_cast<double>(resident * kWavesPerBlock * (3u << 10));
+    m = 1;
+    while (m < 1024 && q >= 1.4142135623730951 * static_cast<double>(m)) m *= 2;
+  }
+  uint64_t blocks = resident * m;
   const uint64_t need = (a.count + kWavesPerBlock - 1) / kWavesPerBlock;
   // runs below 2^30 bytes of output (u32 run arithmetic)
   const uint64_t per_max = std::max<uint64_t>(1, (uint64_t{1} << 30) / a.stride);
