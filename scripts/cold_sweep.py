@@ -71,6 +71,7 @@ def main():
     ap.add_argument("--ms", default="16,32,64", help="grid multipliers (C2)")
     ap.add_argument("--vms", default="16,32,64", help="grid multipliers (C3)")
     ap.add_argument("--sms", default="2,4,8,16", help="grid multipliers (slots)")
+    ap.add_argument("--c2n", type=int, default=1 << 20, help="images of the c2 case (8388608: C5 on one GPU)")
     ap.add_argument("--sorders", default="scatter,xcd-chunked,default order", help="block orders (slots)")
     args = ap.parse_args()
     VARIANTS[:] = [int(x) for x in args.rs.split(",")]
@@ -79,7 +80,7 @@ def main():
     ctx = tcpck.Context(0, probe=True)
     s = torch.cuda.current_stream()
     if "c2" in args.cases.split(","):
-        n, L = 1 << 20, 1492
+        n, L = args.c2n, 1492
         arenas = []
         for _ in range(2):
             a = torch.empty(n * L, dtype=torch.uint8, device="cuda")

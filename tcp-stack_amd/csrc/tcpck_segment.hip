@@ -283,8 +283,12 @@ hipError_t launch_wide(SegmentArgs a, uint32_t oversub, uint32_t num_cus, hipStr
       nb = 1;
     return static_cast<uint32_t>(nb);
   }();
+  // one block per image up to 64 x the resident grid (grid-stride past it):
+  // cold, 1.6 GB of stream, 9000 / 16000 / 65532-B segments ran 65.2 / 63.6 /
+  // 66.8 % of the roof (read + write) at the former 4 x, 70.2 / 69.1 / 70.1 % at
+  // 64 x (profiles/r05/segment_wide2_s5.log)
   uint64_t blocks = a.count;
-  const uint64_t cap = static_cast<uint64_t>(per_cu) * num_cus * (oversub ? oversub : 4);
+  const uint64_t cap = static_cast<uint64_t>(per_cu) * num_cus * (oversub ? oversub : 64);
   if (blocks > cap) blocks = cap;
   hipLaunchKernelGGL((segment_wide_kernel<W, U, MODE>), dim3(static_cast<uint32_t>(blocks)), dim3(64 * W), 0, stream, a);
   return hipGetLastError();
