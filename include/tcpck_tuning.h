@@ -182,9 +182,15 @@ extern "C" {
 int tcpck_batch_fixed_ex(tcpck_ctx *ctx, int op, int mode, void *d_arena,
                          uint64_t stride, uint32_t len, uint64_t count, void *d_out,
                          int kernel, int param, tcpck_stream stream);
-/* tcpck_batch_segment (tcpck.h) with param = variant (0: policy = 4 steps in
- * flight, nt stores; 1: 8 in flight; 2: default-policy stores; 3: sc1 stores;
- * + 8: default block order, else XCD-chunked) | (grid oversubscription << 16). */
+/* tcpck_batch_segment (tcpck.h) with param = variant | (grid << 16).  Variant 0
+ * (+ 8: default block order, else XCD-chunked) is AUTO's form: segments below
+ * 8 KiB one run of whole images per wave, 4 steps in flight, default-policy
+ * loads and stores, M x the resident grid with M the power of two nearest runs
+ * of 3 KiB of output (grid bits: M instead); segments of 8 KiB and more one
+ * block of 4 (16 KiB and more: 16) waves per image, up to 64 x the resident
+ * grid (grid bits: that multiple instead).  Variants 1-7 and 0x40 / 0x80 (store
+ * and load policies, 8 steps in flight, waves per image) are in
+ * libtcpck_probe.so only. */
 int tcpck_batch_segment_ex(tcpck_ctx *ctx, int mode, const void *d_payload, uint64_t payload_bytes,
                            uint32_t seg, const void *hdr, uint32_t seq0, void *d_images, uint64_t stride,
                            uint16_t *d_out, int param, tcpck_stream stream);

@@ -66,7 +66,8 @@ def test_segment_golden(ctx, segment_golden, pad):
         assert list(cs) == c["checksums"], c["name"]
 
 
-PARAMS = [None, 0, 1, 2, 3, 4, 5, 6, 7, 0x17, 0x27, 8, 0 | (1 << 16), 2 | (8 << 16), 4 | (128 << 16), 7 | (2 << 16)]
+PARAMS = [None, 0, 1, 2, 3, 4, 5, 6, 7, 0x17, 0x27, 8, 0 | (1 << 16), 0 | (3 << 16), 0 | (48 << 16), 2 | (8 << 16),
+          4 | (128 << 16), 7 | (2 << 16), 7 | (600 << 16)]
 
 
 @pytest.mark.parametrize("param", PARAMS)
