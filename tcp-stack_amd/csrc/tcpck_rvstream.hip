@@ -222,7 +222,8 @@ hipError_t launch_one(const RunArgs &s, uint32_t num_cus, hipStream_t stream, bo
   a.per_wave = s.count / (blocks * kWavesPerBlock);
   a.rem = s.count % (blocks * kWavesPerBlock);
   a.order = 4u;  // XCD-chunked: groups of 16 blocks per XCD
-  if (table) {  // (probe) a process-wide table buffer, grown as needed: measurement only
+  if (table) {  // (probe) a process-wide table buffer, grown as needed: measurement only, one
+                // thread at a time (hipFree waits for the launches still reading the old one)
     static uint64_t *g_table = nullptr;
     static uint64_t g_cap = 0;
     const uint64_t runs = blocks * kWavesPerBlock;
