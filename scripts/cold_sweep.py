@@ -72,6 +72,8 @@ def main():
     ap.add_argument("--vms", default="16,32,64", help="grid multipliers (C3)")
     ap.add_argument("--sms", default="2,4,8,16", help="grid multipliers (slots)")
     ap.add_argument("--c2n", type=int, default=1 << 20, help="images of the c2 case (8388608: C5 on one GPU)")
+    ap.add_argument("--c3n", type=int, default=4 << 20, help="images of the c3 case (C3's mix)")
+    ap.add_argument("--c3forms", default="U8 xcd keep,U8 xcd,U4 xcd keep", help="vvstream forms swept (c3)")
     ap.add_argument("--sorders", default="scatter,xcd-chunked,default order", help="block orders (slots)")
     args = ap.parse_args()
     VARIANTS[:] = [int(x) for x in args.rs.split(",")]
@@ -102,7 +104,7 @@ def main():
         del arenas, out
         torch.cuda.empty_cache()
     if "c3" in args.cases.split(",") or "c3fixed" in args.cases:
-        n = 4 << 20
+        n = args.c3n
         off, ln, total = synth_np.mixed_layout(n, seed=42)
         d_off, d_ln = torch.from_numpy(off).cuda(), torch.from_numpy(ln).cuda()
         arenas = []
@@ -119,6 +121,8 @@ def main():
         params += [] if "c3" not in args.cases.split(",") else [("vvstream policy, whole first step kept (5)", 5 | 8 | 16), ("vvstream policy (AUTO)", 4 | 8 | 16),
                    ("vvstream policy, no kept line", 4 | 8)]
         for base, lab in ((3 | 8 | 16, "U8 xcd keep"), (3 | 8, "U8 xcd"), (2 | 8 | 16, "U4 xcd keep")):
+            if lab not in args.c3forms.split(","):
+                continue
             for m in VMS:
                 params.append((f"vvstream {lab} M{m}", base | (m << 16)))
         sweep("c3", arenas, run, params, img + 2 * n, s)
