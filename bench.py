@@ -143,7 +143,53 @@ def parse():
                    help="start the ranks and print their layout only (no GPU; tests/test_bench_contract.py)")
     p.add_argument("--per-launch-events", action="store_true",
                    help="one HIP event pair per launch (adds ~10 us idle per step)")
+    p.add_argument("--fail-rank", type=int, default=-1,
+                   help="--launch-check only: this rank exits with status 3 after joining the process group "
+                        "(tests/test_bench_contract.py: the job must fail, not hang)")
     return p.parse_args()
+
+
+# A rank that stalls in the rendezvous, a barrier or a collective must not hold
+# an 8-GPU lease silently for torch's default 10 minutes:
+# every process group gets this timeout (TCPCK_BENCH_PG_TIMEOUT overrides it).
+PG_TIMEOUT_S = 300.0
+
+
+def init_group(backend: str, device=None) -> None:
+    import datetime
+    import torch.distributed as dist
+    timeout = datetime.timedelta(seconds=float(os.environ.get("TCPCK_BENCH_PG_TIMEOUT", PG_TIMEOUT_S)))
+    if device is not None:
+        dist.init_process_group(backend, timeout=timeout, device_id=device)
+    else:
+        dist.init_process_group(backend, timeout=timeout)
+
+
+def device_identity(dev_index: int) -> tuple[str, int]:
+    """(PCI address "dddd:bb:dd", the same as an integer) of the HIP device
+    this rank runs on: ranks on distinct GPUs have distinct addresses."""
+    import torch
+    p = torch.cuda.get_device_properties(dev_index)
+    dom, bus, dv = int(p.pci_domain_id), int(p.pci_bus_id), int(p.pci_device_id)
+    return f"{dom:04x}:{bus:02x}:{dv:02x}", (dom << 16) | (bus << 8) | dv
+
+
+def check_devices(world: int, dev_index: int, coll_dev, rehearsal: bool) -> dict:
+    """Every rank's PCI address, gathered.  With fewer distinct devices than
+    ranks the line would read as an N-GPU result it is not: an error (exit 3 on
+    every rank, all of them see the same list), or -- under the one-GPU
+    rehearsal knob TCPCK_BENCH_DEVICE -- a line marked as a rehearsal."""
+    from tcpck.shard import gather_ranks
+    name, code = device_identity(dev_index)
+    codes = [int(x) for x in gather_ranks(float(code), device=coll_dev)]
+    names = [f"{c >> 16:04x}:{(c >> 8) & 0xFF:02x}:{c & 0xFF:02x}" for c in codes]
+    distinct = len(set(codes))
+    if distinct < world:
+        if not rehearsal:
+            log(f"error: {world} ranks on {distinct} distinct device(s) {names}: not an {world}-GPU run")
+            sys.exit(3)
+        log(f"warning: rehearsal (TCPCK_BENCH_DEVICE set): {world} ranks on {distinct} device(s) {names}")
+    return {"devices": distinct, "device_ids": names, "rehearsal": distinct < world}
 
 
 def run_c1(n: int) -> dict:
@@ -463,7 +509,10 @@ def launch_check(args) -> None:
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        dist.init_process_group(os.environ.get("TCPCK_BENCH_BACKEND", "gloo"))
+        init_group(os.environ.get("TCPCK_BENCH_BACKEND", "gloo"))
+        if rank == args.fail_rank:
+            log(f"rank {rank}: --fail-rank, exiting with status 3")
+            sys.exit(3)
         t = torch.zeros(2 * world, dtype=torch.int64)
         t[2 * rank], t[2 * rank + 1] = rank, local
         dist.all_reduce(t)
@@ -501,15 +550,14 @@ def main():
     # rehearsal knobs (not used by the driver): several ranks on one GPU with
     # gloo collectives, to exercise the N>1 path on a one-GPU box
     backend = os.environ.get("TCPCK_BENCH_BACKEND", "nccl")
+    rehearsal = "TCPCK_BENCH_DEVICE" in os.environ
     dev_index = int(os.environ.get("TCPCK_BENCH_DEVICE", local))
     coll_dev = "cuda" if backend == "nccl" else "cpu"
     torch.cuda.set_device(dev_index)
     local = dev_index
     if world > 1:
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(backend)
+        init_group(backend, torch.device("cuda", local) if backend == "nccl" else None)
+    devices = check_devices(world, dev_index, coll_dev, rehearsal)
 
     from tcpck.shard import gather_ranks, max_over_ranks
     ctx = tcpck.Context(local)
@@ -558,7 +606,11 @@ def main():
                    "parallelism": f"shard{world} (independent per-GPU batches, no collective)"},
         "roofline": roofline(w, launch_ms, launch_ms_all, args.config, world),
         "settle": settle,
+        "devices": devices["devices"],
+        "device_ids": devices["device_ids"],
     }
+    if devices["rehearsal"]:
+        rec["rehearsal"] = "TCPCK_BENCH_DEVICE: several ranks share a device; not an N-GPU measurement"
     if one_arena is not None:
         rec["one_arena"] = one_arena
     del w
@@ -620,7 +672,7 @@ def compact_line(rec: dict) -> tuple[dict, dict]:
     pass lists and per-key descriptions move to the detail."""
     line, detail = {}, {}
     for k, v in rec.items():
-        if k == "settle":
+        if k in ("settle", "device_ids"):
             detail[k] = v
         elif k == "roofline":
             line[k], rest = _split(v, ("bound", "achieved", "peak", "unit", "frac", "traffic",

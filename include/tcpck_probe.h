@@ -70,6 +70,21 @@ int tcpck_ctx_set_debug(tcpck_ctx *ctx, void *d_buf);
  * allocated and a bit per slot that a FILL has used (its event recorded). */
 int tcpck_probe_scratch_state(tcpck_ctx *ctx, int *allocated, int *used_mask);
 
+/* Fault injection for the scratch slots: the next n allocation attempts of an
+ * out-less FILL are refused as if hipMalloc had failed.  *refusals (may be
+ * NULL) receives the refusals so far.  After a refusal the context retries
+ * the allocation 64 out-less FILLs later (not latched). */
+int tcpck_probe_scratch_fail(tcpck_ctx *ctx, int n, uint64_t *refusals);
+
+/* The pipelined FILL (round 6; tcp-stack_amd/csrc/tcpck_api.hip
+ * fill_pipelined) under TCPCK_KERNEL_AUTO in this context: k chunks (0 / 1:
+ * the serial form, -1: AUTO's rule), the field pass of chunk i on a context
+ * stream of priority prio (hipStreamCreateWithPriority; a changed priority
+ * recreates the stream after draining it) beside the stream pass of chunk
+ * i + 1.  Applies to FILLs whose form has a field pass, at least 4096 images
+ * per chunk, k <= 32. */
+int tcpck_probe_set_fill_pipe(tcpck_ctx *ctx, int k, int prio);
+
 /* Timing-only streaming micro-kernel over d_buf (results are not checksums):
  * variant = chunks per lane per step x steps in flight x scan, see
  * tcp-stack_amd/csrc/tcpck_diag.hip.  d_out: u32 per wave. */

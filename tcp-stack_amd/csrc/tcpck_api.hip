@@ -156,6 +156,12 @@ void free_stage(tcpck_ctx *ctx) {
     }
     if (slot.buf) (void)hipFree(slot.buf);
   }
+  if (ctx->pipe) {
+    (void)hipStreamSynchronize(ctx->pipe);
+    (void)hipStreamDestroy(ctx->pipe);
+  }
+  for (auto &ev : ctx->pipe_ev)
+    if (ev) (void)hipEventDestroy(ev);
   if (ctx->side) {
     (void)hipEventDestroy(ctx->fork);
     (void)hipEventDestroy(ctx->join);
@@ -562,10 +568,34 @@ bool var_receive_fuses(int mode, const tcpck_layout *layout, uint64_t count, int
          ((hk.fuse_any_hdr && !auto_pick) || fuse_small || (p & kSstreamHdrStream));
 }
 
+// The header pass before VERIFY: under AUTO (whose choices are always valid),
+// or with an explicit kernel in the probe library; with an explicit kernel the
+// product runs it after VERIFY, so that a rejected kernel / param leaves the
+// caller's header array untouched.
+bool receive_hdr_first(int kernel, const Hooks &hk) {
+  return !hk.hdr_after && (kernel == TCPCK_KERNEL_AUTO || hk.hdr_first_explicit);
+}
+
+// FILL's field pass on `s`, or -- pipelined FILL (fill_pipelined) -- on `ps`
+// after the event `pev` recorded on `s` behind the stream pass it reads.
+hipError_t launch_patch_on(const tcpck::PatchArgs &pa, uint32_t num_cus, hipStream_t s, hipStream_t ps,
+                           hipEvent_t pev) {
+  if (ps) {
+    hipError_t e = hipEventRecord(pev, s);
+    if (e == hipSuccess) e = hipStreamWaitEvent(ps, pev, 0);
+    if (e != hipSuccess) return e;
+    s = ps;
+  }
+  return tcpck::launch_patch_fields(pa, num_cus, s);
+}
+
 hipError_t run_fixed_r(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_t stride, uint32_t len,
-                       uint64_t count, void *out, int kernel, int param, hipStream_t s, uint8_t *hdr, const Hooks &hk) {
+                       uint64_t count, void *out, int kernel, int param, hipStream_t s, uint8_t *hdr, const Hooks &hk,
+                       hipStream_t ps = nullptr, hipEvent_t pev = nullptr) {
   bool patch = false;
-  if (op == TCPCK_OP_RECEIVE && hdr && !hk.hdr_after && !fixed_receive_fuses(mode, arena, stride, len, kernel, param, hk)) {
+  const auto ncu = static_cast<uint32_t>(ctx->num_cus);
+  if (op == TCPCK_OP_RECEIVE && hdr && receive_hdr_first(kernel, hk) &&
+      !fixed_receive_fuses(mode, arena, stride, len, kernel, param, hk)) {
     tcpck::HeaderArgs h{};  // the header pass first (fixed_receive_fuses), then VERIFY
     h.arena = arena;
     h.stride = stride;
@@ -590,7 +620,7 @@ hipError_t run_fixed_r(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_
     pa.hi = (count - 1) * stride + len;
     pa.update = 1;
     pa.reverse = hk.patch_reverse ? 1u : 0u;
-    return tcpck::launch_patch_fields(pa, static_cast<uint32_t>(ctx->num_cus), s);
+    return launch_patch_on(pa, ncu, s, ps, pev);
   }
   bool hdr_done = false;
   const hipError_t e =
@@ -605,7 +635,7 @@ hipError_t run_fixed_r(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint64_
     p.lo = 0;
     p.hi = (count - 1) * stride + len;
     p.reverse = hk.patch_reverse ? 1u : 0u;
-    return tcpck::launch_patch_fields(p, static_cast<uint32_t>(ctx->num_cus), s);
+    return launch_patch_on(p, ncu, s, ps, pev);
   }
   if (op != TCPCK_OP_RECEIVE || hdr_done) return e;
   tcpck::HeaderArgs h{};
@@ -758,7 +788,9 @@ hipError_t run_var_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const 
 
 hipError_t run_var_r(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const uint64_t *off, const uint32_t *len,
                      uint64_t base, uint64_t count, void *out, const tcpck_layout *layout, int kernel, int param,
-                     hipStream_t s, uint8_t *hdr, const Hooks &hk) {
+                     hipStream_t s, uint8_t *hdr, const Hooks &hk, hipStream_t ps = nullptr,
+                     hipEvent_t pev = nullptr) {
+  const auto ncu = static_cast<uint32_t>(ctx->num_cus);
   if (op == TCPCK_OP_RECEIVE && base != 0) return hipErrorInvalidValue;  // device batches only
   if (fill_by_update(op, mode, out, kernel, param, false, 0, 0, layout, count)) {
     const int p = param & ~(TCPCK_PARAM_FILL_UPDATE | TCPCK_PARAM_FILL_INSTREAM);
@@ -775,7 +807,7 @@ hipError_t run_var_r(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const uin
     pa.update = 1;
     pa.reverse = hk.patch_reverse ? 1u : 0u;
     pa.packed = (layout && (layout->flags & TCPCK_LAYOUT_PACKED)) ? 1u : 0u;
-    return tcpck::launch_patch_fields(pa, static_cast<uint32_t>(ctx->num_cus), s);
+    return launch_patch_on(pa, ncu, s, ps, pev);
   }
   tcpck::HeaderArgs h{};
   h.arena = arena;
@@ -783,7 +815,8 @@ hipError_t run_var_r(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const uin
   h.count = count;
   h.out = hdr;
   h.store_bits = hk.hdr_store_bits;
-  if (op == TCPCK_OP_RECEIVE && hdr && !hk.hdr_after && !var_receive_fuses(mode, layout, count, kernel, param, hk)) {
+  if (op == TCPCK_OP_RECEIVE && hdr && receive_hdr_first(kernel, hk) &&
+      !var_receive_fuses(mode, layout, count, kernel, param, hk)) {
     // the header pass first, then VERIFY (fixed_receive_fuses)
     const hipError_t eh = tcpck::launch_header_swap(h, static_cast<uint32_t>(ctx->num_cus), s);
     if (eh != hipSuccess) return eh;
@@ -803,10 +836,20 @@ hipError_t run_var_r(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, const uin
     pa.count = count;
     pa.sums = static_cast<uint16_t *>(out);
     pa.reverse = hk.patch_reverse ? 1u : 0u;
-    return tcpck::launch_patch_fields(pa, static_cast<uint32_t>(ctx->num_cus), s);
+    return launch_patch_on(pa, ncu, s, ps, pev);
   }
   if (op != TCPCK_OP_RECEIVE || hdr_done) return e;
-  return tcpck::launch_header_swap(h, static_cast<uint32_t>(ctx->num_cus), s);
+  return tcpck::launch_header_swap(h, ncu, s);
+}
+
+// A sub-range of an offset-list batch keeps the flags and the length bounds,
+// and its byte hint scales with its image count, so its typical image -- the
+// quantity AUTO chooses by -- is the whole batch's and every chunk runs the
+// same form (tcpck_tuning.h).
+tcpck_layout sub_layout(const tcpck_layout &layout, uint64_t n, uint64_t count) {
+  tcpck_layout sub = layout;
+  sub.total_bytes = static_cast<uint64_t>(static_cast<unsigned __int128>(layout.total_bytes) * n / count);
+  return sub;
 }
 
 // Patches bytes 28-29 of host images after a FILL computed on the device
@@ -877,48 +920,57 @@ tcpck_ctx::ScratchSlot *take_scratch(tcpck_ctx *ctx, hipStream_t s, std::unique_
     return nullptr;
   }
   if (cs != hipStreamCaptureStatusNone) return nullptr;
-  std::lock_guard<std::mutex> lk(ctx->scratch_mu);
-  if (ctx->scratch_failed) return nullptr;
-  if (!ctx->scratch[0].buf) {  // first use: every slot, or none
-    for (auto &slot : ctx->scratch) {
-      void *p = nullptr;
-      hipEvent_t ev = nullptr;
-      if (hipMalloc(&p, tcpck::api::kScratchImages * 2) != hipSuccess ||
-          hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
-        if (p) (void)hipFree(p);
-        (void)hipGetLastError();
-        for (auto &sl : ctx->scratch) {
-          if (sl.buf) (void)hipFree(sl.buf);
-          if (sl.ev) (void)hipEventDestroy(sl.ev);
-          sl.buf = nullptr;
-          sl.ev = nullptr;
-        }
-        ctx->scratch_failed = true;
-        return nullptr;
-      }
-      slot.buf = static_cast<uint16_t *>(p);
-      slot.ev = ev;
-    }
-    ctx->scratch_images = tcpck::api::kScratchImages;
-  }
-  // an idle slot (never used, or its last user's work done), else the next in turn
   constexpr int n = tcpck_ctx::kScratchSlots;
   int pick = -1;
-  for (int i = 0; i < n && pick < 0; ++i) {
-    auto &slot = ctx->scratch[(ctx->scratch_next + i) % n];
-    std::unique_lock<std::mutex> try_lk(slot.mu, std::try_to_lock);
-    if (!try_lk.owns_lock()) continue;
-    if (!slot.used || hipEventQuery(slot.ev) == hipSuccess) {
-      pick = static_cast<int>((ctx->scratch_next + i) % n);
-      held = std::move(try_lk);
+  {
+    std::lock_guard<std::mutex> lk(ctx->scratch_mu);
+    ++ctx->scratch_calls;
+    if (!ctx->scratch[0].buf) {  // first use (or a retry after a refusal): every slot, or none
+      if (ctx->scratch_calls < ctx->scratch_retry_at) return nullptr;
+      for (auto &slot : ctx->scratch) {
+        void *p = nullptr;
+        hipEvent_t ev = nullptr;
+        const bool forced = ctx->probe_scratch_fail > 0;  // probe library (tests): a refused allocation
+        if (forced) --ctx->probe_scratch_fail;
+        if (forced || hipMalloc(&p, tcpck::api::kScratchImages * 2) != hipSuccess ||
+            hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+          if (p) (void)hipFree(p);
+          (void)hipGetLastError();
+          for (auto &sl : ctx->scratch) {
+            if (sl.buf) (void)hipFree(sl.buf);
+            if (sl.ev) (void)hipEventDestroy(sl.ev);
+            sl.buf = nullptr;
+            sl.ev = nullptr;
+          }
+          // not latched: the refusal may be transient (memory pressure, another
+          // thread capturing a graph in global mode); this call and the next
+          // kScratchRetry - 1 run the in-stream form, then allocation is retried
+          ++ctx->scratch_refusals;
+          ctx->scratch_retry_at = ctx->scratch_calls + tcpck::api::kScratchRetry;
+          return nullptr;
+        }
+        slot.buf = static_cast<uint16_t *>(p);
+        slot.ev = ev;
+      }
+      ctx->scratch_images = tcpck::api::kScratchImages;
     }
+    // an idle slot (never used, or its last user's work done), else the next in turn
+    for (int i = 0; i < n && pick < 0; ++i) {
+      auto &slot = ctx->scratch[(ctx->scratch_next + i) % n];
+      std::unique_lock<std::mutex> try_lk(slot.mu, std::try_to_lock);
+      if (!try_lk.owns_lock()) continue;
+      if (!slot.used || hipEventQuery(slot.ev) == hipSuccess) {
+        pick = static_cast<int>((ctx->scratch_next + i) % n);
+        held = std::move(try_lk);
+      }
+    }
+    (void)hipGetLastError();  // hipEventQuery's hipErrorNotReady
+    if (pick < 0) pick = static_cast<int>(ctx->scratch_next % n);
+    ctx->scratch_next = static_cast<unsigned>(pick + 1);
   }
-  (void)hipGetLastError();  // hipEventQuery's hipErrorNotReady
-  if (pick < 0) {
-    pick = static_cast<int>(ctx->scratch_next % n);
-    held = std::unique_lock<std::mutex>(ctx->scratch[pick].mu);
-  }
-  ctx->scratch_next = static_cast<unsigned>(pick + 1);
+  // every slot busy: wait for the chosen one's holder with scratch_mu released,
+  // so other callers can still take a slot that frees meanwhile
+  if (!held.owns_lock()) held = std::unique_lock<std::mutex>(ctx->scratch[pick].mu);
   return &ctx->scratch[pick];
 }
 
@@ -936,6 +988,96 @@ hipError_t with_scratch(tcpck_ctx *ctx, tcpck_ctx::ScratchSlot *slot, uint64_t c
   const hipError_t er = hipEventRecord(slot->ev, s);
   if (er == hipSuccess) slot->used = true;
   return e != hipSuccess ? e : er;
+}
+
+// ---- pipelined FILL (round 6) --------------------------
+// A FILL whose form has a field pass (the deferred-field forms and the update
+// form: fill_reads_results_*) runs the stream over all images and then the
+// field pass over all images, one after the other.  Pipelined, the batch is cut
+// into K chunks: chunk i's stream pass goes on the caller's stream, its field
+// pass on the context's `pipe` stream after an event behind that stream pass,
+// so the field pass of chunk i runs beside the stream pass of chunk i + 1, and
+// the caller's stream waits for the last field pass (pipe_ev[K]) before
+// anything it enqueues next.  Chunks are disjoint image ranges: a field pass
+// writes only bytes 28-29 of its own chunk's images, which no other chunk's
+// stream sums, and it reads only its own chunk's results.
+
+constexpr int kFillPipeAuto = 0;          // AUTO's chunk count (0: not pipelined), DESIGN.md section 8
+constexpr uint64_t kFillPipeMinImages = 4096;  // per chunk
+
+hipError_t ensure_pipe(tcpck_ctx *ctx) {
+  if (ctx->pipe) return hipSuccess;
+  hipStream_t st = nullptr;
+  hipError_t e = hipStreamCreateWithPriority(&st, hipStreamNonBlocking, ctx->pipe_prio);
+  for (int i = 0; i <= tcpck_ctx::kPipeMax && e == hipSuccess; ++i)
+    if (!ctx->pipe_ev[i]) e = hipEventCreateWithFlags(&ctx->pipe_ev[i], hipEventDisableTiming);
+  if (e != hipSuccess) {  // the events made so far stay for the next attempt; freed by free_pipe
+    if (st) (void)hipStreamDestroy(st);
+    (void)hipGetLastError();
+    return e;
+  }
+  ctx->pipe = st;
+  return hipSuccess;
+}
+
+// K for this FILL (<= 1: not pipelined).  Only forms with a field pass, only
+// with the caller's stream not capturing (the pipe stream would join the
+// capture), and at least kFillPipeMinImages per chunk.
+int fill_pipe_k(int op, int kernel, bool has_field_pass, uint64_t count, hipStream_t s, const Hooks &hk) {
+  if (op != TCPCK_OP_FILL || kernel != TCPCK_KERNEL_AUTO || !has_field_pass) return 0;
+  int k = hk.fill_pipe >= 0 ? hk.fill_pipe : kFillPipeAuto;
+  k = static_cast<int>(std::min<uint64_t>(std::min(k, tcpck_ctx::kPipeMax), count / kFillPipeMinImages));
+  if (k <= 1) return 0;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cs) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return cs == hipStreamCaptureStatusNone ? k : 0;
+}
+
+// launch(k0, n, ps, pev) enqueues images [k0, k0 + n): the stream pass on s,
+// the field pass on ps after pev (ps == nullptr: everything on s).
+template <typename Launch>
+hipError_t fill_pipelined(tcpck_ctx *ctx, int k, uint64_t count, hipStream_t s, Launch launch) {
+  std::lock_guard<std::mutex> lk(ctx->pipe_mu);
+  if (ensure_pipe(ctx) != hipSuccess) return launch(0, count, nullptr, nullptr);  // the serial form
+  hipError_t e = hipSuccess;
+  const uint64_t per = (count + static_cast<uint64_t>(k) - 1) / static_cast<uint64_t>(k);
+  int i = 0;
+  for (uint64_t k0 = 0; k0 < count && e == hipSuccess; k0 += per, ++i)
+    e = launch(k0, std::min(per, count - k0), ctx->pipe, ctx->pipe_ev[i]);
+  // join, also after an error: nothing the caller enqueues next may overtake a field pass already queued
+  hipError_t ej = hipEventRecord(ctx->pipe_ev[tcpck_ctx::kPipeMax], ctx->pipe);
+  if (ej == hipSuccess) ej = hipStreamWaitEvent(s, ctx->pipe_ev[tcpck_ctx::kPipeMax], 0);
+  return e != hipSuccess ? e : ej;
+}
+
+// run_fixed / run_var for a FILL, pipelined when fill_pipe_k says so.
+hipError_t fill_fixed(tcpck_ctx *ctx, int mode, uint8_t *arena, uint64_t stride, uint32_t len, uint64_t count,
+                      uint16_t *out, int kernel, int param, hipStream_t s, const Hooks &hk) {
+  const bool field_pass = out && kernel == TCPCK_KERNEL_AUTO && fill_reads_results_fixed(mode, arena, stride, len, param);
+  const int k = fill_pipe_k(TCPCK_OP_FILL, kernel, field_pass, count, s, hk);
+  if (k <= 1)
+    return run_fixed(ctx, TCPCK_OP_FILL, mode, arena, stride, len, count, out, kernel, param, s, nullptr, hk);
+  return fill_pipelined(ctx, k, count, s, [&](uint64_t k0, uint64_t n, hipStream_t ps, hipEvent_t pev) {
+    return run_fixed_r(ctx, TCPCK_OP_FILL, mode, arena + k0 * stride, n == 1 ? len : stride, len, n, out + k0, kernel,
+                       param, s, nullptr, hk, ps, pev);
+  });
+}
+
+hipError_t fill_var(tcpck_ctx *ctx, int mode, uint8_t *arena, const uint64_t *off, const uint32_t *len,
+                    uint64_t count, uint16_t *out, const tcpck_layout *layout, int kernel, int param, hipStream_t s,
+                    const Hooks &hk) {
+  const bool field_pass = out && kernel == TCPCK_KERNEL_AUTO && fill_reads_results_var(mode, layout, count, param);
+  const int k = fill_pipe_k(TCPCK_OP_FILL, kernel, field_pass, count, s, hk);
+  if (k <= 1) return run_var(ctx, TCPCK_OP_FILL, mode, arena, off, len, 0, count, out, layout, kernel, param, s, nullptr, hk);
+  return fill_pipelined(ctx, k, count, s, [&](uint64_t k0, uint64_t n, hipStream_t ps, hipEvent_t pev) {
+    tcpck_layout sub{};
+    if (layout) sub = sub_layout(*layout, n, count);
+    return run_var_r(ctx, TCPCK_OP_FILL, mode, arena, off + k0, len + k0, 0, n, out + k0, layout ? &sub : nullptr,
+                     kernel, param, s, nullptr, hk, ps, pev);
+  });
 }
 
 }  // namespace
@@ -961,10 +1103,12 @@ int batch_fixed_ex(tcpck_ctx *ctx, int op, int mode, void *d_arena, uint64_t str
     std::unique_lock<std::mutex> held;
     if (auto *slot = take_scratch(ctx, s, held))
       return hip_status(with_scratch(ctx, slot, count, s, [&](uint64_t k0, uint64_t n, uint16_t *res) {
-        return run_fixed(ctx, op, mode, arena + k0 * stride, n == 1 ? len : stride, len, n, res, kernel, param, s,
-                         nullptr, hk);
+        return fill_fixed(ctx, mode, arena + k0 * stride, n == 1 ? len : stride, len, n, res, kernel, param, s, hk);
       }));
   }
+  if (op == TCPCK_OP_FILL)
+    return hip_status(fill_fixed(ctx, mode, arena, stride, len, count, static_cast<uint16_t *>(d_out), kernel, param,
+                                 s, hk));
   return hip_status(run_fixed(ctx, op, mode, arena, stride, len, count, d_out, kernel, param, s, nullptr, hk));
 }
 
@@ -984,18 +1128,14 @@ int batch_var_ex(tcpck_ctx *ctx, int op, int mode, void *d_arena, const uint64_t
     if (auto *slot = take_scratch(ctx, s, held))
       return hip_status(with_scratch(ctx, slot, count, s, [&](uint64_t k0, uint64_t n, uint16_t *res) {
         tcpck_layout sub{};
-        if (layout) {
-          // a sub-range keeps the flags and the length bounds, and its byte hint
-          // scales with its image count, so its typical image -- the quantity
-          // AUTO chooses by -- is the whole batch's and every chunk runs the
-          // same form (tcpck_tuning.h)
-          sub = *layout;
-          sub.total_bytes = static_cast<uint64_t>(static_cast<unsigned __int128>(layout->total_bytes) * n / count);
-        }
-        return run_var(ctx, op, mode, arena, d_offsets + k0, d_lengths + k0, 0, n, res, layout ? &sub : nullptr,
-                       kernel, param, s, nullptr, hk);
+        if (layout) sub = sub_layout(*layout, n, count);
+        return fill_var(ctx, mode, arena, d_offsets + k0, d_lengths + k0, n, res, layout ? &sub : nullptr, kernel,
+                        param, s, hk);
       }));
   }
+  if (op == TCPCK_OP_FILL)
+    return hip_status(fill_var(ctx, mode, arena, d_offsets, d_lengths, count, static_cast<uint16_t *>(d_out), layout,
+                               kernel, param, s, hk));
   return hip_status(run_var(ctx, op, mode, arena, d_offsets, d_lengths, 0, count, d_out, layout, kernel, param, s,
                             nullptr, hk));
 }

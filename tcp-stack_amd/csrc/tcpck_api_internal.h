@@ -51,7 +51,24 @@ struct tcpck_ctx {
   ScratchSlot scratch[kScratchSlots];
   uint64_t scratch_images = 0;
   unsigned scratch_next = 0;
-  bool scratch_failed = false;  // allocation refused once: in-stream forms from then on
+  // A refused allocation is not latched: the call runs the in-stream form and
+  // the slots are tried again after kScratchRetry more out-less FILLs.
+  uint64_t scratch_retry_at = 0;   // out-less FILL count from which allocation is tried again
+  uint64_t scratch_calls = 0;      // out-less FILLs that asked for a slot
+  uint64_t scratch_refusals = 0;   // allocations refused so far (tcpck_probe_scratch_state)
+  int probe_scratch_fail = 0;      // probe library: refuse this many more allocation attempts (tests)
+
+  // Pipelined FILL (round 6): the batch in K chunks, chunk i's stream pass on
+  // the caller's stream and its field pass on `pipe` after the event
+  // pipe_ev[i], so the field pass of chunk i runs beside the stream of chunk
+  // i + 1; pipe_ev[K] joins `pipe` back into the caller's stream.  Created on
+  // first use; one pipelined call is enqueued at a time (pipe_mu).
+  static constexpr int kPipeMax = 32;
+  std::mutex pipe_mu;
+  hipStream_t pipe = nullptr;
+  hipEvent_t pipe_ev[kPipeMax + 1] = {};
+  int pipe_prio = 0;               // the pipe stream's priority (probe: tcpck_probe_set_fill_pipe)
+  int probe_fill_pipe = -1;        // probe library: K (0/1 off, -1 AUTO's rule)
 
   // probe library only (tcpck_ex_probe.hip): per-wave time stamp buffer, and the
   // side stream + events of the concurrent RECEIVE form
@@ -65,15 +82,19 @@ namespace tcpck {
 namespace api {
 
 constexpr uint64_t kScratchImages = 8ull << 20;  // 16 MiB of u16 results: C5's 8M images in one chunk
+constexpr uint64_t kScratchRetry = 64;           // out-less FILLs between allocation attempts after a refusal
 
 // Measurement hooks (libtcpck_probe.so only; the product passes Hooks{}).
 struct Hooks {
   bool fuse_any_hdr = false;     // RECEIVE, explicit kernel: fuse the headers into any kernel that can
                                  // (sstream's after-the-verdicts conversion, HDR 1)
   bool hdr_after = false;        // RECEIVE into a header array: the separate header pass after VERIFY (the
-                                 // product runs it first, tcpck_api.hip receive_hdr_first)
+                                 // product runs it first under AUTO, tcpck_api.hip fixed_receive_fuses)
+  bool hdr_first_explicit = false;  // ... first with an explicit VERIFY kernel too (the product runs it after
+                                    // an explicit kernel, so a rejected choice leaves the header array as it was)
   uint32_t hdr_store_bits = 0;   // HeaderArgs::store_bits of the header pass
   bool patch_reverse = false;    // FILL's field pass in reverse image order (PatchArgs::reverse)
+  int fill_pipe = -1;            // pipelined FILL chunks: -1 AUTO's rule, 0 / 1 off, K > 1 K chunks
 };
 
 // probe library: tcpck_batch_*_ex param bit selecting Hooks::patch_reverse

@@ -10,7 +10,8 @@
 //   * tcpck_batch_receive_ex: with an explicit kernel, the headers fused into
 //     any kernel that can (sstream's after-the-verdicts conversion, HDR 1);
 //   * tcpck_probe_receive_ex: the header pass forms (TCPCK_PROBE_RECEIVE_*);
-//   * tcpck_ctx_set_debug, tcpck_diag_stream, tcpck_probe_scratch_state.
+//   * tcpck_ctx_set_debug, tcpck_diag_stream, tcpck_probe_scratch_state,
+//     tcpck_probe_scratch_fail, tcpck_probe_set_fill_pipe.
 #include <hip/hip_runtime.h>
 
 #include <mutex>
@@ -30,6 +31,7 @@ namespace {
 Hooks probe_hooks(int flags) {
   Hooks h;
   h.fuse_any_hdr = true;
+  h.hdr_first_explicit = true;
   h.hdr_after = (flags & TCPCK_PROBE_RECEIVE_HDR_AFTER) != 0;
   h.hdr_store_bits = ((flags & TCPCK_PROBE_RECEIVE_HDR_WT) ? 1u : 0u) |
                      ((flags & TCPCK_PROBE_RECEIVE_HDR_WIDE)
@@ -104,6 +106,7 @@ int tcpck_batch_fixed_ex(tcpck_ctx *ctx, int op, int mode, void *d_arena, uint64
   }
   Hooks hk = probe_hooks(0);
   hk.patch_reverse = (param & tcpck::api::kProbeParamPatchReverse) != 0;
+  if (ctx) hk.fill_pipe = ctx->probe_fill_pipe;
   return tcpck::api::batch_fixed_ex(ctx, op, mode, d_arena, stride, len, count, d_out, kernel,
                                     param & ~tcpck::api::kProbeParamPatchReverse, static_cast<hipStream_t>(stream), hk);
 }
@@ -113,6 +116,7 @@ int tcpck_batch_var_ex(tcpck_ctx *ctx, int op, int mode, void *d_arena, const ui
                        int kernel, int param, tcpck_stream stream) {
   Hooks hk = probe_hooks(0);
   hk.patch_reverse = (param & tcpck::api::kProbeParamPatchReverse) != 0;
+  if (ctx) hk.fill_pipe = ctx->probe_fill_pipe;
   return tcpck::api::batch_var_ex(ctx, op, mode, d_arena, d_offsets, d_lengths, count, d_out, layout, kernel,
                                   param & ~tcpck::api::kProbeParamPatchReverse, static_cast<hipStream_t>(stream), hk);
 }
@@ -175,6 +179,28 @@ int tcpck_diag_stream(tcpck_ctx *ctx, int variant, const void *d_buf, uint64_t b
 int tcpck_ctx_set_debug(tcpck_ctx *ctx, void *d_buf) {
   if (!ctx) return TCPCK_EINVAL;
   ctx->dbg = d_buf;
+  return TCPCK_OK;
+}
+
+int tcpck_probe_scratch_fail(tcpck_ctx *ctx, int n, uint64_t *refusals) {
+  if (!ctx || n < 0) return TCPCK_EINVAL;
+  std::lock_guard<std::mutex> lk(ctx->scratch_mu);
+  ctx->probe_scratch_fail = n;
+  if (refusals) *refusals = ctx->scratch_refusals;
+  return TCPCK_OK;
+}
+
+int tcpck_probe_set_fill_pipe(tcpck_ctx *ctx, int k, int prio) {
+  if (!ctx || k < -1 || k > tcpck_ctx::kPipeMax) return TCPCK_EINVAL;
+  std::lock_guard<std::mutex> lk(ctx->pipe_mu);
+  if (ctx->pipe && prio != ctx->pipe_prio) {
+    DeviceGuard g(ctx->device);
+    (void)hipStreamSynchronize(ctx->pipe);
+    (void)hipStreamDestroy(ctx->pipe);
+    ctx->pipe = nullptr;
+  }
+  ctx->pipe_prio = prio;
+  ctx->probe_fill_pipe = k;
   return TCPCK_OK;
 }
 

@@ -58,7 +58,8 @@ SEG_SHAPES = {1: "G8/U2", 2: "G16/U6", 3: "G64/U4", 4: "G64/U2", 5: "G32/U3", 6:
 # include/tcpck_tuning.h: in libtcpck.so (AUTO's kernels only) and libtcpck_probe.so
 TUNING_EXPORTS = ("tcpck_batch_fixed_ex", "tcpck_batch_var_ex", "tcpck_batch_segment_ex", "tcpck_batch_receive_ex")
 # include/tcpck_tuning.h, measurement only: libtcpck_probe.so
-PROBE_EXPORTS = ("tcpck_ctx_set_debug", "tcpck_diag_stream", "tcpck_probe_receive_ex", "tcpck_probe_scratch_state")
+PROBE_EXPORTS = ("tcpck_ctx_set_debug", "tcpck_diag_stream", "tcpck_probe_receive_ex", "tcpck_probe_scratch_state",
+                 "tcpck_probe_scratch_fail", "tcpck_probe_set_fill_pipe")
 # include/tcpck_probe.h: tcpck_probe_receive_ex's flags word (the header pass forms)
 PROBE_RECEIVE_HDR_FIRST = 1    # accepted, no effect (the product's separate header pass runs first since round 5)
 PROBE_PARAM_PATCH_REVERSE = 1 << 27  # tcpck_batch_*_ex param (probe library): FILL's field pass in reverse order
@@ -180,6 +181,8 @@ def lib(probe: bool = False) -> ctypes.CDLL:
         "tcpck_batch_var_ex": (i32, [vp, i32, i32, vp, vp, vp, u64, vp, ctypes.POINTER(Layout), i32, i32, vp]),
         "tcpck_ctx_set_debug": (i32, [vp, vp]),
         "tcpck_probe_scratch_state": (i32, [vp, ctypes.POINTER(i32), ctypes.POINTER(i32)]),
+        "tcpck_probe_scratch_fail": (i32, [vp, i32, ctypes.POINTER(u64)]),
+        "tcpck_probe_set_fill_pipe": (i32, [vp, i32, i32]),
         "tcpck_diag_stream": (i32, [vp, i32, vp, u64, vp, vp]),
         "tcpck_probe_receive_ex": (i32, [vp, i32, vp, u64, u32, vp, vp, u64, vp, vp, ctypes.POINTER(Layout), i32, i32,
                                          i32, vp]),
@@ -411,6 +414,18 @@ class Context:
         _check(self._L.tcpck_probe_scratch_state(self._h, ctypes.byref(a), ctypes.byref(m)),
                "tcpck_probe_scratch_state")
         return a.value, m.value
+
+    def scratch_fail(self, n: int) -> int:
+        """Refuse the next n scratch allocations (fault injection, libtcpck_probe.so only);
+        returns the refusals so far."""
+        r = ctypes.c_uint64()
+        _check(self._L.tcpck_probe_scratch_fail(self._h, n, ctypes.byref(r)), "tcpck_probe_scratch_fail")
+        return r.value
+
+    def set_fill_pipe(self, k: int, prio: int = 0) -> None:
+        """The pipelined FILL under AUTO in this context: k chunks (0/1 serial, -1 AUTO's rule), the
+        field passes on a context stream of priority prio (libtcpck_probe.so only, tcpck_probe.h)."""
+        _check(self._L.tcpck_probe_set_fill_pipe(self._h, k, prio), "tcpck_probe_set_fill_pipe")
 
     def set_chunk_bytes(self, n: int) -> None:
         _check(self._L.tcpck_ctx_set_chunk_bytes(self._h, n), "tcpck_ctx_set_chunk_bytes")

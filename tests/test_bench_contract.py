@@ -89,6 +89,59 @@ def test_launcher_world_mismatch_fails():
     assert r.returncode == 2 and "WORLD_SIZE 3" in r.stderr
 
 
+def test_failing_rank_fails_the_job():
+    """a rank that dies must fail the job, not leave the
+    others waiting in a collective for torch's default 10 minutes.  Bare
+    `--gpus 2 --launch-check --fail-rank 1` over gloo: rank 1 exits 3 after
+    joining the group, rank 0 waits in its all-reduce; the job must return
+    non-zero well inside the process-group timeout (shortened to 60 s here)."""
+    import subprocess
+    import time
+    env = _env_without_launcher()
+    env["TCPCK_BENCH_PG_TIMEOUT"] = "60"
+    t0 = time.monotonic()
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--launch-check",
+                        "--fail-rank", "1"], capture_output=True, text=True, timeout=200, env=env, cwd="/tmp")
+    assert r.returncode != 0, r.stdout
+    assert time.monotonic() - t0 < 150
+    assert "--fail-rank, exiting with status 3" in r.stderr
+
+
+def test_device_check(monkeypatch):
+    """The line proves its ranks sat on distinct devices:
+    check_devices gathers every rank's PCI address; fewer distinct devices than
+    ranks exits 3, unless the one-GPU rehearsal knob is set (then the line is
+    marked a rehearsal)."""
+    import pytest
+    from tcpck import shard
+    for codes, rehearsal, want in (([0x10300, 0x10400], False, 2), ([0x10300, 0x10300], True, 1),
+                                   ([0x10300, 0x10300], False, None)):
+        monkeypatch.setattr(bench, "device_identity", lambda i, c=codes: ("x", c[0]))
+        monkeypatch.setattr(shard, "gather_ranks", lambda v, device=None, c=codes: [float(x) for x in c])
+        if want is None:
+            with pytest.raises(SystemExit) as e:
+                bench.check_devices(2, 0, "cpu", rehearsal)
+            assert e.value.code == 3
+        else:
+            d = bench.check_devices(2, 0, "cpu", rehearsal)
+            assert d["devices"] == want and d["rehearsal"] == (want < 2)
+            assert d["device_ids"][0] == "0001:03:00"
+
+
+def test_init_group_timeout(monkeypatch):
+    """Every process group gets PG_TIMEOUT_S (or TCPCK_BENCH_PG_TIMEOUT), not torch's default."""
+    import datetime
+    import torch.distributed as dist
+    seen = {}
+    monkeypatch.setattr(dist, "init_process_group", lambda backend, **kw: seen.update(kw, backend=backend))
+    monkeypatch.delenv("TCPCK_BENCH_PG_TIMEOUT", raising=False)
+    bench.init_group("gloo")
+    assert seen["timeout"] == datetime.timedelta(seconds=bench.PG_TIMEOUT_S) and "device_id" not in seen
+    monkeypatch.setenv("TCPCK_BENCH_PG_TIMEOUT", "42")
+    bench.init_group("nccl", "cuda:0")
+    assert seen["timeout"] == datetime.timedelta(seconds=42) and seen["device_id"] == "cuda:0"
+
+
 def _full_record(world=1):
     """A bench record as main() assembles it before compact_line, every prose
     field at its real length and every number at full width."""
@@ -108,6 +161,7 @@ def _full_record(world=1):
            "config": {"workload": bench.CONFIGS["c2"][0], "images_per_gpu": 1 << 20, "image_bytes": 1492,
                       "bytes_per_gpu": 1564475392, "parallelism": "shard1 (independent per-GPU batches, no collective)"},
            "roofline": dict(roof), "settle": {"ms": 250.3, "launches": 1184},
+           "devices": world, "device_ids": [f"0000:{0x11 + i:02x}:00" for i in range(world)],
            "one_arena": {"value": 6999.99, "frac": 0.9399}}
     for name, key in bench.EXTRAS:
         desc = bench.CONFIGS[name][0] if name in bench.CONFIGS else bench.EXTRA[name][0]
@@ -156,3 +210,4 @@ def test_line_fits_the_driver_tail():
         assert line["c1"]["verified"] == line["c1"]["segments"]
         assert line["receive"]["same_ring"]["frac"] > 0
         assert line["one_arena"]["frac"] > 0
+        assert line["devices"] == world and len(detail["device_ids"]) == world

@@ -1,0 +1,231 @@
+"""GPU parity: the pipelined FILL and the round-6 router fixes.
+
+Pipelined FILL (tcp-stack_amd/csrc/tcpck_api.hip fill_pipelined, VERDICT r05
+item 1; reached through the probe library's tcpck_batch_*_ex under
+TCPCK_KERNEL_AUTO after tcpck_probe_set_fill_pipe): the batch in K chunks, the field pass of chunk i on a context stream
+beside the stream pass of chunk i + 1.  Whatever K, the bytes must be the
+reference's insert (socket-manager.cc:9-10: field zeroed, CalculateChecksum of
+include/tcp-header.h:252-263, stored raw) and the results its checksums --
+checked here against the oracle (oracle/ref16.c, pinned by tests/golden) on
+C2's fixed layout (rstream's deferred fields) and C3's packed mix (the update
+form), with and without a results buffer, for K that do and do not divide the
+batch, from several threads at once and under graph capture (which must fall
+back to the serial form).
+
+Also: a refused scratch allocation is retried, not latched; a
+RECEIVE with a rejected explicit kernel leaves the header array untouched.
+"""
+import threading
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+from test_gpu_full_paths import expected_fill  # noqa: E402
+
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def host(t):
+    torch.cuda.synchronize()
+    return t.cpu().numpy()
+
+
+def fields(arena: np.ndarray, offs) -> np.ndarray:
+    o = np.asarray(offs, np.int64) + 28
+    return arena[o].astype(np.uint16) | (arena[o + 1].astype(np.uint16) << 8)
+
+
+@pytest.fixture(scope="module")
+def pctx(built_lib):
+    import tcpck
+    assert torch.cuda.is_available(), "gpu tests need a GPU"
+    c = tcpck.Context(0, probe=True)
+    yield c
+    c.set_fill_pipe(-1, 0)
+    c.close()
+
+
+def _c2(count, seed, oracle_c, L=1492):
+    import tcpck
+    a = torch.empty(count * L, dtype=torch.uint8, device="cuda")
+    tcpck.synth_fixed(a, L, L, count, seed=seed)
+    offs = np.arange(count, dtype=np.int64) * L
+    want = expected_fill(host(a), offs, np.full(count, L), oracle_c)
+    return a, want, offs
+
+
+def _c3(count, seed, oracle_c):
+    import tcpck
+    import synth_np
+    off, ln, total = synth_np.mixed_layout(count, seed=seed)
+    a = torch.empty(total, dtype=torch.uint8, device="cuda")
+    d_off, d_ln = dev(off), dev(ln)
+    tcpck.synth_var(a, d_off, d_ln, 1492, count, seed=seed)
+    want = expected_fill(host(a), off, ln, oracle_c)
+    hints = dict(total_bytes=int(ln.astype(np.int64).sum()), min_len=int(ln.min()), max_len=int(ln.max()),
+                 packed=True)
+    return a, want, off, d_off, d_ln, hints
+
+
+@pytest.mark.parametrize("k", [2, 3, 8, 32])
+@pytest.mark.parametrize("with_out", [True, False], ids=["out", "noout"])
+@pytest.mark.parametrize("prio", [0, -1])
+def test_pipe_c2_fixed(pctx, oracle_c, k, with_out, prio):
+    """C2's layout (rstream's deferred fields), 200,003 images (no K divides it)."""
+    import tcpck
+    count = 200_003
+    pctx.set_fill_pipe(k, prio)
+    a, want, offs = _c2(count, 900 + k, oracle_c)
+    out = torch.full((count,), -1, dtype=torch.int16, device="cuda") if with_out else None
+    pctx.batch_fixed_ex(tcpck.OP_FILL, a, 1492, 1492, count, out, tcpck.KERNEL_AUTO)
+    got = host(a)
+    np.testing.assert_array_equal(got, want)
+    if with_out:
+        np.testing.assert_array_equal(host(out).view(np.uint16), fields(want, offs))
+
+
+@pytest.mark.parametrize("k", [2, 5, 16])
+@pytest.mark.parametrize("with_out", [True, False], ids=["out", "noout"])
+def test_pipe_c3_var(pctx, oracle_c, k, with_out):
+    """C3's packed 96/608/1492 mix (the update form: CHECKSUM stream + field update)."""
+    import tcpck
+    count = (1 << 19) + 77
+    pctx.set_fill_pipe(k, 0)
+    a, want, off, d_off, d_ln, hints = _c3(count, 910 + k, oracle_c)
+    out = torch.full((count,), -1, dtype=torch.int16, device="cuda") if with_out else None
+    pctx.batch_var_ex(tcpck.OP_FILL, a, d_off, d_ln, count, out, tcpck.KERNEL_AUTO, **hints)
+    np.testing.assert_array_equal(host(a), want)
+    if with_out:
+        np.testing.assert_array_equal(host(out).view(np.uint16), fields(want, off))
+
+
+def test_pipe_c3_full_size_twice(pctx, oracle_c):
+    """bench.py's fill_c3 call at full size (4M images), K = 8, twice in a
+    row (FILL is idempotent): the whole arena and every result."""
+    import tcpck
+    count = 4 << 20
+    pctx.set_fill_pipe(8, 0)
+    a, want, off, d_off, d_ln, hints = _c3(count, 42, oracle_c)
+    out = torch.empty(count, dtype=torch.int16, device="cuda")
+    for _ in range(2):
+        pctx.batch_var_ex(tcpck.OP_FILL, a, d_off, d_ln, count, out, tcpck.KERNEL_AUTO, **hints)
+    np.testing.assert_array_equal(host(a), want)
+    np.testing.assert_array_equal(host(out).view(np.uint16), fields(want, off))
+
+
+def test_pipe_small_batch_serial(pctx, oracle_c):
+    """Fewer than 4096 images per chunk: the serial form (same bytes)."""
+    import tcpck
+    count = 6000
+    pctx.set_fill_pipe(16, 0)
+    a, want, offs = _c2(count, 920, oracle_c)
+    pctx.batch_fixed_ex(tcpck.OP_FILL, a, 1492, 1492, count, None, tcpck.KERNEL_AUTO)
+    np.testing.assert_array_equal(host(a), want)
+
+
+def test_pipe_threads_share_the_pipe_stream(pctx, oracle_c):
+    """3 host threads on 3 streams, pipelined out-less FILLs at once (one pipe
+    stream per context, enqueued one call at a time): every arena exact."""
+    import tcpck
+    pctx.set_fill_pipe(8, 0)
+    jobs = [_c2(1 << 16, 930 + t, oracle_c) for t in range(3)]
+    streams = [torch.cuda.Stream() for _ in jobs]
+    torch.cuda.synchronize()
+    barrier = threading.Barrier(len(jobs))
+    errors = []
+
+    def worker(i):
+        try:
+            a = jobs[i][0]
+            barrier.wait()
+            for _ in range(10):
+                pctx.batch_fixed_ex(tcpck.OP_FILL, a, 1492, 1492, 1 << 16, None, tcpck.KERNEL_AUTO,
+                                    stream=streams[i])
+            streams[i].synchronize()
+        except Exception as e:  # noqa: BLE001 -- reported below
+            errors.append(e)
+
+    th = [threading.Thread(target=worker, args=(i,)) for i in range(len(jobs))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors, errors
+    for a, want, _ in jobs:
+        np.testing.assert_array_equal(host(a), want)
+
+
+def test_pipe_under_graph_capture_is_serial(pctx, oracle_c):
+    """A pipelined-K FILL captured into a HIP graph: the capture check keeps
+    it on the caller's stream (no pipe stream in the graph), replay exact."""
+    import tcpck
+    pctx.set_fill_pipe(8, 0)
+    count, L = 1 << 16, 1492
+    a, want, offs = _c2(count, 940, oracle_c)
+    out = torch.empty(count, dtype=torch.int16, device="cuda")
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            pctx.batch_fixed_ex(tcpck.OP_FILL, a, L, L, count, out, tcpck.KERNEL_AUTO,
+                                 stream=torch.cuda.current_stream())
+    tcpck.synth_fixed(a, L, L, count, seed=940)
+    g.replay()
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(host(a), want)
+    np.testing.assert_array_equal(host(out).view(np.uint16), fields(want, offs))
+
+
+def test_scratch_refusal_is_retried(built_lib, oracle_c):
+    """a refused scratch allocation is not latched.  The first
+    out-less FILL is refused (in-stream form, same bytes, no slot); 64 calls
+    later the allocation is retried and a slot is taken."""
+    import tcpck
+    c = tcpck.Context(0, probe=True)
+    try:
+        assert c.scratch_fail(1) == 0
+        count, L = 1 << 14, 1492
+        a, want, _ = _c2(count, 950, oracle_c)
+        c.batch_fixed(tcpck.OP_FILL, a, L, L, count, None)
+        np.testing.assert_array_equal(host(a), want)
+        assert c.scratch_state() == (0, 0)
+        assert c.scratch_fail(0) == 1
+        for _ in range(63):  # calls 2..64: still inside the retry window
+            c.batch_fixed(tcpck.OP_FILL, a, L, L, count, None)
+        assert c.scratch_state() == (0, 0)
+        c.batch_fixed(tcpck.OP_FILL, a, L, L, count, None)  # call 65, the 64th after the refusal: retried
+        np.testing.assert_array_equal(host(a), want)
+        alloc, used = c.scratch_state()
+        assert alloc == 4 and used != 0
+    finally:
+        c.close()
+
+
+def test_receive_rejected_kernel_leaves_headers(built_lib):
+    """RECEIVE into a header array with a rejected explicit kernel
+    (rstream needs stride == len) returns an error and leaves the header array
+    as it was (libtcpck.so: the header pass follows an explicit kernel)."""
+    import tcpck
+    c = tcpck.Context(0)
+    try:
+        count, L, stride = 4096, 1492, 2048
+        a = torch.empty(count * stride, dtype=torch.uint8, device="cuda")
+        tcpck.synth_fixed(a, stride, L, count, seed=960)
+        hdr = torch.full((count * 32,), 0xA5, dtype=torch.uint8, device="cuda")
+        ok = torch.empty(count, dtype=torch.uint8, device="cuda")
+        with pytest.raises(tcpck.TcpckError):
+            c.batch_receive(a, count, ok, hdr, stride=stride, length=L, kernel=tcpck.KERNEL_RSTREAM, param=20)
+        assert bool((hdr == 0xA5).all().item())
+        # the same call under AUTO runs (header pass first) and fills the array
+        c.batch_receive(a, count, ok, hdr, stride=stride, length=L)
+        torch.cuda.synchronize()
+        assert not bool((hdr == 0xA5).all().item())
+    finally:
+        c.close()
