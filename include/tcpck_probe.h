@@ -82,7 +82,9 @@ int tcpck_probe_scratch_fail(tcpck_ctx *ctx, int n, uint64_t *refusals);
  * stream of priority prio (hipStreamCreateWithPriority; a changed priority
  * recreates the stream after draining it) beside the stream pass of chunk
  * i + 1.  Applies to FILLs whose form has a field pass, at least 4096 images
- * per chunk, k <= 32. */
+ * per chunk, k <= 32.  k | TCPCK_PROBE_PIPE_ONE_STREAM: the same k chunks
+ * with both passes on the caller's stream (the cost of chunking alone). */
+#define TCPCK_PROBE_PIPE_ONE_STREAM 0x100
 int tcpck_probe_set_fill_pipe(tcpck_ctx *ctx, int k, int prio);
 
 /* Timing-only streaming micro-kernel over d_buf (results are not checksums):

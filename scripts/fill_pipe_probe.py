@@ -18,9 +18,12 @@ part of the slack: C3 636 -> <= 560 us (fill_c3 >= 0.66) if the overlap is
 real.  Stop rule: if no K in {4, 8, 16} beats serial by >= 3 % at C3, FILL is
 closed.
 
-  --ks 0,2,4,8,16,32   chunk counts (0 = serial)
+  --ks 0,2,4,8,16,32   chunk counts (0 = serial; + 256: the chunks on the caller's
+                       stream only, no pipe stream -- the chunking cost alone)
   --prio 0,-1          pipe stream priorities
   --only c3,c3_noout,c2,c2_noout
+  --pmc-calls N        (under rocprofv3 --pmc, one K per run) N FILLs and no timing;
+                       scripts/fill_pipe_pmc.py sums the counters per call
 """
 import argparse
 import os
@@ -54,7 +57,7 @@ def timed(fn, s, reps=10, rounds=5):
     return float(np.median(t)), float(min(t)), float(max(t))
 
 
-def run_case(ctx, s, name, ks, prios, reps, rounds):
+def run_case(ctx, s, name, ks, prios, reps, rounds, pmc_calls=0):
     n_c3 = 4 << 20
     if name.startswith("c3"):
         off, ln, total = synth_np.mixed_layout(n_c3, seed=42)
@@ -99,6 +102,15 @@ def run_case(ctx, s, name, ks, prios, reps, rounds):
             turn[0] += 1
         return f
 
+    if pmc_calls:  # rocprofv3 --pmc runs: exactly pmc_calls FILLs of each form, nothing else timed
+        for k in ks:
+            ctx.set_fill_pipe(k, prios[0])
+            for _ in range(pmc_calls):
+                step(call, None if noout else out)()
+            torch.cuda.synchronize()
+            print(f"{name:10s} FILL K {k}: {pmc_calls} calls", flush=True)
+        ctx.set_fill_pipe(-1, 0)
+        return
     ms, lo, hi = timed(step(checksum, out), s, reps, rounds)
     print(f"{name:10s} CHECKSUM          {ms * 1e3:8.1f} us [{lo * 1e3:.1f}, {hi * 1e3:.1f}]  "
           f"{(img + 2 * n) / ms / 1e6 / 80:5.1f} % of the roof", flush=True)
@@ -113,7 +125,9 @@ def run_case(ctx, s, name, ks, prios, reps, rounds):
             torch.cuda.synchronize()
             time.sleep(0.05)
             ms, lo, hi = timed(step(call, None if noout else out), s, reps, rounds)
-            label = "serial" if k == 0 else f"pipe K{k:<2d} prio{prio:+d}"
+            kk = k & 0xFF
+            label = ("serial" if k == 0 else f"pipe K{kk:<2d} prio{prio:+d}" if not k & tcpck.PROBE_PIPE_ONE_STREAM
+                     else f"chunks K{kk:<2d} 1-strm")
             line = (f"{name:10s} FILL {label:14s} {ms * 1e3:8.1f} us [{lo * 1e3:.1f}, {hi * 1e3:.1f}]  "
                     f"{algo_fill / ms / 1e6 / 80:5.1f} % of the roof")
             got = (None if noout else out.clone(), arenas[0].clone(), arenas[1].clone())
@@ -136,6 +150,8 @@ def main():
     p.add_argument("--only", default="c3,c3_noout,c2,c2_noout")
     p.add_argument("--reps", type=int, default=10)
     p.add_argument("--rounds", type=int, default=5)
+    p.add_argument("--pmc-calls", type=int, default=0,
+                   help="for rocprofv3 --pmc: only this many FILL calls per K (one K per run), no timing")
     args = p.parse_args()
     print(__doc__.split("Hypothesis")[1].split("--ks")[0].strip(), flush=True)
     ctx = tcpck.Context(0, probe=True)
@@ -143,7 +159,7 @@ def main():
     ks = [int(x) for x in args.ks.split(",")]
     prios = [int(x) for x in args.prio.split(",")]
     for name in args.only.split(","):
-        run_case(ctx, s, name, ks, prios, args.reps, args.rounds)
+        run_case(ctx, s, name, ks, prios, args.reps, args.rounds, args.pmc_calls)
     ctx.close()
 
 

@@ -1038,15 +1038,18 @@ int fill_pipe_k(int op, int kernel, bool has_field_pass, uint64_t count, hipStre
 
 // launch(k0, n, ps, pev) enqueues images [k0, k0 + n): the stream pass on s,
 // the field pass on ps after pev (ps == nullptr: everything on s).
+// (one_stream, probe library: the same chunks with both passes on s -- the
+// cost of chunking alone, without the second stream)
 template <typename Launch>
-hipError_t fill_pipelined(tcpck_ctx *ctx, int k, uint64_t count, hipStream_t s, Launch launch) {
+hipError_t fill_pipelined(tcpck_ctx *ctx, int k, uint64_t count, hipStream_t s, bool one_stream, Launch launch) {
   std::lock_guard<std::mutex> lk(ctx->pipe_mu);
   if (ensure_pipe(ctx) != hipSuccess) return launch(0, count, nullptr, nullptr);  // the serial form
   hipError_t e = hipSuccess;
   const uint64_t per = (count + static_cast<uint64_t>(k) - 1) / static_cast<uint64_t>(k);
   int i = 0;
   for (uint64_t k0 = 0; k0 < count && e == hipSuccess; k0 += per, ++i)
-    e = launch(k0, std::min(per, count - k0), ctx->pipe, ctx->pipe_ev[i]);
+    e = one_stream ? launch(k0, std::min(per, count - k0), nullptr, nullptr)
+                   : launch(k0, std::min(per, count - k0), ctx->pipe, ctx->pipe_ev[i]);
   // join, also after an error: nothing the caller enqueues next may overtake a field pass already queued
   hipError_t ej = hipEventRecord(ctx->pipe_ev[tcpck_ctx::kPipeMax], ctx->pipe);
   if (ej == hipSuccess) ej = hipStreamWaitEvent(s, ctx->pipe_ev[tcpck_ctx::kPipeMax], 0);
@@ -1060,7 +1063,7 @@ hipError_t fill_fixed(tcpck_ctx *ctx, int mode, uint8_t *arena, uint64_t stride,
   const int k = fill_pipe_k(TCPCK_OP_FILL, kernel, field_pass, count, s, hk);
   if (k <= 1)
     return run_fixed(ctx, TCPCK_OP_FILL, mode, arena, stride, len, count, out, kernel, param, s, nullptr, hk);
-  return fill_pipelined(ctx, k, count, s, [&](uint64_t k0, uint64_t n, hipStream_t ps, hipEvent_t pev) {
+  return fill_pipelined(ctx, k, count, s, hk.pipe_one_stream, [&](uint64_t k0, uint64_t n, hipStream_t ps, hipEvent_t pev) {
     return run_fixed_r(ctx, TCPCK_OP_FILL, mode, arena + k0 * stride, n == 1 ? len : stride, len, n, out + k0, kernel,
                        param, s, nullptr, hk, ps, pev);
   });
@@ -1072,7 +1075,7 @@ hipError_t fill_var(tcpck_ctx *ctx, int mode, uint8_t *arena, const uint64_t *of
   const bool field_pass = out && kernel == TCPCK_KERNEL_AUTO && fill_reads_results_var(mode, layout, count, param);
   const int k = fill_pipe_k(TCPCK_OP_FILL, kernel, field_pass, count, s, hk);
   if (k <= 1) return run_var(ctx, TCPCK_OP_FILL, mode, arena, off, len, 0, count, out, layout, kernel, param, s, nullptr, hk);
-  return fill_pipelined(ctx, k, count, s, [&](uint64_t k0, uint64_t n, hipStream_t ps, hipEvent_t pev) {
+  return fill_pipelined(ctx, k, count, s, hk.pipe_one_stream, [&](uint64_t k0, uint64_t n, hipStream_t ps, hipEvent_t pev) {
     tcpck_layout sub{};
     if (layout) sub = sub_layout(*layout, n, count);
     return run_var_r(ctx, TCPCK_OP_FILL, mode, arena, off + k0, len + k0, 0, n, out + k0, layout ? &sub : nullptr,

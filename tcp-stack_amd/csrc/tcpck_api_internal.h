@@ -69,6 +69,7 @@ struct tcpck_ctx {
   hipEvent_t pipe_ev[kPipeMax + 1] = {};
   int pipe_prio = 0;               // the pipe stream's priority (probe: tcpck_probe_set_fill_pipe)
   int probe_fill_pipe = -1;        // probe library: K (0/1 off, -1 AUTO's rule)
+  bool probe_pipe_one_stream = false;  // probe library: the K chunks one after the other on the caller's stream
 
   // probe library only (tcpck_ex_probe.hip): per-wave time stamp buffer, and the
   // side stream + events of the concurrent RECEIVE form
@@ -95,6 +96,7 @@ struct Hooks {
   uint32_t hdr_store_bits = 0;   // HeaderArgs::store_bits of the header pass
   bool patch_reverse = false;    // FILL's field pass in reverse image order (PatchArgs::reverse)
   int fill_pipe = -1;            // pipelined FILL chunks: -1 AUTO's rule, 0 / 1 off, K > 1 K chunks
+  bool pipe_one_stream = false;  // ... every chunk's passes on the caller's stream (the chunking cost alone)
 };
 
 // probe library: tcpck_batch_*_ex param bit selecting Hooks::patch_reverse

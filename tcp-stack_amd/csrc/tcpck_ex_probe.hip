@@ -106,7 +106,10 @@ int tcpck_batch_fixed_ex(tcpck_ctx *ctx, int op, int mode, void *d_arena, uint64
   }
   Hooks hk = probe_hooks(0);
   hk.patch_reverse = (param & tcpck::api::kProbeParamPatchReverse) != 0;
-  if (ctx) hk.fill_pipe = ctx->probe_fill_pipe;
+  if (ctx) {
+    hk.fill_pipe = ctx->probe_fill_pipe;
+    hk.pipe_one_stream = ctx->probe_pipe_one_stream;
+  }
   return tcpck::api::batch_fixed_ex(ctx, op, mode, d_arena, stride, len, count, d_out, kernel,
                                     param & ~tcpck::api::kProbeParamPatchReverse, static_cast<hipStream_t>(stream), hk);
 }
@@ -116,7 +119,10 @@ int tcpck_batch_var_ex(tcpck_ctx *ctx, int op, int mode, void *d_arena, const ui
                        int kernel, int param, tcpck_stream stream) {
   Hooks hk = probe_hooks(0);
   hk.patch_reverse = (param & tcpck::api::kProbeParamPatchReverse) != 0;
-  if (ctx) hk.fill_pipe = ctx->probe_fill_pipe;
+  if (ctx) {
+    hk.fill_pipe = ctx->probe_fill_pipe;
+    hk.pipe_one_stream = ctx->probe_pipe_one_stream;
+  }
   return tcpck::api::batch_var_ex(ctx, op, mode, d_arena, d_offsets, d_lengths, count, d_out, layout, kernel,
                                   param & ~tcpck::api::kProbeParamPatchReverse, static_cast<hipStream_t>(stream), hk);
 }
@@ -191,6 +197,8 @@ int tcpck_probe_scratch_fail(tcpck_ctx *ctx, int n, uint64_t *refusals) {
 }
 
 int tcpck_probe_set_fill_pipe(tcpck_ctx *ctx, int k, int prio) {
+  const bool one_stream = k >= 0 && (k & TCPCK_PROBE_PIPE_ONE_STREAM);
+  if (k >= 0) k &= ~TCPCK_PROBE_PIPE_ONE_STREAM;
   if (!ctx || k < -1 || k > tcpck_ctx::kPipeMax) return TCPCK_EINVAL;
   std::lock_guard<std::mutex> lk(ctx->pipe_mu);
   if (ctx->pipe && prio != ctx->pipe_prio) {
@@ -201,6 +209,7 @@ int tcpck_probe_set_fill_pipe(tcpck_ctx *ctx, int k, int prio) {
   }
   ctx->pipe_prio = prio;
   ctx->probe_fill_pipe = k;
+  ctx->probe_pipe_one_stream = one_stream;
   return TCPCK_OK;
 }
 

@@ -1,0 +1,105 @@
+"""The C ABI's host logic under AddressSanitizer + UBSan.
+
+tcp-stack_amd/Makefile `asan` (run by __graft_entry__.build()) builds
+libtcpck_asan.so -- the product library with its HOST code compiled
+-fsanitize=address,undefined (device code untouched) -- and, against it,
+tests/cpp/build/abi_host_test (tests/cpp/abi_host_test.cc) and the drop-in
+C++ test tests/cpp/build/drop_in_test_libasan.  A sanitizer report aborts the
+program (-fno-sanitize-recover=all), so a zero exit status is a clean run.
+
+CPU (here): argument validation of every entry point, the host single-image
+paths at every alignment, the drop-in header's golden vectors and known
+answers, and tests/test_abi.py + tests/test_oracle.py in a python that loads
+the sanitized library (TCPCK_LIB_VARIANT=asan, sanitizer runtime preloaded).
+GPU box (-m gpu): every batch entry point incl. the results-scratch chunks
+past 8M images, host batches in many chunks over two contexts, four threads of
+out-less FILLs, and the drop-in PacketBatch / receive / segment paths.  The
+error contract is SURVEY §8b's (include/tcp-header.h:259-260: odd lengths are
+an out-of-bounds read in the reference, TCPCK_EINVAL here).
+"""
+import glob
+import os
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+BUILD = os.path.join(ROOT, "tests", "cpp", "build")
+ABI_TEST = os.path.join(BUILD, "abi_host_test")
+DROPIN = os.path.join(BUILD, "drop_in_test_libasan")
+LIB = os.path.join(ROOT, "tcp-stack_amd", "libtcpck_asan.so")
+ENV = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=0:halt_on_error=1",
+           UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
+
+
+@pytest.fixture(scope="module")
+def asan_build(built_lib):
+    srcs = [os.path.join(ROOT, "tests", "cpp", f) for f in ("abi_host_test.cc", "drop_in_test.cc")]
+    srcs += glob.glob(os.path.join(ROOT, "tcp-stack_amd", "csrc", "*"))
+    outs = (LIB, ABI_TEST, DROPIN)
+    if not all(os.path.exists(o) for o in outs) or \
+            max(map(os.path.getmtime, srcs)) > min(map(os.path.getmtime, outs)):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tcp-stack_amd"), "-j8", "asan"], check=True)
+    return True
+
+
+def run(args, timeout=300):
+    r = subprocess.run(args, capture_output=True, text=True, env=ENV, timeout=timeout, cwd="/tmp")
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+    assert "ERROR: AddressSanitizer" not in r.stderr and "runtime error:" not in r.stderr, r.stderr[-4000:]
+    return r.stdout.splitlines()
+
+
+def test_library_is_instrumented(asan_build):
+    """The host code of libtcpck_asan.so calls the sanitizer runtime; libtcpck.so does not."""
+    syms = subprocess.run(["nm", "-D", "--undefined-only", LIB], capture_output=True, text=True, check=True).stdout
+    assert "__asan_report" in syms and "__ubsan_handle" in syms
+    prod = subprocess.run(["nm", "-D", os.path.join(ROOT, "tcp-stack_amd", "libtcpck.so")], capture_output=True,
+                          text=True, check=True).stdout
+    assert "__asan" not in prod
+
+
+def test_abi_host_logic_cpu(asan_build):
+    lines = run([ABI_TEST, "cpu"])
+    assert lines[-1].startswith("ok ") and int(lines[-1].split()[1]) > 10000
+
+
+def test_drop_in_golden_and_layout(asan_build, golden, tmp_path):
+    manifest = tmp_path / "manifest.txt"
+    manifest.write_text("".join(f"{c['kind']} {c['off']} {c['len']}\n" for c in golden.cases))
+    lines = run([DROPIN, "golden", os.path.join(ROOT, "tests", "golden", "golden.bin"), str(manifest)])
+    assert len(lines) == len(golden.cases)
+    for c, line in zip(golden.cases, lines):
+        assert int(line.split()[0]) == c["expected"], c["name"]
+    out = dict(line.split(" ", 1) for line in run([DROPIN, "layout"]))
+    assert int(out["checksum"]) == 0x4BA4 and out["reverify"] == "0"
+
+
+def test_python_suite_on_sanitized_library(asan_build):
+    """tests/test_abi.py and tests/test_oracle.py in a python that loads
+    libtcpck_asan.so (the sanitizer runtime preloaded; python itself is not
+    instrumented)."""
+    rt = glob.glob("/opt/rocm/lib/llvm/lib/clang/*/lib/linux/libclang_rt.asan-x86_64.so")
+    assert rt, "clang's shared ASan runtime"
+    env = dict(ENV, LD_PRELOAD=rt[0], TCPCK_LIB_VARIANT="asan")
+    tests = [os.path.join(ROOT, "tests", f) for f in ("test_abi.py", "test_oracle.py")]
+    r = subprocess.run([sys.executable, "-m", "pytest", "-x", "-q", "-m", "not gpu", "-p", "no:cacheprovider",
+                        *tests], capture_output=True, text=True, env=env, timeout=600, cwd="/tmp")
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "ERROR: AddressSanitizer" not in r.stdout + r.stderr
+
+
+@pytest.mark.gpu
+def test_abi_host_logic_gpu(asan_build):
+    lines = run([ABI_TEST, "gpu"], timeout=600)
+    assert lines[-1].startswith("ok ")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("args", [("batch", 20000, 7, 3), ("receive", 5000, 2048, 5), ("segment", 1_000_000, 1448, 11)],
+                         ids=["packet_batch", "receive", "segment"])
+def test_drop_in_gpu_paths(asan_build, args):
+    lines = run([DROPIN, *map(str, args)], timeout=300)
+    assert lines[-1].endswith("mismatches=0"), lines
