@@ -6,19 +6,21 @@ KiB, FETCH_SIZE doubled on gfx950 for wide streaming reads).
 
     python scripts/fill_pipe_pmc.py DIR_PREFIX N  ->  per K: read GB, written GB per call
 
-DIR_PREFIX_<K>_{fetch,write}/run_counter_collection.csv; the synth kernels
-(the batch generator) are excluded, every other dispatch is a FILL's.
+DIR_PREFIX_<K>_{fetch,write}/run_counter_collection.csv; only the FILL's own
+kernels (OURS) count -- the batch generator and torch's clone are excluded.
 """
 import csv
 import glob
 import sys
+
+OURS = ("vvstream_kernel", "rstream_kernel", "patch_fields_kernel", "seg_kernel", "sstream_kernel")
 
 
 def total(path: str, counter: str) -> float:
     s = 0.0
     with open(path) as f:
         for r in csv.DictReader(f):
-            if "synth" in r["Kernel_Name"] or r.get("Counter_Name", counter) != counter:
+            if not any(k in r["Kernel_Name"] for k in OURS) or r.get("Counter_Name", counter) != counter:
                 continue
             s += float(r["Counter_Value"])
     return s

@@ -201,16 +201,17 @@ constexpr uint64_t kFixedRunMaxLen = 4096;   // packed fixed: rstream up to here
 // order (dev::ordered_block, groups of 16 blocks per XCD): each XCD streams
 // compact regions instead of every eighth run (C2 86.3% -> 90.6%, C3 82.7 ->
 // 84.1%, C4 85.5 -> 87.4%, profiles/r01/xcd_*.log; the HBM bytes do not
-// change, PMC).  rstream also reads each run's first step with the default
+// change, PMC).  rstream also reads each run's first line with the default
 // cache policy: that line is the previous run's last line, and the
 // neighbour's last step then finds it in L2 (PMC bytes x1.015 -> x1.000;
-// C2 90.9 -> 93.1%), and large batches keep runs of 4-8 KiB with up to
+// C2 90.9 -> 93.1% warm with the whole first step; since round 5 only the
+// first line, 92.3% cold and warm), and large batches keep runs of 4-8 KiB with up to
 // 1024 x the resident grid (C5: 256x, 84.7% at 32x -> 92.5%,
 // profiles/r01/oversub_c5_first_step.log, split_probe.log); vvstream the
 // same with runs >= 8 KiB (C3 86.3 -> 89.5%, profiles/r01/xcd_first_step_probe.log).
-constexpr int kRstreamPolicy = 20;       // v_dot2 sums, buffer loads, XCD-chunked order, L2-kept first step
+constexpr int kRstreamPolicy = 20;       // v_dot2 sums, buffer loads, XCD-chunked order, L2-kept first line
 constexpr int kRstreamDeferFill = 25;    // FILL: kRstreamPolicy's stream to out, then the 2-B write-through field pass
-constexpr int kVvPolicy = 4 | 8 | 16;    // size policy, XCD-chunked order, L2-kept first step
+constexpr int kVvPolicy = 4 | 8 | 16;    // size policy, XCD-chunked order, L2-kept first line
 constexpr int kSegXcdOrder = 1 << 24;    // seg: XCD-chunked order
 // seg W16 on packed jumbo images (C4): image k's chunk walk starts at 1-KiB
 // step (29 k) mod 64 and wraps (SegArgs::rot), so the blocks in flight --
@@ -241,7 +242,7 @@ constexpr uint64_t kDeferFillMinLen = 512;
 // (rstream 25) -> 322, 768 B 318 -> 308; 1 KiB stays on rstream 25: 279 vs 284)
 constexpr uint64_t kVvDeferPackedMin = 320, kVvDeferPackedEnd = 1024;
 constexpr int kSstreamDeferFill = 128;   // sstream: kFill writes the results only, the field pass follows
-// variable layouts: vvstream's in-stream zeroing costs ~25 ns per image, so
+// variable layouts: vvstream's in-stream zeroing costs ~25 us per 1M images, so
 // its deferred form pays only for larger images (C3's mean 732 B: 718 -> 702
 // us; 256-1024 B: 700 -> 740 us; 1492 B: 365 -> 262 us; profiles/r03/fill_forms.log)
 constexpr uint64_t kDeferFillMinVar = 1024;
@@ -517,7 +518,7 @@ hipError_t run_fixed_impl(tcpck_ctx *ctx, int op, int mode, uint8_t *arena, uint
 // and writes it through into the field and out[k].  Round 3 (the pass's stores
 // written through, scripts/fill_defer_vv_probe.py, profiles/r03/fill_forms.log,
 // % of the roof, in-stream -> update): packed variable batches on vvstream,
-// whose in-stream field zeroing costs ~25 ns per image, gain most -- C3 53.7 ->
+// whose in-stream field zeroing costs ~25 us per 1M images, gain most -- C3 53.7 ->
 // 62.2 %, a 608/1492 mix 46.6 -> 69.2 %, 256-1024 B 48.3 -> 55.4 % -- so AUTO
 // takes it there for typical images >= 448 B (below, vvstream's default-policy
 // in-stream FILL); gapped fixed jumbo images keep it (9000 B in 9216-B slots

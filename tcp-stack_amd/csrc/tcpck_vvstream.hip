@@ -631,7 +631,7 @@ hipError_t launch_vvstream(int op, int variant, bool fixed, const RunArgs &a, ui
   const bool gap = fixed && a.stride != a.len;
   const uint64_t bytes = fixed ? a.count * a.stride : a.total_bytes;
   uint32_t m = a.oversub ? a.oversub : 1;
-  // 8: XCD-chunked run order; 16: L2-kept first step; 32: kFill reads every
+  // 8: XCD-chunked run order; 16: L2-kept first line; 32: kFill reads every
   // step with the default cache policy (small images); 64: kFill writes the
   // results only (the caller runs launch_patch_fields for the fields); 128:
   // kFill stores each field's whole 64-B block (BLK; reference mode, no gaps)

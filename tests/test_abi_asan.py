@@ -85,8 +85,13 @@ def test_python_suite_on_sanitized_library(asan_build):
     assert rt, "clang's shared ASan runtime"
     env = dict(ENV, LD_PRELOAD=rt[0], TCPCK_LIB_VARIANT="asan")
     tests = [os.path.join(ROOT, "tests", f) for f in ("test_abi.py", "test_oracle.py")]
+    # (test_ctx_create_without_gpu_fails_cleanly asks torch whether a GPU is
+    # present: on a GPU box that initialises torch's own HIP stack under the
+    # preloaded runtime, third-party code outside this check's scope; the C++
+    # abi_host_test covers context creation on the device instead)
     r = subprocess.run([sys.executable, "-m", "pytest", "-x", "-q", "-m", "not gpu", "-p", "no:cacheprovider",
-                        *tests], capture_output=True, text=True, env=env, timeout=600, cwd="/tmp")
+                        "-k", "not ctx_create_without_gpu", *tests], capture_output=True, text=True, env=env,
+                       timeout=600, cwd="/tmp")
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "ERROR: AddressSanitizer" not in r.stdout + r.stderr
 
