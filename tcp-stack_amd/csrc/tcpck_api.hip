@@ -162,6 +162,7 @@ void free_stage(tcpck_ctx *ctx) {
   }
   for (auto &ev : ctx->pipe_ev)
     if (ev) (void)hipEventDestroy(ev);
+  if (ctx->probe_side) (void)hipFree(ctx->probe_side);
   if (ctx->side) {
     (void)hipEventDestroy(ctx->fork);
     (void)hipEventDestroy(ctx->join);

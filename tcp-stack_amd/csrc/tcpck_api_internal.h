@@ -74,6 +74,8 @@ struct tcpck_ctx {
   // probe library only (tcpck_ex_probe.hip): per-wave time stamp buffer, and the
   // side stream + events of the concurrent RECEIVE form
   void *dbg = nullptr;
+  uint8_t *probe_side = nullptr;   // rstream 33 / 34: the field blocks' side buffer (64 B per image)
+  uint64_t probe_side_cap = 0;
   std::mutex side_mu;
   hipStream_t side = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;

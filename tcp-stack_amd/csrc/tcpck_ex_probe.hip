@@ -85,6 +85,47 @@ int tcpck_batch_fixed_ex(tcpck_ctx *ctx, int op, int mode, void *d_arena, uint64
     return hip_status(tcpck::launch_patch_fields(pa, static_cast<uint32_t>(ctx->num_cus),
                                                  static_cast<hipStream_t>(stream)));
   }
+  if (kernel == TCPCK_KERNEL_RSTREAM && ((param & 0xFF) == 33 || (param & 0xFF) == 34)) {
+    // FILL with each field's 64-B block staged to a dense side buffer by the
+    // stream, then copied whole to its place (launch_side_copy): no merge read
+    // (round 6 probe; param bit 8: the side stores nt)
+    if (!ctx || op != TCPCK_OP_FILL || mode != TCPCK_MODE_REF || !d_arena || !d_out || count == 0 ||
+        stride != len || len < 128 || (reinterpret_cast<uintptr_t>(d_arena) & 1))
+      return TCPCK_EINVAL;
+    if (count > (UINT64_MAX >> 7) || stride > (UINT64_MAX - len) / count) return TCPCK_EINVAL;
+    DeviceGuard g(ctx->device);
+    if (g.status() != hipSuccess) return hip_status(g.status());
+    const auto s = static_cast<hipStream_t>(stream);
+    if (ctx->probe_side_cap < 64 * count) {
+      if (ctx->probe_side) {
+        (void)hipStreamSynchronize(s);
+        (void)hipFree(ctx->probe_side);
+        ctx->probe_side = nullptr;
+        ctx->probe_side_cap = 0;
+      }
+      void *p = nullptr;
+      if (hipMalloc(&p, 64 * count) != hipSuccess) {
+        (void)hipGetLastError();
+        return TCPCK_ENOMEM;
+      }
+      ctx->probe_side = static_cast<uint8_t *>(p);
+      ctx->probe_side_cap = 64 * count;
+    }
+    tcpck::FixedStreamArgs a{};
+    a.mode = tcpck::kRef;
+    a.arena = static_cast<uint8_t *>(d_arena);
+    a.stride = stride;
+    a.count = count;
+    a.out = d_out;
+    a.order = 0xFFu;
+    a.side = ctx->probe_side;
+    a.side_nt = (param >> 8) & 1u;
+    hipError_t e = tcpck::launch_rstream(tcpck::kFill, param & 0xFF, a, static_cast<uint32_t>(ctx->num_cus), s);
+    if (e == hipSuccess)
+      e = tcpck::launch_side_copy(static_cast<uint8_t *>(d_arena), stride, count, ctx->probe_side,
+                                  static_cast<const uint16_t *>(d_out), static_cast<uint32_t>(ctx->num_cus), s);
+    return hip_status(e);
+  }
   if (kernel == TCPCK_KERNEL_RSTREAM && ((param & 0xFF) == 29 || (param & 0xFF) == 30)) {
     // FILL's deferred stream ALONE (timing): results to d_out, the fields left
     // for a TCPCK_KERNEL_PATCH pass the caller times separately

@@ -442,4 +442,44 @@ hipError_t launch_header_swap(const HeaderArgs &a, uint32_t num_cus, hipStream_t
   return a.offsets ? launch_one<false, false>(a, num_cus, stream) : launch_one<true, false>(a, num_cus, stream);
 }
 
+#ifdef TCPCK_PROBE
+// ---- FILL's field blocks from the side buffer (probe, round 6) --------------
+// Four lanes per image: lane c copies bytes [16c, 16c + 16) of image k's block
+// from side[64 k] to the block's place with a write-through 16-B store (sc0
+// sc1 nt): a whole 64-B block needs no merge read at the memory side, where a
+// 2-B store does (profiles/r03/fill_blind.log: blind 64-B blocks 20 us per 1M
+// fields after the stream, 2-B stores 41-42 us).  The side buffer holds the
+// bytes the stream read, checksum in place, so nothing else changes.
+__global__ void __launch_bounds__(kBlock) side_copy_kernel(uint8_t *arena, uint64_t stride, uint64_t count,
+                                                           const uint8_t *side, const uint16_t *sums) {
+  const uint64_t step = static_cast<uint64_t>(gridDim.x) * kBlock;
+  for (uint64_t q = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x; q < 4 * count; q += step) {
+    const uint64_t k = q >> 2;
+    const uint32_t c = static_cast<uint32_t>(q & 3u);
+    const uintptr_t f = reinterpret_cast<uintptr_t>(arena) + k * stride + 28;
+    const uintptr_t blk = f & ~uintptr_t{63};
+    if (blk >= reinterpret_cast<uintptr_t>(arena)) {
+      const dev::u32x4 v = dev::load16_nt(side + 64 * k + 16 * c);
+      uint8_t *dst = reinterpret_cast<uint8_t *>(blk + 16 * c);
+      asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt" ::"v"(dst), "v"(v) : "memory");
+    } else if (c == ((f & 63u) >> 4)) {  // the block starts before the arena: the field alone
+      store16_through(reinterpret_cast<uint8_t *>(f), sums[k]);
+    }
+  }
+}
+
+hipError_t launch_side_copy(uint8_t *arena, uint64_t stride, uint64_t count, const uint8_t *side,
+                            const uint16_t *sums, uint32_t num_cus, hipStream_t stream) {
+  if (count == 0) return hipSuccess;
+  if (stride < 128 || !side || !sums) return hipErrorInvalidValue;
+  static const uint32_t per_cu = dev::resident_blocks_per_cu(side_copy_kernel);
+  uint64_t blocks = (4 * count + kBlock - 1) / kBlock;
+  const uint64_t cap = static_cast<uint64_t>(per_cu) * num_cus * 8;
+  if (blocks > cap) blocks = cap;
+  hipLaunchKernelGGL(side_copy_kernel, dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0, stream, arena, stride,
+                     count, side, sums);
+  return hipGetLastError();
+}
+#endif
+
 }  // namespace tcpck

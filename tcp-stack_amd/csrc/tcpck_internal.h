@@ -79,6 +79,9 @@ struct FixedStreamArgs {
   uint32_t order;          // block order (dev::ordered_block; 0xFF default)
   int mode;                // kRef, or kRfc1071 (variant 20 only)
   uint32_t defer_field;    // kFill: results to out only, the fields left for launch_patch_fields
+  uint8_t *side;           // probe variants 33 / 34 (kFill): each field's 64-B block, checksum in place, to
+                           // side[64 k, 64 k + 64) for launch_side_copy (nullptr otherwise)
+  uint32_t side_nt;        // ... those side stores nt (else the default policy)
 };
 
 // Fixed stride == len == S, S a power of two in [32, 1024], 16-B aligned arena
@@ -199,6 +202,13 @@ struct PatchArgs {
   uint32_t reverse;         // the fields in reverse index order (the stream's last lines first)
 };
 hipError_t launch_patch_fields(const PatchArgs &a, uint32_t num_cus, hipStream_t stream);
+// Probe (round 6): FILL's field blocks from a dense side buffer -- image k's
+// 64-B block (the stream's bytes, checksum in place; rstream variants 33 / 34)
+// copied from side[64 k] to its place, a whole-block write-through store that
+// needs no merge read; a block starting before the arena takes the 2-B store
+// of sums[k] instead.  Fixed stride >= 128.
+hipError_t launch_side_copy(uint8_t *arena, uint64_t stride, uint64_t count, const uint8_t *side,
+                            const uint16_t *sums, uint32_t num_cus, hipStream_t stream);
 
 
 // timing-only streaming micro-kernels (tcpck_diag.hip)

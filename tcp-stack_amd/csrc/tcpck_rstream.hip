@@ -193,6 +193,8 @@ __global__ void __launch_bounds__(kBlock) rstream_kernel(FixedStreamArgs a) {
   // block, each image's checksum from its staging lane
   auto flush_sect = [&](uint32_t j0, uint32_t n) {
     const uint32_t i = j0 + (lane >> 2), c = lane & 3u;
+    // FLAV bit 9 (probe, SIDE): the blocks go to the dense side buffer instead
+    // of in place -- 16 images' blocks are one contiguous KiB, one coalesced store
     const uint32_t cs = static_cast<uint32_t>(__shfl(static_cast<int>(stage), static_cast<int>((i - out_rel) & 63u), 64));
     if (lane < 4 * n) {
       const uint32_t f = lead + 28 + i * S;  // the field, run-relative
@@ -208,7 +210,16 @@ __global__ void __launch_bounds__(kBlock) rstream_kernel(FixedStreamArgs a) {
         v.z = di == 2 ? (v.z & m) | x : v.z;
         v.w = di == 3 ? (v.w & m) | x : v.w;
       }
-      if (static_cast<int64_t>(A0) + static_cast<int64_t>(b) >= 0) {
+      if constexpr ((FLAV & 512) != 0) {
+        typedef unsigned v4u __attribute__((ext_vector_type(4)));
+        v4u *dst = reinterpret_cast<v4u *>(a.side + (kb + i) * 64 + 16 * c);
+        const v4u x{v.x, v.y, v.z, v.w};
+        if (a.side_nt)
+          __builtin_nontemporal_store(x, dst);
+        else
+          *dst = x;
+        (void)b;
+      } else if (static_cast<int64_t>(A0) + static_cast<int64_t>(b) >= 0) {
         typedef unsigned v4u __attribute__((ext_vector_type(4)));
         __builtin_amdgcn_raw_buffer_store_b128(v4u{v.x, v.y, v.z, v.w}, rsrc, static_cast<int>(b + 16 * c), 0, 19);
       } else if ((o >> 4) == c) {  // the block starts before the arena: the field alone
@@ -426,6 +437,15 @@ hipError_t launch_rstream(int op, int variant, const FixedStreamArgs &a, uint32_
       FixedStreamArgs b = a;
       b.order = 4u;
       return dispatch<4, false, 0, 103>(op, b, num_cus, stream);
+    }
+    case 33: case 34: {  // 20's FILL with each field's block (checksum in place) to the side buffer a.side
+                         // (FLAV bits 5 + 9; 34: + bit 6, a short run's blocks after its last load), for
+                         // launch_side_copy (tcpck_ex_probe.hip)
+      if (op != kFill || a.stride < 128 || a.defer_field || !a.side) return hipErrorInvalidValue;
+      FixedStreamArgs b = a;
+      b.order = 4u;
+      return variant == 33 ? launch_one<4, kFill, false, 0, 807>(b, num_cus, stream)
+                           : launch_one<4, kFill, false, 0, 871>(b, num_cus, stream);
     }
     case 29: case 30: {  // FILL's deferred stream alone (a.defer_field): 29 with the field blocks read
                          // with the default policy (FLAV bit 7), 30 the policy's stream (timing)

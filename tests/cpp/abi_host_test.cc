@@ -42,7 +42,16 @@ long g_checks = 0;
       std::exit(1);                                                                  \
     }                                                                                \
   } while (0)
-#define CHECK_RC(expr, want) CHECK((expr) == (want))
+#define CHECK_RC(expr, want)                                                          \
+  do {                                                                                \
+    ++g_checks;                                                                       \
+    const int rc_ = (expr);                                                           \
+    if (rc_ != (want)) {                                                              \
+      std::fprintf(stderr, "FAILED %s:%d: %s = %d (%s), want %d\n", __FILE__, __LINE__, #expr, rc_, \
+                   tcpck_strerror(rc_), (want));                                      \
+      std::exit(1);                                                                   \
+    }                                                                                 \
+  } while (0)
 
 // The reference arithmetic (tcp-header.h:252-263), restated scalar: the sum of
 // little-endian u16 words mod 2^16, complemented; mode 1 folds the carries.
