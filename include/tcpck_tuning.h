@@ -149,8 +149,11 @@ extern "C" {
                                    wave; param = variant (0: policy = 4 steps in
                                    flight, XCD-chunked order, the run's first
                                    line L2-kept; probe library: 1: 8 in flight,
-                                   2: 2) | (grid oversubscription << 16: 0 = by
-                                   batch size, runs >= 4 KiB)                   */
+                                   2: 2; 3 / 4: 0 / 2 with each run's span from
+                                   a run-start table built by a pass before the
+                                   stream -- packed batches only, one table
+                                   buffer per device) | (grid oversubscription
+                                   << 16: 0 = by batch size, runs >= 4 KiB)     */
 /* FILL in TCPCK_MODE_REF with a results buffer, any kernel (param bits, OR'ed
  * with the kernel's own param):
  *   TCPCK_PARAM_FILL_UPDATE    the kernel's CHECKSUM pass, then a field pass that

@@ -37,6 +37,10 @@
 // per run before its first data load, which the fixed-stride walk never does
 // (rstream C2 92.3 %); the walk itself is not what costs.  Not AUTO's: the
 // probe library only.
+#include <map>
+#include <mutex>
+#include <utility>
+
 #include "tcpck_device.h"
 
 namespace tcpck {
@@ -222,21 +226,36 @@ hipError_t launch_one(const RunArgs &s, uint32_t num_cus, hipStream_t stream, bo
   a.per_wave = s.count / (blocks * kWavesPerBlock);
   a.rem = s.count % (blocks * kWavesPerBlock);
   a.order = 4u;  // XCD-chunked: groups of 16 blocks per XCD
-  if (table) {  // (probe) a process-wide table buffer, grown as needed: measurement only, one
-                // thread at a time (hipFree waits for the launches still reading the old one)
-    static uint64_t *g_table = nullptr;
-    static uint64_t g_cap = 0;
+  if (table) {
+    // (probe) one table buffer per device (a single process-wide
+    // buffer was reused across devices and freed under concurrent callers),
+    // grown as needed; the lock covers the growth and both launches, and a
+    // growth first drains the device, so no launch still reads the old buffer
+    static std::mutex mu;
+    static std::map<int, std::pair<uint64_t *, uint64_t>> tables;  // device -> (buffer, entries)
+    std::lock_guard<std::mutex> lk(mu);
+    int device = 0;
+    if (hipGetDevice(&device) != hipSuccess) return hipGetLastError();
+    auto &t = tables[device];
     const uint64_t runs = blocks * kWavesPerBlock;
-    if (runs + 1 > g_cap) {
-      if (g_table) (void)hipFree(g_table);
-      g_table = nullptr;
-      g_cap = 0;
-      if (hipMalloc(&g_table, (runs + 1) * 8) != hipSuccess) return hipErrorOutOfMemory;
-      g_cap = runs + 1;
+    if (runs + 1 > t.second) {
+      if (t.first) {
+        (void)hipDeviceSynchronize();
+        (void)hipFree(t.first);
+      }
+      t = {nullptr, 0};
+      void *p = nullptr;
+      if (hipMalloc(&p, (runs + 1) * 8) != hipSuccess) {
+        (void)hipGetLastError();
+        return hipErrorOutOfMemory;
+      }
+      t = {static_cast<uint64_t *>(p), runs + 1};
     }
     hipLaunchKernelGGL(run_table_kernel, dim3(static_cast<uint32_t>((runs + 256) / 256)), dim3(256), 0, stream,
-                       s.offsets, s.lengths, s.base, s.count, a.per_wave, a.rem, runs, g_table);
-    a.table = g_table;
+                       s.offsets, s.lengths, s.base, s.count, a.per_wave, a.rem, runs, t.first);
+    a.table = t.first;
+    hipLaunchKernelGGL((rvstream_kernel<U, OP>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0, stream, a);
+    return hipGetLastError();
   }
   hipLaunchKernelGGL((rvstream_kernel<U, OP>), dim3(static_cast<uint32_t>(blocks)), dim3(kBlock), 0, stream, a);
   return hipGetLastError();
