@@ -36,6 +36,11 @@ namespace api {
 int hip_status(hipError_t e) { return e == hipSuccess ? TCPCK_OK : TCPCK_EHIP - static_cast<int>(e); }
 
 DeviceGuard::DeviceGuard(int device) {
+  // A stale error left in the thread's last-error slot by an earlier failed
+  // HIP call -- the caller's, or e.g. tcpck_device_supported(-1) -- would be
+  // read back by the launchers' hipGetLastError() as this call's launch
+  // status (found by tests/cpp/abi_host_test.cc): clear it first.
+  (void)hipGetLastError();
   if (hipGetDevice(&prev_) != hipSuccess) prev_ = -1;
   if (prev_ != device) ok_ = hipSetDevice(device);
 }
@@ -1251,7 +1256,10 @@ const char *tcpck_strerror(int status) {
 
 int tcpck_device_supported(int device) {
   hipDeviceProp_t prop;
-  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return 0;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) {
+    (void)hipGetLastError();  // no stale error for the caller's next HIP call
+    return 0;
+  }
   return std::strncmp(prop.gcnArchName, "gfx950", 6) == 0 ? 1 : 0;
 }
 
@@ -1259,7 +1267,10 @@ int tcpck_ctx_create(int device, tcpck_ctx **out) {
   if (!out) return TCPCK_EINVAL;
   *out = nullptr;
   int n = 0;
-  if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return TCPCK_ENODEV;
+  if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) {
+    (void)hipGetLastError();
+    return TCPCK_ENODEV;
+  }
   if (!tcpck_device_supported(device)) return TCPCK_ENODEV;  // gfx950 code object only
   auto *ctx = new (std::nothrow) tcpck_ctx;
   if (!ctx) return TCPCK_ENOMEM;

@@ -229,3 +229,24 @@ def test_receive_rejected_kernel_leaves_headers(built_lib):
         assert not bool((hdr == 0xA5).all().item())
     finally:
         c.close()
+
+
+def test_stale_hip_error_does_not_fail_a_launch(built_lib, oracle_c):
+    """A failed HIP call earlier in the thread (here the library's own
+    tcpck_device_supported(-1): hipGetDeviceProperties on a bad ordinal) left
+    its error in the last-error slot, and the next batch call's launch check
+    read it back as its own failure (found by tests/cpp/abi_host_test.cc under
+    ASan).  Every device entry point now clears it first."""
+    import tcpck
+    L = tcpck.lib()
+    c = tcpck.Context(0)
+    try:
+        assert L.tcpck_device_supported(-1) == 0
+        assert L.tcpck_device_supported(1 << 20) == 0
+        count = 4096
+        a, want, offs = _c2(count, 970, oracle_c)
+        out = torch.empty(count, dtype=torch.int16, device="cuda")
+        c.batch_fixed(tcpck.OP_FILL, a, 1492, 1492, count, out)
+        np.testing.assert_array_equal(host(a), want)
+    finally:
+        c.close()
