@@ -87,6 +87,7 @@ int launch(void *d_arena, const uint64_t *d_off, const uint32_t *d_len, uint64_t
   const uint64_t gy = count < 65535 ? count : 65535;
   const uint64_t gz = (count + gy - 1) / gy;
   if (gz > 65535) return TCPCK_EINVAL;
+  (void)hipGetLastError();  // a stale error from an earlier failed call is not this launch's
   hipLaunchKernelGGL(synth_kernel, dim3(gx, static_cast<uint32_t>(gy), static_cast<uint32_t>(gz)),
                      dim3(threads), 0, static_cast<hipStream_t>(stream),
                      static_cast<uint8_t *>(d_arena), d_off, d_len, stride, flen, count, seed, first,
