@@ -165,24 +165,41 @@ def init_group(backend: str, device=None) -> None:
         dist.init_process_group(backend, timeout=timeout)
 
 
-def device_identity(dev_index: int) -> tuple[str, int]:
-    """(PCI address "dddd:bb:dd", the same as an integer) of the HIP device
-    this rank runs on: ranks on distinct GPUs have distinct addresses."""
+def device_identity(dev_index: int) -> tuple[int, int]:
+    """(PCI address as dom << 16 | bus << 8 | device, a 48-bit identity code)
+    of the HIP device this rank runs on.  The code hashes the PCI address and
+    the device UUID, so ranks on distinct GPUs get distinct codes; 0 when the
+    runtime reports neither (then nothing can be concluded)."""
+    import hashlib
     import torch
     p = torch.cuda.get_device_properties(dev_index)
     dom, bus, dv = int(p.pci_domain_id), int(p.pci_bus_id), int(p.pci_device_id)
-    return f"{dom:04x}:{bus:02x}:{dv:02x}", (dom << 16) | (bus << 8) | dv
+    try:
+        uuid = str(p.uuid).strip()
+    except Exception:  # noqa: BLE001 -- an optional field
+        uuid = ""
+    pci = (dom << 16) | (bus << 8) | dv
+    if pci == 0 and uuid.strip("0-") in ("", "GPU"):
+        return pci, 0
+    code = int.from_bytes(hashlib.sha256(f"{pci:x}|{uuid}".encode()).digest()[:6], "big") or 1
+    return pci, code
 
 
 def check_devices(world: int, dev_index: int, coll_dev, rehearsal: bool) -> dict:
-    """Every rank's PCI address, gathered.  With fewer distinct devices than
-    ranks the line would read as an N-GPU result it is not: an error (exit 3 on
-    every rank, all of them see the same list), or -- under the one-GPU
-    rehearsal knob TCPCK_BENCH_DEVICE -- a line marked as a rehearsal."""
+    """Every rank's device identity, gathered.  With fewer distinct devices
+    than ranks the line would read as an N-GPU result it is not: an error (exit
+    3 on every rank -- all of them see the same list), or, under the one-GPU
+    rehearsal knob TCPCK_BENCH_DEVICE, a line marked as a rehearsal.  A rank
+    whose runtime reports no identity makes the count unknown (null), never an
+    error."""
     from tcpck.shard import gather_ranks
-    name, code = device_identity(dev_index)
+    pci, code = device_identity(dev_index)
+    pcis = [int(x) for x in gather_ranks(float(pci), device=coll_dev)]
     codes = [int(x) for x in gather_ranks(float(code), device=coll_dev)]
-    names = [f"{c >> 16:04x}:{(c >> 8) & 0xFF:02x}:{c & 0xFF:02x}" for c in codes]
+    names = [f"{c >> 16:04x}:{(c >> 8) & 0xFF:02x}:{c & 0xFF:02x}" for c in pcis]
+    if 0 in codes:
+        log(f"warning: the runtime reports no device identity on some rank ({names}): devices unknown")
+        return {"devices": None, "device_ids": names, "rehearsal": rehearsal}
     distinct = len(set(codes))
     if distinct < world:
         if not rehearsal:

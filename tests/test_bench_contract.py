@@ -109,23 +109,31 @@ def test_failing_rank_fails_the_job():
 
 def test_device_check(monkeypatch):
     """The line proves its ranks sat on distinct devices:
-    check_devices gathers every rank's PCI address; fewer distinct devices than
-    ranks exits 3, unless the one-GPU rehearsal knob is set (then the line is
-    marked a rehearsal)."""
+    check_devices gathers every rank's device identity (PCI address + UUID);
+    fewer distinct devices than ranks exits 3, unless the one-GPU rehearsal
+    knob is set (then the line is marked a rehearsal); a rank whose runtime
+    reports no identity makes the count unknown, never an error."""
     import pytest
     from tcpck import shard
-    for codes, rehearsal, want in (([0x10300, 0x10400], False, 2), ([0x10300, 0x10300], True, 1),
-                                   ([0x10300, 0x10300], False, None)):
-        monkeypatch.setattr(bench, "device_identity", lambda i, c=codes: ("x", c[0]))
-        monkeypatch.setattr(shard, "gather_ranks", lambda v, device=None, c=codes: [float(x) for x in c])
-        if want is None:
+    cases = (([(0x10300, 11), (0x10400, 12)], False, 2), ([(0x10300, 11), (0x10300, 11)], True, 1),
+             ([(0x10300, 11), (0x10300, 11)], False, "exit"), ([(0, 0), (0, 0)], False, None))
+    for ranks, rehearsal, want in cases:
+        calls = []
+
+        def gather(v, device=None, ranks=ranks, calls=calls):
+            calls.append(v)  # first the PCI addresses, then the identity codes
+            return [float(r[(len(calls) - 1) % 2]) for r in ranks]
+        monkeypatch.setattr(bench, "device_identity", lambda i, r=ranks: r[0])
+        monkeypatch.setattr(shard, "gather_ranks", gather)
+        if want == "exit":
             with pytest.raises(SystemExit) as e:
                 bench.check_devices(2, 0, "cpu", rehearsal)
             assert e.value.code == 3
-        else:
-            d = bench.check_devices(2, 0, "cpu", rehearsal)
-            assert d["devices"] == want and d["rehearsal"] == (want < 2)
-            assert d["device_ids"][0] == "0001:03:00"
+            continue
+        d = bench.check_devices(2, 0, "cpu", rehearsal)
+        assert d["devices"] == want
+        if want is not None:
+            assert d["rehearsal"] == (want < 2) and d["device_ids"][0] == "0001:03:00"
 
 
 def test_init_group_timeout(monkeypatch):
