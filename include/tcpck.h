@@ -111,7 +111,8 @@ int tcpck_device_supported(int device);
  * (on the caller's stream, asynchronously) for its previous user's work.  On a
  * stream under capture (HIP graphs), or when the slots cannot be allocated,
  * such a FILL runs AUTO's in-stream form instead (same bytes, no slot, no
- * event).  Context creation allocates nothing on the device. */
+ * event); a refused allocation is tried again 64 out-less FILLs later.
+ * Context creation allocates nothing on the device. */
 int tcpck_ctx_create(int device, tcpck_ctx **out);
 int tcpck_ctx_destroy(tcpck_ctx *ctx);
 int tcpck_ctx_device(const tcpck_ctx *ctx);
