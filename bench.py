@@ -178,11 +178,30 @@ def device_identity(dev_index: int) -> tuple[int, int]:
         uuid = str(p.uuid).strip()
     except Exception:  # noqa: BLE001 -- an optional field
         uuid = ""
+    bus_id = hip_pci_bus_id(dev_index)  # "dddd:bb:dd.f": the function too (partitioned GPUs)
     pci = (dom << 16) | (bus << 8) | dv
-    if pci == 0 and uuid.strip("0-") in ("", "GPU"):
+    if pci == 0 and uuid.strip("0-") in ("", "GPU") and not bus_id:
         return pci, 0
-    code = int.from_bytes(hashlib.sha256(f"{pci:x}|{uuid}".encode()).digest()[:6], "big") or 1
+    code = int.from_bytes(hashlib.sha256(f"{pci:x}|{uuid}|{bus_id}".encode()).digest()[:6], "big") or 1
     return pci, code
+
+
+def hip_pci_bus_id(dev_index: int) -> str:
+    """hipDeviceGetPCIBusId of the HIP runtime this process already loaded
+    (found in /proc/self/maps, never a second copy), or "" if unavailable."""
+    import ctypes
+    try:
+        with open("/proc/self/maps") as f:
+            paths = {ln.split()[-1] for ln in f if "libamdhip64.so" in ln}
+        if len(paths) != 1:
+            return ""
+        hip = ctypes.CDLL(paths.pop())
+        buf = ctypes.create_string_buffer(64)
+        if hip.hipDeviceGetPCIBusId(buf, 64, int(dev_index)) != 0:
+            return ""
+        return buf.value.decode(errors="replace")
+    except Exception:  # noqa: BLE001 -- identity is best effort
+        return ""
 
 
 def check_devices(world: int, dev_index: int, coll_dev, rehearsal: bool) -> dict:
