@@ -5,6 +5,8 @@ and the extras keep the order that made each match its own process
 import os
 import sys
 
+import pytest
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
@@ -77,6 +79,19 @@ def test_bare_gpus_n_spawns_n_ranks():
     assert r.returncode == 0, r.stderr[-2000:]
     line = json.loads(r.stdout.strip().splitlines()[-1])
     assert line == {"n_gpus": 2, "gpus_arg": 2, "ranks": [[0, 0], [1, 1]]}
+
+
+@pytest.mark.parametrize("n", [4, 8])
+def test_bare_gpus_4_and_8_spawn_their_ranks(n):
+    """The driver's SCALE runs (N = 4, 8) through the same bare launch: N ranks,
+    local ranks 0..N-1 (one device each on an 8-GPU node), over gloo on CPU."""
+    import json
+    import subprocess
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--launch-check"],
+                       capture_output=True, text=True, timeout=400, env=_env_without_launcher(), cwd="/tmp")
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line == {"n_gpus": n, "gpus_arg": n, "ranks": [[i, i] for i in range(n)]}
 
 
 def test_launcher_world_mismatch_fails():
