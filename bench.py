@@ -47,6 +47,11 @@ ONE JSON line with the driver's fields plus:
   e2e           host-memory rate incl. pinned hipMemcpyAsync H2D + D2H (not `value`)
   settle        untimed launches run before the W warm-up steps until --settle-ms
                 has passed (the idle GPU's clock ramp, scripts/transient.py)
+  devices       distinct GPUs the ranks ran on (a hash of each rank's PCI
+                address, UUID and HIP bus id, gathered): fewer than the ranks
+                exits 3, unless the one-GPU rehearsal knob TCPCK_BENCH_DEVICE
+                is set, which marks the line `rehearsal`; every process group
+                times out after 300 s (TCPCK_BENCH_PG_TIMEOUT)
 """
 from __future__ import annotations
 
