@@ -64,33 +64,9 @@ bool valid_op_mode(int op, int mode) {
 bool valid_device_op_mode(int op, int mode) { return valid_op_mode(op == TCPCK_OP_RECEIVE ? TCPCK_OP_VERIFY : op, mode); }
 
 // ---- host single-image path (product code, not the oracle) ---------------
-// SWAR over 8-byte words: the two u16 halves of each 32-bit lane are split
-// into 0x0000FFFF0000FFFF lanes and summed in u64; 2^14 iterations cannot
-// overflow a 32-bit lane (2^14 * 2 * 0xFFFF < 2^32), so lanes are folded every
-// 2^14 words into an exact u64 total.  Returns the exact sum of the LE u16
-// words (REF needs it mod 2^16, RFC 1071 mod 0xFFFF with zero-ness).
-uint64_t host_word_sum(const uint8_t *p, size_t n) {
-  constexpr uint64_t kLo = 0x0000FFFF0000FFFFull;
-  uint64_t total = 0;
-  size_t i = 0;
-  while (n - i >= 8) {
-    uint64_t a = 0;
-    const size_t stop = i + std::min<size_t>((n - i) & ~size_t{7}, size_t{8} << 14);
-    for (; i < stop; i += 8) {
-      uint64_t x;
-      std::memcpy(&x, p + i, 8);
-      a += (x & kLo) + ((x >> 16) & kLo);
-    }
-    total += (a & 0xFFFFFFFFull) + (a >> 32);
-  }
-  for (; i + 1 < n; i += 2) {
-    uint16_t w;
-    std::memcpy(&w, p + i, 2);
-    total += w;
-  }
-  return total;
-}
-
+// The exact sum of the image's LE u16 words is tcpck::host::word_sum
+// (tcpck_host.cc: AVX2 where the CPU has it, else SWAR); REF needs it mod
+// 2^16, RFC 1071 mod 0xFFFF with zero-ness.
 uint16_t finish_host(uint64_t total, int mode) {
   if (mode == TCPCK_MODE_REF) return static_cast<uint16_t>(~total);  // tcp-header.h:262
   while (total >> 16) total = (total & 0xFFFF) + (total >> 16);
@@ -1307,7 +1283,7 @@ int tcpck_checksum16(const void *image, size_t len, int mode, uint16_t *out) {
   if ((!image && len) || !out || (len & 1) ||
       (mode != TCPCK_MODE_REF && mode != TCPCK_MODE_RFC1071))
     return TCPCK_EINVAL;
-  *out = finish_host(host_word_sum(static_cast<const uint8_t *>(image), len), mode);
+  *out = finish_host(tcpck::host::word_sum(static_cast<const uint8_t *>(image), len), mode);
   return TCPCK_OK;
 }
 

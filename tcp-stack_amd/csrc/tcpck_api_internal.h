@@ -11,6 +11,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cstddef>
 #include <cstdint>
 #include <mutex>
 
@@ -82,6 +83,12 @@ struct tcpck_ctx {
 };
 
 namespace tcpck {
+namespace host {
+// The exact sum of the little-endian u16 words of p[0, n) (n even), host code
+// (tcpck_host.cc); tcpck_checksum16 finishes it.
+uint64_t word_sum(const uint8_t *p, size_t n);
+}  // namespace host
+
 namespace api {
 
 constexpr uint64_t kScratchImages = 8ull << 20;  // 16 MiB of u16 results: C5's 8M images in one chunk
