@@ -22,8 +22,9 @@
  * end-around carry).  Odd sizes read out of bounds in the reference, so no
  * parity exists for them; the oracle reports them as an error (-1) from the
  * checked entry points.  The RFC 1071 variant (opt-in mode 1 of the product)
- * is restated here too, as its own oracle; it has no reference to pin it
- * ("parity unpinned" for mode 1).
+ * is restated here too, as its own oracle; the reference does not compute
+ * it, so it is pinned instead by RFC 1071 section 3's worked example
+ * (00 01 f2 03 f4 f5 f6 f7 -> 0x0d22 here; tests/test_oracle.py).
  */
 #include <stddef.h>
 #include <stdint.h>
