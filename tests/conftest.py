@@ -185,8 +185,11 @@ def _variant_kernel(item):
 def pytest_collection_modifyitems(config, items):
     """Measurement-only variants (libtcpck_probe.so) keep ONE representative
     case per test function -- the middle one of their matrix; AUTO's variants
-    (libtcpck.so) keep every case."""
+    (libtcpck.so) keep every case.  TCPCK_ALL_VARIANTS=1 keeps every case of
+    every variant (a full sweep of the probe library)."""
     import tcpck
+    if os.environ.get("TCPCK_ALL_VARIANTS") == "1":
+        return
     groups, keep, drop = {}, [], []
     for it in items:
         kv = _variant_kernel(it)
